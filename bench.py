@@ -1,0 +1,205 @@
+#!/usr/bin/env python
+"""Headline benchmark: VGG-11 training throughput (images/sec, whole node) on CIFAR-shaped data.
+
+Metric/config from BASELINE.json: "images/sec (whole node) VGG-11 CIFAR-shaped at 1/2/4/8 MI355X".
+One step = the reference's full training iteration (``/root/reference/src/Part 3/main.py:88-97``):
+batch fetch + RandomCrop/Flip/Normalize (on-GPU kernel), zero_grad, forward, CrossEntropy, backward
+with the bucketed RCCL all-reduce overlapped (DDP wrapper when N > 1), SGD(momentum 0.9,
+wd 1e-4) step. fp32 end to end (the reference's precision), random-init weights, synthetic uint8
+CIFAR-10-shaped images resident on the GPU. Weak scaling by default: 256 images per GPU per step
+(the reference's per-process batch); ``--scaling strong`` keeps the reference's global 256.
+
+Usage:  python bench.py [--gpus N --steps K --warmup W]
+        (N > 1 is launched by the driver with torch.distributed.run, one rank per GPU)
+Prints ONE JSON line on rank 0.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+BASELINE_IMG_S = 322.9  # reference Part 1, single process, B=256 (measured, CPU)
+METRIC = "images/sec (whole node) VGG-11 CIFAR-shaped at 1/2/4/8 MI355X; scaling eff"
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=50)
+    p.add_argument("--warmup", type=int, default=10)
+    p.add_argument("--model", default="vgg11")
+    p.add_argument("--local-batch", type=int, default=256)
+    p.add_argument("--scaling", default="weak", choices=["weak", "strong"])
+    p.add_argument("--strategy", default="ddp", choices=["ddp", "bucketed_overlap", "allreduce_blocking",
+                                                          "gather_scatter"])
+    p.add_argument("--no-graph", action="store_true", help="eager steps instead of one hipGraph replay per step")
+    p.add_argument("--backend", default="native", choices=["native", "torch"],
+                   help="torch = stock PyTorch-ROCm ops + torch DDP (comparison only)")
+    p.add_argument("--bucket-cap-mb", type=float, default=None)
+    p.add_argument("--dataset-size", type=int, default=50000)
+    return p.parse_args()
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        print(f"[bench] note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
+
+    import cs744_distributed_data_parallel_amd as cdp
+    from cs744_distributed_data_parallel_amd import distributed as dist
+    from cs744_distributed_data_parallel_amd.data import DistributedSampler, DeviceLoader, synthetic_cifar10
+
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("rccl" if args.backend == "native" else "nccl", rank=rank, world_size=world)
+    if args.backend == "native":
+        cdp._native.lib()  # fail loudly if the HIP extension is missing
+
+    local_batch = args.local_batch if args.scaling == "weak" else max(1, 256 // world)
+    global_batch = local_batch * world
+    cdp.utils.seed_everything(0)
+
+    ds = synthetic_cifar10(args.dataset_size, seed=0, device=dev)
+    sampler = DistributedSampler(ds, num_replicas=world, rank=rank) if world > 1 else None
+    loader = DeviceLoader(ds, local_batch, sampler=sampler, shuffle=(world == 1), train=True)
+
+    if args.backend == "native":
+        model = cdp.get_model(args.model).to(dev)
+        if world > 1 and args.strategy == "ddp":
+            model = cdp.DistributedDataParallel(model, bucket_cap_mb=args.bucket_cap_mb)
+        sync = None
+        if world > 1 and args.strategy == "bucketed_overlap":
+            sync = cdp.parallel.BucketedOverlap(model, bucket_cap_mb=args.bucket_cap_mb)
+        opt = cdp.SGD(model.parameters(), lr=0.1, momentum=0.9, weight_decay=1e-4)
+        crit = cdp.CrossEntropyLoss()
+    else:
+        os.environ["CDP_FORCE_REFERENCE"] = "1"
+        model = cdp.get_model(args.model).to(dev).to(memory_format=torch.channels_last)
+        sync = None
+        if world > 1:
+            model = torch.nn.parallel.DistributedDataParallel(model, device_ids=[local])
+        opt = torch.optim.SGD(model.parameters(), lr=0.1, momentum=0.9, weight_decay=1e-4)
+        crit = torch.nn.CrossEntropyLoss()
+
+    order = loader._order()
+    nb = max(1, order.numel() // local_batch)
+    static_idx = torch.empty(local_batch, dtype=torch.int64, device=dev)
+
+    def step(i):
+        s = (i % nb) * local_batch
+        static_idx.copy_(order[s:s + local_batch], non_blocking=True)
+        return i
+
+    def body():
+        x, y = loader.batch(static_idx, 0, local_batch)
+        opt.zero_grad()
+        out = model(x)
+        if sync is not None:
+            sync.prepare(out)
+        loss = crit(out, y)
+        loss.backward()
+        if world > 1 and args.strategy == "allreduce_blocking":
+            cdp.parallel.average_gradients_allreduce(model)
+        elif world > 1 and args.strategy == "gather_scatter":
+            cdp.parallel.average_gradients_gather_scatter(model)
+        opt.step()
+        return loss
+
+    # warmup (eager; includes bucket rebuild in ready order after iteration 1)
+    n_eager_warm = max(3, args.warmup)
+    for i in range(n_eager_warm):
+        step(i)
+        loss = body()
+    torch.cuda.synchronize()
+
+    graph = None
+    use_graph = not args.no_graph and args.strategy in ("ddp", "bucketed_overlap")
+    if use_graph:
+        try:
+            s = torch.cuda.Stream()
+            s.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(s):
+                for _ in range(2):
+                    body()
+            torch.cuda.current_stream().wait_stream(s)
+            torch.cuda.synchronize()
+            graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(graph):
+                static_loss = body()
+            torch.cuda.synchronize()
+            for i in range(2):  # warm replays
+                step(i)
+                graph.replay()
+            torch.cuda.synchronize()
+        except Exception as e:  # pragma: no cover - depends on the runtime
+            print(f"[bench] hipGraph capture failed ({e!r}); timing eager steps", file=sys.stderr)
+            graph = None
+            torch.cuda.synchronize()
+
+    def run_one(i):
+        step(i)
+        if graph is not None:
+            graph.replay()
+        else:
+            body()
+
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        run_one(i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    el_t = torch.tensor([el], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(el_t, "max")
+    el = float(el_t.item())
+    ms = el / args.steps * 1e3
+    img_s = global_batch * args.steps / el
+    if rank == 0:
+        rec = {
+            "metric": METRIC,
+            "value": round(img_s, 1),
+            "unit": "images/sec",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms, 4),
+            "higher_is_better": True,
+            "scaling": args.scaling,
+            "vs_baseline": round(img_s / BASELINE_IMG_S, 2),
+            "dtype": "fp32",
+            "data": "synthetic (random uint8 CIFAR-10-shaped 32x32x3, GPU-resident, on-GPU crop/flip/normalize); "
+                    "random-init weights",
+            "config": {
+                "model": "VGG-11" if args.model == "vgg11" else args.model,
+                "global_batch": global_batch,
+                "local_batch": local_batch,
+                "seq_len": None,
+                "image_shape": [3, 32, 32],
+                "parallelism": f"dp{world}",
+                "strategy": args.strategy if world > 1 else "single",
+                "backend": args.backend,
+                "hipgraph": graph is not None,
+                "optimizer": "SGD(lr=0.1, momentum=0.9, wd=1e-4)",
+            },
+        }
+        print(json.dumps(rec), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,203 @@
+"""Autograd-visible fused ops backed by the gfx950 kernels.
+
+Each public function takes the same modules / tensors as its ``torch.nn`` counterpart and is
+numerically the same op; GPU tensors run the native HIP kernels (no silent fallback: a missing
+extension raises), CPU tensors run the PyTorch reference composition (used by the CPU tests and
+as the parity oracle).
+
+Reference anchors: the VGG block ``Conv2d -> BatchNorm2d -> ReLU [-> MaxPool2d]`` of
+``/root/reference/src/Part 1/model.py:11-27``; ``fc1`` (``:40,45``); ``CrossEntropyLoss``
+(``/root/reference/src/Part 1/main.py:110``).
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn.functional as F
+
+from .. import _native
+
+__all__ = [
+    "conv_bn_act",
+    "linear",
+    "cross_entropy",
+    "max_pool2d",
+    "global_avg_pool",
+    "use_native",
+]
+
+
+def use_native(*tensors) -> bool:
+    if _native.force_reference():
+        return False
+    return _native.require(*tensors)
+
+
+def _bn_momentum(bn) -> float:
+    return -1.0 if bn.momentum is None else float(bn.momentum)
+
+
+# --------------------------------------------------------------------------- conv + BN + act
+class _ConvBNAct(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, b, gamma, beta, rm, rv, nbt, momentum, eps, training, stride, pad, pool, relu, residual):
+        C = _native.lib()
+        out, y, stats = C.conv_bn_act_fwd(
+            x, w, b, gamma, beta, rm, rv, nbt, momentum, eps, training, stride, pad, pool, relu, residual
+        )
+        ctx.cfg = (stride, pad, pool, relu, training, b is not None, residual is not None)
+        zout = out if residual is not None else None
+        ctx.save_for_backward(x, w, y, stats, zout)
+        return out
+
+    @staticmethod
+    def backward(ctx, gout):
+        x, w, y, stats, zout = ctx.saved_tensors
+        stride, pad, pool, relu, training, has_bias, has_res = ctx.cfg
+        C = _native.lib()
+        dx, dw, db, dgamma, dbeta, dres = C.conv_bn_act_bwd(
+            gout, x, w, y, stats, stride, pad, pool, relu, ctx.needs_input_grad[0], has_bias, zout, training
+        )
+        return (
+            dx if ctx.needs_input_grad[0] else None,
+            dw,
+            db if has_bias else None,
+            dgamma if ctx.needs_input_grad[3] else None,
+            dbeta if ctx.needs_input_grad[4] else None,
+            None, None, None, None, None, None, None, None, None, None,
+            dres if has_res else None,
+        )
+
+
+def conv_bn_act(x, conv, bn, relu: bool = True, pool: bool = False, residual=None):
+    """``[maxpool2x2](act(bn(conv(x)) [+ residual]))`` for an ``nn.Conv2d`` / ``nn.BatchNorm2d`` pair.
+
+    ``pool`` is the reference's ``MaxPool2d(kernel_size=2, stride=2)``; ``relu`` its
+    ``ReLU(inplace=True)``; ``residual`` (ResNet) is added after BN and before the activation.
+    """
+    stride = conv.stride[0]
+    pad = conv.padding[0]
+    if use_native(x):
+        training = bn.training or not bn.track_running_stats
+        track = bn.track_running_stats and bn.training
+        return _ConvBNAct.apply(
+            x,
+            conv.weight,
+            conv.bias,
+            bn.weight,
+            bn.bias,
+            bn.running_mean if (track or not training) else None,
+            bn.running_var if (track or not training) else None,
+            bn.num_batches_tracked if track else None,
+            _bn_momentum(bn),
+            float(bn.eps),
+            training,
+            stride,
+            pad,
+            pool,
+            relu,
+            residual,
+        )
+    y = F.conv2d(x, conv.weight, conv.bias, conv.stride, conv.padding)
+    y = bn(y)
+    if residual is not None:
+        y = y + residual
+    if relu:
+        y = F.relu(y)
+    if pool:
+        y = F.max_pool2d(y, 2, 2)
+    return y
+
+
+# --------------------------------------------------------------------------- linear
+class _Linear(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, b):
+        ctx.save_for_backward(x, w)
+        ctx.has_bias = b is not None
+        return _native.lib().linear_fwd(x, w, b)
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, w = ctx.saved_tensors
+        dx, dw, db = _native.lib().linear_bwd(gy, x, w, ctx.needs_input_grad[0], ctx.has_bias)
+        return (dx if ctx.needs_input_grad[0] else None), dw, (db if ctx.has_bias else None)
+
+
+def linear(x, weight, bias=None):
+    if use_native(x) and x.dim() == 2:
+        return _Linear.apply(x, weight, bias)
+    return F.linear(x, weight, bias)
+
+
+# --------------------------------------------------------------------------- cross entropy
+class _XEnt(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, logits, target):
+        ctx.save_for_backward(logits, target)
+        return _native.lib().xent_fwd(logits, target)
+
+    @staticmethod
+    def backward(ctx, g):
+        logits, target = ctx.saved_tensors
+        return _native.lib().xent_bwd(g.reshape(1), logits, target), None
+
+
+def cross_entropy(logits, target):
+    """Mean-reduced softmax cross-entropy (``torch.nn.CrossEntropyLoss()`` defaults)."""
+    if use_native(logits) and logits.dim() == 2 and logits.dtype == torch.float32:
+        return _XEnt.apply(logits, target)
+    return F.cross_entropy(logits, target)
+
+
+def count_correct(logits, target, out=None):
+    """Top-1 correct count (``output.max(1)`` + ``eq`` + ``sum``) as an int64 device tensor."""
+    if use_native(logits):
+        if out is None:
+            out = torch.zeros(1, dtype=torch.long, device=logits.device)
+        _native.lib().xent_fwd(logits.detach().float().contiguous(), target, out)
+        return out
+    c = logits.max(1)[1].eq(target).sum().reshape(1)
+    if out is None:
+        return c
+    out += c
+    return out
+
+
+# --------------------------------------------------------------------------- pooling
+class _MaxPool(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, k, s, p):
+        y, arg = _native.lib().maxpool2d_fwd(x, k, s, p)
+        ctx.save_for_backward(arg)
+        ctx.in_shape = list(x.shape)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        (arg,) = ctx.saved_tensors
+        return _native.lib().maxpool2d_bwd(gy, arg, ctx.in_shape), None, None, None
+
+
+def max_pool2d(x, kernel_size, stride=None, padding=0):
+    stride = kernel_size if stride is None else stride
+    if use_native(x):
+        return _MaxPool.apply(x, int(kernel_size), int(stride), int(padding))
+    return F.max_pool2d(x, kernel_size, stride, padding)
+
+
+class _AvgPool(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        ctx.in_shape = list(x.shape)
+        return _native.lib().avgpool_fwd(x)
+
+    @staticmethod
+    def backward(ctx, gy):
+        return _native.lib().avgpool_bwd(gy, ctx.in_shape)
+
+
+def global_avg_pool(x):
+    """``AdaptiveAvgPool2d(1)`` + ``flatten(1)`` -> [N, C]."""
+    if use_native(x):
+        return _AvgPool.apply(x)
+    return torch.flatten(F.adaptive_avg_pool2d(x, 1), 1)

@@ -1,0 +1,191 @@
+"""Fused SGD (momentum, dampening, weight decay, Nesterov, maximize) over flat arenas.
+
+Drop-in for ``torch.optim.SGD`` as used by every reference stage
+(``optim.SGD(model.parameters(), lr=0.1, momentum=0.9, weight_decay=0.0001)``,
+``/root/reference/src/Part 1/main.py:114-115``): it *is* a ``torch.optim.Optimizer`` subclass, so
+``param_groups``, ``state_dict()`` / ``load_state_dict()`` (``momentum_buffer`` per parameter) and
+LR schedulers behave exactly like torch's.
+
+MI355X path: parameters, gradients and momentum live in :class:`~.utils.arena.FlatArena` storages,
+so a param group whose parameters form one contiguous arena run is updated by ONE vectorised HIP
+kernel (float4, fma order matching ATen's ``add(alpha=...)``) instead of one launch per tensor.
+``zero_grad`` zeroes the gradient arena in place (the arena views stay attached, which keeps the
+bucketed reducer zero-copy). The learning rate can live on the device (``lr_tensor``) so a captured
+hipGraph step follows an LR schedule without re-capture.
+"""
+from __future__ import annotations
+
+import torch
+from torch.optim import Optimizer
+
+from . import _native
+from .utils.arena import arena_for
+
+
+class SGD(Optimizer):
+    def __init__(
+        self,
+        params,
+        lr: float = 1e-3,
+        momentum: float = 0.0,
+        dampening: float = 0.0,
+        weight_decay: float = 0.0,
+        nesterov: bool = False,
+        *,
+        maximize: bool = False,
+        flat: bool = True,
+    ):
+        if lr < 0.0:
+            raise ValueError(f"Invalid learning rate: {lr}")
+        if momentum < 0.0:
+            raise ValueError(f"Invalid momentum value: {momentum}")
+        if weight_decay < 0.0:
+            raise ValueError(f"Invalid weight_decay value: {weight_decay}")
+        if nesterov and (momentum <= 0 or dampening != 0):
+            raise ValueError("Nesterov momentum requires a momentum and zero dampening")
+        defaults = dict(
+            lr=lr, momentum=momentum, dampening=dampening, weight_decay=weight_decay, nesterov=nesterov,
+            maximize=maximize, foreach=None, differentiable=False, fused=None,
+        )
+        super().__init__(params, defaults)
+        self._flat = flat
+        self._arena = None
+        self._lr_tensor = None
+        self._steps = 0
+        all_params = [p for g in self.param_groups for p in g["params"]]
+        if flat and all_params and all_params[0].is_cuda:
+            self._arena = arena_for(all_params)
+            self._arena.on_relayout(self._on_relayout)
+
+    def _on_relayout(self, arena):
+        # the arena moved the momentum values with their parameters; re-point the state views
+        if arena.momentum is None:
+            return
+        views = arena.momentum_views()
+        for p in arena.params:
+            st = self.state.get(p)
+            if st and st.get("momentum_buffer") is not None:
+                st["momentum_buffer"] = views[p._cdp_index]
+
+    # ------------------------------------------------------------------ device-side LR
+    def lr_tensor(self) -> torch.Tensor:
+        """A 1-element device tensor holding the LR of param group 0 (graph-capture friendly)."""
+        if self._lr_tensor is None:
+            dev = self.param_groups[0]["params"][0].device
+            self._lr_tensor = torch.tensor([self.param_groups[0]["lr"]], dtype=torch.float32, device=dev)
+        return self._lr_tensor
+
+    def sync_lr_tensor(self):
+        if self._lr_tensor is not None:
+            self._lr_tensor.fill_(self.param_groups[0]["lr"])
+
+    # ------------------------------------------------------------------ zero_grad
+    def zero_grad(self, set_to_none: bool = True):
+        if self._arena is not None and self._arena.grad is not None:
+            # in-place: keeps p.grad as arena views (zero-copy bucketed all-reduce)
+            self._arena.zero_grad()
+            return
+        super().zero_grad(set_to_none=set_to_none)
+
+    # ------------------------------------------------------------------ step
+    @torch.no_grad()
+    def step(self, closure=None):
+        loss = None
+        if closure is not None:
+            with torch.enable_grad():
+                loss = closure()
+        for gi, group in enumerate(self.param_groups):
+            params = [p for p in group["params"] if p.grad is not None]
+            if not params:
+                continue
+            if params[0].is_cuda and not _native.force_reference():
+                self._step_native(gi, group, params)
+            else:
+                self._step_reference(group, params)
+        self._steps += 1
+        return loss
+
+    def _first_flags(self, params):
+        firsts = [self.state[p].get("momentum_buffer") is None for p in params]
+        return firsts
+
+    def _step_native(self, gi, group, params):
+        C = _native.lib()
+        lr, m, damp, wd = group["lr"], group["momentum"], group["dampening"], group["weight_decay"]
+        nest, maxim = group["nesterov"], group["maximize"]
+        lr_t = self._lr_tensor if (gi == 0 and self._lr_tensor is not None) else None
+        arena = self._arena
+        rng = None
+        if arena is not None and len(params) == len(group["params"]):
+            rng = arena.contiguous_range(params)
+        if rng is not None and m != 0.0:
+            # momentum buffers must be the arena's views (first step: buf = d_p)
+            firsts = self._first_flags(params)
+            mom = arena.momentum_buffer()
+            mviews = arena.momentum_views()
+            consistent = all(
+                (self.state[p].get("momentum_buffer") is None)
+                or self.state[p]["momentum_buffer"].data_ptr() == mviews[p._cdp_index].data_ptr()
+                for p in params
+            )
+            if not consistent:
+                # e.g. after load_state_dict: move loaded buffers into the arena
+                for p in params:
+                    b = self.state[p].get("momentum_buffer")
+                    if b is not None:
+                        mviews[p._cdp_index].copy_(b)
+                        self.state[p]["momentum_buffer"] = mviews[p._cdp_index]
+                firsts = self._first_flags(params)
+            if all(firsts) or not any(firsts):
+                s, e = rng
+                C.sgd_step(arena.data[s:e], arena.grad[s:e], mom[s:e], lr_t, lr, m, damp, wd, 1.0, nest, all(firsts),
+                           maxim)
+                if all(firsts):
+                    for p in params:
+                        self.state[p]["momentum_buffer"] = mviews[p._cdp_index]
+                return
+        elif rng is not None and m == 0.0:
+            s, e = rng
+            C.sgd_step(arena.data[s:e], arena.grad[s:e], None, lr_t, lr, 0.0, damp, wd, 1.0, nest, True, maxim)
+            return
+        # general path: one launch per parameter (non-arena / partial groups)
+        for p in params:
+            st = self.state[p]
+            buf = st.get("momentum_buffer")
+            first = buf is None
+            if m != 0.0 and first:
+                buf = torch.empty_like(p, memory_format=torch.contiguous_format)
+            pv = p.data if p.data.is_contiguous() else None
+            g = p.grad
+            if pv is None or not g.is_contiguous():
+                # strided (channels_last) tensors: update through flat contiguous copies
+                pc = p.data.contiguous()
+                gc = g.contiguous()
+                bc = buf.contiguous() if buf is not None else None
+                C.sgd_step(pc.view(-1), gc.view(-1), bc.view(-1) if bc is not None else None, lr_t, lr, m, damp, wd,
+                           1.0, nest, first, maxim)
+                p.data.copy_(pc)
+                if buf is not None and bc is not buf:
+                    buf.copy_(bc)
+            else:
+                C.sgd_step(pv.view(-1), g.view(-1), buf.view(-1) if buf is not None else None, lr_t, lr, m, damp,
+                           wd, 1.0, nest, first, maxim)
+            if m != 0.0:
+                st["momentum_buffer"] = buf
+
+    def _step_reference(self, group, params):
+        lr, m, damp, wd = group["lr"], group["momentum"], group["dampening"], group["weight_decay"]
+        for p in params:
+            d_p = p.grad if not group["maximize"] else -p.grad
+            if wd != 0:
+                d_p = d_p.add(p, alpha=wd)
+            if m != 0:
+                st = self.state[p]
+                buf = st.get("momentum_buffer")
+                if buf is None:
+                    buf = torch.clone(d_p).detach()
+                    st["momentum_buffer"] = buf
+                else:
+                    buf.mul_(m).add_(d_p, alpha=1 - damp)
+                d_p = d_p.add(buf, alpha=m) if group["nesterov"] else buf
+            p.add_(d_p, alpha=-lr)

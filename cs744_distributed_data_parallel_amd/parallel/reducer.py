@@ -1,0 +1,275 @@
+"""Bucketed, backward-overlapped gradient averaging (Python orchestration of the native reducer).
+
+:class:`GradReducer` owns the bucket plan over a :class:`~..utils.arena.FlatArena` and drives the
+C++ ``_C.Reducer`` (autograd post-hooks in C++, RCCL launches on the communicator's stream, see
+``csrc/runtime/reducer.cpp``). A pure-Python reducer with identical semantics
+(``register_post_accumulate_grad_hook`` + an engine callback) is used when the extension is not
+built (CPU-only environments); both are exercised by the CPU test-suite with gloo.
+
+Reference: the bucketed all-reduce that ``DDP(model)`` performs inside torch's Reducer
+(``/root/reference/src/Part 3/main.py:61``), and the north-star "Part 2b: backward-hook bucketed
+all-reduce overlapped with autograd" (BASELINE.json).
+"""
+from __future__ import annotations
+
+import threading
+from typing import List, Optional, Sequence, Tuple
+
+import torch
+import torch.distributed as tdist
+
+from .. import _native
+from ..utils.arena import ALIGN, FlatArena
+from .buckets import DEFAULT_BUCKET_CAP_MB, DEFAULT_FIRST_BUCKET_CAP_MB, plan_buckets
+from .comm import Communicator, RcclCommunicator, TorchCommunicator
+
+
+def _aligned(n: int) -> int:
+    return (n + ALIGN - 1) // ALIGN * ALIGN
+
+
+class _PyReducer:
+    """Semantics twin of ``_C.Reducer`` (used when the native extension is unavailable)."""
+
+    def __init__(self, params, grad_views, bucket_views, bucket_starts, comm: Communicator, find_unused, average):
+        self.params, self.grad_views, self.bucket_views = params, grad_views, bucket_views
+        self.comm, self.find_unused, self.average = comm, find_unused, average
+        nb = len(bucket_views)
+        self.bucket_of = [-1] * len(params)
+        self.bucket_size = [0] * nb
+        for b in range(nb):
+            lo, hi = sorted((bucket_starts[b], bucket_starts[b + 1]))
+            for i in range(lo, hi):
+                self.bucket_of[i] = b
+                self.bucket_size[b] += 1
+        self.pending = [0] * nb
+        self.works = [None] * nb
+        self.ready = [False] * len(params)
+        self.armed = False
+        self.next_launch = 0
+        self.callback_queued = False
+        self.order: List[int] = []
+        self.record_order = True
+        self.have_order = False
+        self.iterations = 0
+        self.launched_total = 0
+        self._lock = threading.Lock()
+        self._handles = [p.register_post_accumulate_grad_hook(self._make_hook(i)) for i, p in enumerate(params)]
+
+    @property
+    def num_buckets(self):
+        return len(self.bucket_views)
+
+    def _make_hook(self, i):
+        def hook(p):
+            with self._lock:
+                if self.armed:
+                    self._mark(i, True)
+
+        return hook
+
+    def remove_hooks(self):
+        for h in self._handles:
+            h.remove()
+        self._handles = []
+
+    def disarm(self):
+        self.armed = False
+
+    def prepare_for_backward(self, outputs):
+        with self._lock:
+            if self.armed and self.next_launch != 0:
+                raise RuntimeError(
+                    "Expected to have finished reduction in the prior iteration before starting a new one."
+                )
+            self.pending = list(self.bucket_size)
+            self.ready = [False] * len(self.params)
+            self.works = [None] * len(self.works)
+            self.next_launch = 0
+            self.callback_queued = False
+            self.armed = True
+            if not self.find_unused:
+                return
+            seen = set()
+            stack = [o.grad_fn for o in outputs if isinstance(o, torch.Tensor) and o.grad_fn is not None]
+            while stack:
+                fn = stack.pop()
+                if fn is None or fn in seen:
+                    continue
+                seen.add(fn)
+                for nxt, _ in fn.next_functions:
+                    if nxt is not None:
+                        stack.append(nxt)
+            reached = {id(getattr(fn, "variable", None)) for fn in seen if hasattr(fn, "variable")}
+            for i, p in enumerate(self.params):
+                if id(p) not in reached:
+                    self._mark(i, False)
+
+    def _mark(self, i, from_hook):
+        if self.ready[i]:
+            return
+        self.ready[i] = True
+        p = self.params[i]
+        view = self.grad_views[i]
+        if p.grad is None:
+            view.zero_()
+            p.grad = view
+        elif p.grad.data_ptr() != view.data_ptr():
+            view.copy_(p.grad)
+            p.grad = view
+        if from_hook:
+            if self.record_order:
+                self.order.append(i)
+            if not self.callback_queued:
+                self.callback_queued = True
+                torch.autograd.Variable._execution_engine.queue_callback(self._finalize)
+        b = self.bucket_of[i]
+        self.pending[b] -= 1
+        if self.pending[b] == 0:
+            while self.next_launch < len(self.pending) and self.pending[self.next_launch] == 0:
+                self._launch(self.next_launch)
+                self.next_launch += 1
+
+    def _launch(self, b):
+        self.works[b] = self.comm.all_reduce(self.bucket_views[b], "avg" if self.average else "sum", async_op=True)
+        self.launched_total += 1
+
+    def _finalize(self):
+        with self._lock:
+            if not self.armed:
+                return
+            if self.next_launch < len(self.pending):
+                if self.find_unused:
+                    for i in range(len(self.params)):
+                        self._mark(i, False)
+                else:
+                    missing = [i for i, r in enumerate(self.ready) if not r]
+                    self.armed = False
+                    raise RuntimeError(
+                        f"DistributedDataParallel: parameters with indices {missing} did not receive gradients "
+                        "in this iteration. Enable find_unused_parameters=True."
+                    )
+            for w in self.works:
+                if w is not None:
+                    w.wait()
+            if self.record_order:
+                self.record_order = False
+                self.have_order = True
+            self.iterations += 1
+            self.armed = False
+            self.next_launch = 0
+
+    def ready_order(self):
+        return list(self.order) if self.have_order else []
+
+
+class GradReducer:
+    """Bucket plan + reducer over a flat gradient arena.
+
+    ``launch_order`` lists arena indices in the order gradients are expected to become ready; each
+    bucket is a contiguous arena range in that order.
+    """
+
+    def __init__(
+        self,
+        arena: FlatArena,
+        comm: Communicator,
+        bucket_cap_mb: float = DEFAULT_BUCKET_CAP_MB,
+        first_bucket_cap_mb: float = DEFAULT_FIRST_BUCKET_CAP_MB,
+        find_unused_parameters: bool = False,
+        average: bool = True,
+        arena_in_ready_order: bool = False,
+    ):
+        self.arena, self.comm = arena, comm
+        self.cap, self.first_cap = bucket_cap_mb, first_bucket_cap_mb
+        self.find_unused, self.average = find_unused_parameters, average
+        self.arena_in_ready_order = arena_in_ready_order
+        self._impl = None
+        self._build()
+
+    # ------------------------------------------------------------------ plan
+    def _build(self):
+        a = self.arena
+        n = len(a.params)
+        launch = list(range(n)) if self.arena_in_ready_order else list(range(n - 1, -1, -1))
+        nbytes = [a.numels[i] * a.data.element_size() for i in launch]
+        groups = plan_buckets(nbytes, self.cap, self.first_cap)
+        starts = [launch[0] if self.arena_in_ready_order else n]
+        views = []
+        self.bucket_ranges: List[Tuple[int, int]] = []
+        for g in groups:
+            idx = [launch[j] for j in g]
+            lo, hi = min(idx), max(idx)
+            s = a.offsets[lo]
+            e = a.offsets[hi] + _aligned(a.numels[hi])
+            self.bucket_ranges.append((s, e))
+            views.append(a.grad[s:e])
+            starts.append(hi + 1 if self.arena_in_ready_order else lo)
+        self.bucket_starts = starts
+        grad_views = a.grad_views()
+        if self._impl is not None:
+            self._impl.remove_hooks()
+        use_native = _native.available() and (
+            isinstance(self.comm, RcclCommunicator) or isinstance(self.comm, TorchCommunicator)
+        )
+        if use_native:
+            C = _native.lib()
+            rccl = self.comm.native if isinstance(self.comm, RcclCommunicator) else None
+            pg = None
+            if rccl is None:
+                pg = self.comm.group if self.comm.group is not None else tdist.group.WORLD
+            self._impl = C.Reducer(list(a.params), grad_views, views, starts, rccl, pg, self.find_unused, self.average)
+        else:
+            self._impl = _PyReducer(list(a.params), grad_views, views, starts, self.comm, self.find_unused, self.average)
+
+    @property
+    def native(self) -> bool:
+        return not isinstance(self._impl, _PyReducer)
+
+    @property
+    def num_buckets(self) -> int:
+        return self._impl.num_buckets
+
+    @property
+    def iterations(self) -> int:
+        return self._impl.iterations
+
+    def bucket_sizes_bytes(self) -> List[int]:
+        es = self.arena.data.element_size()
+        return [(e - s) * es for s, e in self.bucket_ranges]
+
+    def prepare_for_backward(self, outputs: Sequence[torch.Tensor]):
+        self._impl.prepare_for_backward(list(outputs))
+
+    def disarm(self):
+        self._impl.disarm()
+
+    def ready_order(self) -> List[int]:
+        return list(self._impl.ready_order())
+
+    def rebuild_in_ready_order(self, order: Optional[Sequence[int]] = None) -> bool:
+        """Relayout the arena in gradient-ready order (rank 0's order, broadcast) and re-bucket."""
+        if order is None:
+            order = self.ready_order()
+        n = len(self.arena.params)
+        order = list(order)
+        # parameters that never fired (unused) go last, in reverse model order
+        seen = set(order)
+        order += [i for i in range(n - 1, -1, -1) if i not in seen]
+        t = torch.tensor(order, dtype=torch.int64)
+        if self.comm.size > 1:
+            t = t.to(self.arena.device)
+            self.comm.broadcast(t, 0)
+            t = t.cpu()
+        order = t.tolist()
+        if order == list(range(n)) and self.arena_in_ready_order:
+            return False
+        self.arena.relayout(order)
+        self.arena_in_ready_order = True
+        self._build()
+        return True
+
+    def remove(self):
+        if self._impl is not None:
+            self._impl.remove_hooks()
+            self._impl = None

@@ -1,0 +1,204 @@
+"""Flat parameter / gradient / momentum arenas.
+
+MI355X-first memory layout: all parameters of a model live in ONE contiguous fp32
+allocation, every ``p.grad`` is a view into ONE gradient allocation and the optimizer's momentum
+buffers into a third. Consequences:
+
+* a gradient bucket is a contiguous arena range -> the RCCL all-reduce runs in place, zero copies
+  (PyTorch DDP calls this ``gradient_as_bucket_view``);
+* the SGD step is one vectorised kernel over the whole arena instead of 34 (VGG-11) / 161
+  (ResNet-50) per-tensor launches;
+* the construction-time parameter broadcast and the per-forward buffer broadcast are single
+  collectives;
+* every view keeps its parameter's shape *and strides* (conv weights stay channels_last), so
+  ``state_dict`` / ``load_state_dict`` / AccumulateGrad's layout contract are unaffected.
+
+Offsets are padded to 16 bytes so every view is float4-aligned for the kernels.
+"""
+from __future__ import annotations
+
+from typing import Iterable, List, Sequence
+
+import torch
+
+ALIGN = 4  # elements (16 B for fp32)
+
+
+def _dense(t: torch.Tensor) -> bool:
+    return t.is_contiguous() or (t.dim() == 4 and t.is_contiguous(memory_format=torch.channels_last))
+
+
+def _view_like(flat: torch.Tensor, offset: int, ref: torch.Tensor) -> torch.Tensor:
+    return flat.as_strided(ref.size(), ref.stride(), flat.storage_offset() + offset)
+
+
+class FlatArena:
+    """Owns the flat storages for a fixed, ordered list of parameters."""
+
+    def __init__(self, params: Sequence[torch.nn.Parameter], with_grad: bool = True):
+        params = list(params)
+        if not params:
+            raise ValueError("FlatArena needs at least one parameter")
+        dev, dt = params[0].device, params[0].dtype
+        for p in params:
+            if p.device != dev or p.dtype != dt:
+                raise ValueError("all arena parameters must share device and dtype")
+            if not _dense(p.data):
+                p.data = p.data.contiguous()
+        self.device, self.dtype = dev, dt
+        self.params: List[torch.nn.Parameter] = params
+        self._layout(params)
+        self.data = torch.empty(self.total, device=dev, dtype=dt)
+        self.data.zero_()
+        for p, off in zip(params, self.offsets):
+            v = _view_like(self.data, off, p.data)
+            v.copy_(p.data)
+            p.data = v
+        self.grad = None
+        self.momentum = None
+        if with_grad:
+            self.attach_grads()
+        for i, p in enumerate(params):
+            p._cdp_arena = self
+            p._cdp_index = i
+
+    # ------------------------------------------------------------------ layout
+    def _layout(self, params):
+        self.offsets, self.numels = [], []
+        off = 0
+        for p in params:
+            n = p.numel()
+            self.offsets.append(off)
+            self.numels.append(n)
+            off += (n + ALIGN - 1) // ALIGN * ALIGN
+        self.total = max(off, ALIGN)
+
+    def index(self, p) -> int:
+        return p._cdp_index
+
+    def attach_grads(self):
+        """(Re)point every ``p.grad`` at its arena slot (keeping any existing values)."""
+        if self.grad is None:
+            self.grad = torch.zeros(self.total, device=self.device, dtype=self.dtype)
+        for p, off in zip(self.params, self.offsets):
+            v = _view_like(self.grad, off, p.data)
+            if p.grad is not None and p.grad.data_ptr() != v.data_ptr():
+                v.copy_(p.grad)
+            p.grad = v
+        return self.grad
+
+    def grad_views(self) -> List[torch.Tensor]:
+        return [_view_like(self.grad, off, p.data) for p, off in zip(self.params, self.offsets)]
+
+    def param_views(self) -> List[torch.Tensor]:
+        return [_view_like(self.data, off, p.data) for p, off in zip(self.params, self.offsets)]
+
+    def momentum_buffer(self) -> torch.Tensor:
+        if self.momentum is None:
+            self.momentum = torch.zeros(self.total, device=self.device, dtype=self.dtype)
+        return self.momentum
+
+    def momentum_views(self) -> List[torch.Tensor]:
+        buf = self.momentum_buffer()
+        return [_view_like(buf, off, p.data) for p, off in zip(self.params, self.offsets)]
+
+    def zero_grad(self):
+        if self.grad is not None:
+            self.grad.zero_()
+            self.attach_grads()
+
+    def range_of(self, first: int, last: int):
+        """Flat [start, end) element range covering parameters first..last (inclusive, arena order)."""
+        s = self.offsets[first]
+        e = self.offsets[last] + (self.numels[last] + ALIGN - 1) // ALIGN * ALIGN
+        return s, e
+
+    def contiguous_range(self, params: Iterable[torch.nn.Parameter]):
+        """If ``params`` cover a gap-free run of arena slots, return its flat [start, end); else None."""
+        idx = sorted(p._cdp_index for p in params if getattr(p, "_cdp_arena", None) is self)
+        if not idx:
+            return None
+        if idx != list(range(idx[0], idx[-1] + 1)):
+            return None
+        return self.range_of(idx[0], idx[-1])
+
+    # ------------------------------------------------------------------ relayout
+    def relayout(self, new_order: Sequence[int]):
+        """Permute the arena into ``new_order`` (indices into the current parameter list).
+
+        Used after the first iteration to lay gradients out in their observed ready order, so every
+        bucket is a contiguous range. Parameter values, gradients and momentum move with their
+        parameters; all views are re-pointed.
+        """
+        new_order = list(new_order)
+        if sorted(new_order) != list(range(len(self.params))):
+            raise ValueError("relayout order must be a permutation of the parameter indices")
+        old_params, old_offsets = self.params, self.offsets
+        old_data, old_grad, old_mom = self.data, self.grad, self.momentum
+        params = [old_params[i] for i in new_order]
+        self._layout(params)
+        self.params = params
+        self.data = torch.zeros(self.total, device=self.device, dtype=self.dtype)
+        self.grad = None if old_grad is None else torch.zeros_like(self.data)
+        self.momentum = None if old_mom is None else torch.zeros_like(self.data)
+        for new_i, old_i in enumerate(new_order):
+            p = params[new_i]
+            o_off, n_off = old_offsets[old_i], self.offsets[new_i]
+            v = _view_like(self.data, n_off, p.data)
+            v.copy_(_view_like(old_data, o_off, p.data))
+            p.data = v
+            if old_grad is not None:
+                _view_like(self.grad, n_off, p.data).copy_(_view_like(old_grad, o_off, p.data))
+            if old_mom is not None:
+                _view_like(self.momentum, n_off, p.data).copy_(_view_like(old_mom, o_off, p.data))
+            p._cdp_index = new_i
+        if old_grad is not None:
+            self.attach_grads()
+        for cb in getattr(self, "_relayout_callbacks", []):
+            cb(self)
+
+    def on_relayout(self, cb):
+        if not hasattr(self, "_relayout_callbacks"):
+            self._relayout_callbacks = []
+        self._relayout_callbacks.append(cb)
+
+
+def arena_for(params: Sequence[torch.nn.Parameter], create: bool = True) -> FlatArena | None:
+    """Return the arena shared by ``params`` (creating one over exactly these params if needed)."""
+    params = [p for p in params if p.requires_grad]
+    arenas = {id(getattr(p, "_cdp_arena", None)) for p in params}
+    if len(arenas) == 1:
+        a = getattr(params[0], "_cdp_arena", None)
+        if a is not None:
+            return a
+    if not create:
+        return None
+    return FlatArena(params)
+
+
+class BufferArena:
+    """Flat arena for module buffers (BN running stats) so they broadcast as ONE collective.
+
+    Floating buffers share one fp32 storage; integer buffers (``num_batches_tracked``) another.
+    """
+
+    def __init__(self, buffers: Sequence[torch.Tensor]):
+        self.buffers = list(buffers)
+        self.groups = {}
+        by_dtype = {}
+        for b in self.buffers:
+            by_dtype.setdefault(b.dtype, []).append(b)
+        for dt, bufs in by_dtype.items():
+            total = sum(b.numel() for b in bufs)
+            flat = torch.empty(total, device=bufs[0].device, dtype=dt)
+            off = 0
+            for b in bufs:
+                n = b.numel()
+                v = flat[off : off + n].view(b.shape)
+                v.copy_(b.data)
+                b.data = v
+                off += n
+            self.groups[dt] = flat
+
+    def flats(self) -> List[torch.Tensor]:
+        return list(self.groups.values())

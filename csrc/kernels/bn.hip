@@ -1,0 +1,460 @@
+// BatchNorm2d (+ReLU)(+MaxPool2d 2x2/2) forward and backward on NHWC fp32, gfx950.
+//
+// Reference layer stack: Conv2d -> BatchNorm2d -> ReLU(inplace) [-> MaxPool2d(2,2)] built by
+// _make_layers at /root/reference/src/Part 1/model.py:11-27. Training-mode BN uses batch
+// statistics (biased variance) and updates running_mean / running_var (unbiased) with
+// momentum 0.1 and num_batches_tracked; eval mode uses the running statistics.
+//
+// Data flow per block (forward):
+//   conv epilogue -> per-tile (mean, M2) partials  ->  bn_finalize (Chan merge, fp64)  ->
+//   bn_act_fwd: z = relu(y*scale + shift), optional 2x2 max -> next layer input
+// Backward recomputes z and the pool argmax from the saved conv output y (nothing else is
+// stored):  bn_bwd_reduce (sum dz, sum dz*xhat per channel)  ->  chan_finalize  ->
+//   bn_bwd_apply: dy = scale*(dz - mean(dz) - xhat*mean(dz*xhat)), plus partial sum(dy) for the
+//   conv bias gradient.
+// All element kernels move float4 along C (C % 4 == 0).
+#include "common.h"
+#include "kernels.h"
+
+namespace cdp {
+namespace {
+
+// ------------------------------------------------------------------ finalize (train)
+__global__ __launch_bounds__(256) void bn_finalize_kernel(const float* __restrict__ part, int nparts, int rpp, int M,
+                                                          int C, const float* __restrict__ gamma,
+                                                          const float* __restrict__ beta, float* running_mean,
+                                                          float* running_var, long long* nbt, float momentum,
+                                                          float eps, float* __restrict__ stats) {
+  __shared__ double red[4];
+  const int c = blockIdx.x;
+  const int tid = threadIdx.x;
+  double s = 0.0;
+  for (int b = tid; b < nparts; b += 256) {
+    const int cnt = min(rpp, M - b * rpp);
+    s += (double)cnt * (double)part[((long long)b * C + c) * 2];
+  }
+  s = wave_sum_d(s);
+  if ((tid & 63) == 0) red[tid >> 6] = s;
+  __syncthreads();
+  const double mean = (red[0] + red[1] + red[2] + red[3]) / (double)M;
+  __syncthreads();
+  double q = 0.0;
+  for (int b = tid; b < nparts; b += 256) {
+    const int cnt = min(rpp, M - b * rpp);
+    const double d = (double)part[((long long)b * C + c) * 2] - mean;
+    q += (double)part[((long long)b * C + c) * 2 + 1] + (double)cnt * d * d;
+  }
+  q = wave_sum_d(q);
+  if ((tid & 63) == 0) red[tid >> 6] = q;
+  __syncthreads();
+  if (tid == 0) {
+    const double m2 = red[0] + red[1] + red[2] + red[3];
+    const double var = m2 / (double)M;
+    const float invstd = (float)(1.0 / sqrt(var + (double)eps));
+    const float g = gamma ? gamma[c] : 1.f;
+    const float bb = beta ? beta[c] : 0.f;
+    const float scale = g * invstd;
+    // stats layout: [mean | invstd | scale | shift] x C
+    stats[c] = (float)mean;
+    stats[C + c] = invstd;
+    stats[2 * C + c] = scale;
+    stats[3 * C + c] = bb - (float)mean * scale;
+    if (running_mean) {
+      float f = momentum;
+      if (f < 0.f) f = 1.f / (float)(nbt[0] + 1);  // momentum=None: cumulative average
+      const double unb = M > 1 ? m2 / (double)(M - 1) : var;
+      running_mean[c] = (1.f - f) * running_mean[c] + f * (float)mean;
+      running_var[c] = (1.f - f) * running_var[c] + f * (float)unb;
+    }
+    if (c == 0 && nbt) nbt[0] += 1;
+  }
+}
+
+// eval mode: scale/shift from running stats
+__global__ void bn_eval_stats_kernel(int C, const float* gamma, const float* beta, const float* rm, const float* rv,
+                                     float eps, float* stats) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  const float invstd = 1.f / sqrtf(rv[c] + eps);
+  const float g = gamma ? gamma[c] : 1.f;
+  const float b = beta ? beta[c] : 0.f;
+  stats[c] = rm[c];
+  stats[C + c] = invstd;
+  stats[2 * C + c] = g * invstd;
+  stats[3 * C + c] = b - rm[c] * g * invstd;
+}
+
+__device__ __forceinline__ float4 affine_act(float4 y, float4 sc, float4 sh, bool relu) {
+  float4 z;
+  z.x = fmaf(y.x, sc.x, sh.x);
+  z.y = fmaf(y.y, sc.y, sh.y);
+  z.z = fmaf(y.z, sc.z, sh.z);
+  z.w = fmaf(y.w, sc.w, sh.w);
+  if (relu) {
+    z.x = fmaxf(z.x, 0.f);
+    z.y = fmaxf(z.y, 0.f);
+    z.z = fmaxf(z.z, 0.f);
+    z.w = fmaxf(z.w, 0.f);
+  }
+  return z;
+}
+
+// ------------------------------------------------------------------ forward apply
+// out = [pool2](relu(y*scale+shift)) (+ residual before relu when res != null)
+__global__ __launch_bounds__(256) void bn_act_fwd_kernel(const float* __restrict__ y, const float* __restrict__ stats,
+                                                         const float* __restrict__ res, float* __restrict__ out,
+                                                         int N, int H, int W, int C, int pool, int relu) {
+  const int C4 = C >> 2;
+  const int Ho = pool ? H / 2 : H, Wo = pool ? W / 2 : W;
+  const long long total = (long long)N * Ho * Wo * C4;
+  const float* scale = stats + 2 * C;
+  const float* shift = stats + 3 * C;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int c4 = (int)(i % C4);
+    const long long pix = i / C4;
+    const float4 sc = ld4(scale + 4 * c4), sh = ld4(shift + 4 * c4);
+    if (!pool) {
+      float4 z = affine_act(ld4(y + pix * C + 4 * c4), sc, sh, false);
+      if (res) {
+        const float4 r = ld4(res + pix * C + 4 * c4);
+        z.x += r.x; z.y += r.y; z.z += r.z; z.w += r.w;
+      }
+      if (relu) {
+        z.x = fmaxf(z.x, 0.f); z.y = fmaxf(z.y, 0.f); z.z = fmaxf(z.z, 0.f); z.w = fmaxf(z.w, 0.f);
+      }
+      st4(out + pix * C + 4 * c4, z);
+    } else {
+      const int wo = (int)(pix % Wo);
+      const long long t = pix / Wo;
+      const int ho = (int)(t % Ho);
+      const int n = (int)(t / Ho);
+      const float* base = y + (((long long)n * H + 2 * ho) * W + 2 * wo) * C + 4 * c4;
+      const float4 z0 = affine_act(ld4(base), sc, sh, relu);
+      const float4 z1 = affine_act(ld4(base + C), sc, sh, relu);
+      const float4 z2 = affine_act(ld4(base + (long long)W * C), sc, sh, relu);
+      const float4 z3 = affine_act(ld4(base + (long long)W * C + C), sc, sh, relu);
+      float4 m;
+      m.x = fmaxf(fmaxf(z0.x, z1.x), fmaxf(z2.x, z3.x));
+      m.y = fmaxf(fmaxf(z0.y, z1.y), fmaxf(z2.y, z3.y));
+      m.z = fmaxf(fmaxf(z0.z, z1.z), fmaxf(z2.z, z3.z));
+      m.w = fmaxf(fmaxf(z0.w, z1.w), fmaxf(z2.w, z3.w));
+      st4(out + pix * C + 4 * c4, m);
+    }
+  }
+}
+
+// ------------------------------------------------------------------ backward helpers
+// For one channel component of a 2x2 window: the gradient reaching each element through
+// max-pool (first max wins, scanning (0,0),(0,1),(1,0),(1,1) like ATen) and ReLU (z > 0).
+__device__ __forceinline__ void pool_relu_grad(float z0, float z1, float z2, float z3, float g, bool relu, float& d0,
+                                               float& d1, float& d2, float& d3) {
+  int arg = 0;
+  float mx = z0;
+  if (z1 > mx) { mx = z1; arg = 1; }
+  if (z2 > mx) { mx = z2; arg = 2; }
+  if (z3 > mx) { mx = z3; arg = 3; }
+  const float gg = (!relu || mx > 0.f) ? g : 0.f;
+  d0 = arg == 0 ? gg : 0.f;
+  d1 = arg == 1 ? gg : 0.f;
+  d2 = arg == 2 ? gg : 0.f;
+  d3 = arg == 3 ? gg : 0.f;
+}
+
+#define F4GET(v, j) ((j) == 0 ? (v).x : (j) == 1 ? (v).y : (j) == 2 ? (v).z : (v).w)
+
+// Per (block, channel) partial sums of dz and dz*xhat, where dz is the gradient at the BN output.
+// Block = 256 threads; for C4 <= 256 threads split as ppb pixel lanes x C4 channel quads.
+__global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const float* __restrict__ y, const float* __restrict__ gout,
+                                                            const float* __restrict__ stats, float* __restrict__ part,
+                                                            int N, int H, int W, int C, int pool, int relu,
+                                                            const float* __restrict__ zout) {
+  __shared__ float4 red1[256], red2[256];
+  const int C4 = C >> 2;
+  const int tid = threadIdx.x;
+  const int cq_per_thread = (C4 + 255) / 256;  // 1 or 2
+  const int lanes_c = C4 < 256 ? C4 : 256;
+  const int ppb = 256 / lanes_c;               // pixel lanes per block
+  const int cq0 = tid % lanes_c;
+  const int pl = tid / lanes_c;
+  const bool active = pl < ppb;
+  const float* mean = stats;
+  const float* invstd = stats + C;
+  const float* scale = stats + 2 * C;
+  const float* shift = stats + 3 * C;
+  const int Ho = pool ? H / 2 : H, Wo = pool ? W / 2 : W;
+  const long long npix = (long long)N * Ho * Wo;  // output (pooled) pixels
+  for (int j = 0; j < cq_per_thread; ++j) {
+    const int cq = cq0 + j * 256;
+    float4 a1 = f4zero(), a2 = f4zero();
+    if (active && cq < C4) {
+      const float4 sc = ld4(scale + 4 * cq), sh = ld4(shift + 4 * cq);
+      const float4 mu = ld4(mean + 4 * cq), is = ld4(invstd + 4 * cq);
+      for (long long px = (long long)blockIdx.x * ppb + pl; px < npix; px += (long long)gridDim.x * ppb) {
+        const float4 g = ld4(gout + px * C + 4 * cq);
+        if (!pool) {
+          const float4 yv = ld4(y + px * C + 4 * cq);
+          const float4 z = zout ? ld4(zout + px * C + 4 * cq) : affine_act(yv, sc, sh, relu);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float dz = (!relu || F4GET(z, e) > 0.f) ? F4GET(g, e) : 0.f;
+            const float xh = (F4GET(yv, e) - F4GET(mu, e)) * F4GET(is, e);
+            if (e == 0) { a1.x += dz; a2.x += dz * xh; }
+            if (e == 1) { a1.y += dz; a2.y += dz * xh; }
+            if (e == 2) { a1.z += dz; a2.z += dz * xh; }
+            if (e == 3) { a1.w += dz; a2.w += dz * xh; }
+          }
+        } else {
+          const int wo = (int)(px % Wo);
+          const long long t = px / Wo;
+          const int ho = (int)(t % Ho);
+          const int n = (int)(t / Ho);
+          const float* base = y + (((long long)n * H + 2 * ho) * W + 2 * wo) * C + 4 * cq;
+          const float4 y0 = ld4(base), y1 = ld4(base + C), y2 = ld4(base + (long long)W * C),
+                       y3 = ld4(base + (long long)W * C + C);
+          const float4 z0 = affine_act(y0, sc, sh, relu), z1 = affine_act(y1, sc, sh, relu),
+                       z2 = affine_act(y2, sc, sh, relu), z3 = affine_act(y3, sc, sh, relu);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            float d0, d1, d2, d3;
+            pool_relu_grad(F4GET(z0, e), F4GET(z1, e), F4GET(z2, e), F4GET(z3, e), F4GET(g, e), relu, d0, d1, d2,
+                           d3);
+            const float m = F4GET(mu, e), s = F4GET(is, e);
+            const float sdz = d0 + d1 + d2 + d3;
+            const float sdx = d0 * ((F4GET(y0, e) - m) * s) + d1 * ((F4GET(y1, e) - m) * s) +
+                              d2 * ((F4GET(y2, e) - m) * s) + d3 * ((F4GET(y3, e) - m) * s);
+            if (e == 0) { a1.x += sdz; a2.x += sdx; }
+            if (e == 1) { a1.y += sdz; a2.y += sdx; }
+            if (e == 2) { a1.z += sdz; a2.z += sdx; }
+            if (e == 3) { a1.w += sdz; a2.w += sdx; }
+          }
+        }
+      }
+    }
+    red1[tid] = a1;
+    red2[tid] = a2;
+    __syncthreads();
+    if (pl == 0 && cq < C4) {
+      float4 s1 = a1, s2 = a2;
+      for (int k = 1; k < ppb; ++k) {
+        const float4 b1 = red1[k * lanes_c + cq0], b2 = red2[k * lanes_c + cq0];
+        s1.x += b1.x; s1.y += b1.y; s1.z += b1.z; s1.w += b1.w;
+        s2.x += b2.x; s2.y += b2.y; s2.z += b2.z; s2.w += b2.w;
+      }
+      float* dst = part + ((long long)blockIdx.x * C + 4 * cq) * 2;
+      dst[0] = s1.x; dst[1] = s2.x; dst[2] = s1.y; dst[3] = s2.y;
+      dst[4] = s1.z; dst[5] = s2.z; dst[6] = s1.w; dst[7] = s2.w;
+    }
+    __syncthreads();
+  }
+}
+
+// Sum per-block partial pairs: out[c] = sum_b part[b][c][0], out[C+c] = sum_b part[b][c][1]
+// (fp64 accumulation; deterministic order). Optionally also writes into two gradient slots
+// (accumulating if requested).
+__global__ __launch_bounds__(256) void chan_finalize_kernel(const float* __restrict__ part, int nparts, int C,
+                                                            float* __restrict__ out, float* g0, float* g1,
+                                                            int accumulate) {
+  __shared__ double r0[4], r1[4];
+  const int c = blockIdx.x;
+  double s0 = 0.0, s1 = 0.0;
+  for (int b = threadIdx.x; b < nparts; b += 256) {
+    s0 += (double)part[((long long)b * C + c) * 2];
+    s1 += (double)part[((long long)b * C + c) * 2 + 1];
+  }
+  s0 = wave_sum_d(s0);
+  s1 = wave_sum_d(s1);
+  if ((threadIdx.x & 63) == 0) {
+    r0[threadIdx.x >> 6] = s0;
+    r1[threadIdx.x >> 6] = s1;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const float t0 = (float)(r0[0] + r0[1] + r0[2] + r0[3]);
+    const float t1 = (float)(r1[0] + r1[1] + r1[2] + r1[3]);
+    if (out) {
+      out[c] = t0;
+      out[C + c] = t1;
+    }
+    if (g0) g0[c] = accumulate ? g0[c] + t0 : t0;
+    if (g1) g1[c] = accumulate ? g1[c] + t1 : t1;
+  }
+}
+
+// dy = scale*(dz - sum(dz)/M - xhat*sum(dz*xhat)/M), full resolution; partial sum(dy) per
+// (block, channel) for the conv bias gradient. Each thread handles one pooled window (pool) or
+// one pixel; for odd H/W under pooling the uncovered border gets dz = 0.
+__global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const float* __restrict__ y, const float* __restrict__ gout,
+                                                           const float* __restrict__ stats,
+                                                           const float* __restrict__ sums, float* __restrict__ dy,
+                                                           float* __restrict__ dbias_part, int N, int H, int W,
+                                                           int C, int pool, int relu, const float* __restrict__ zout,
+                                                           float* __restrict__ dres) {
+  __shared__ float4 red[256];
+  const int C4 = C >> 2;
+  const int tid = threadIdx.x;
+  const int cq_per_thread = (C4 + 255) / 256;
+  const int lanes_c = C4 < 256 ? C4 : 256;
+  const int ppb = 256 / lanes_c;
+  const int cq0 = tid % lanes_c;
+  const int pl = tid / lanes_c;
+  const bool active = pl < ppb;
+  const float* mean = stats;
+  const float* invstd = stats + C;
+  const float* scale = stats + 2 * C;
+  const float* shift = stats + 3 * C;
+  const long long Mtot = (long long)N * H * W;
+  const float invM = 1.f / (float)Mtot;
+  const int Ho = pool ? H / 2 : H, Wo = pool ? W / 2 : W;
+  const long long npix = pool ? (long long)N * Ho * Wo : Mtot;
+  for (int j = 0; j < cq_per_thread; ++j) {
+    const int cq = cq0 + j * 256;
+    float4 acc = f4zero();
+    if (active && cq < C4) {
+      const float4 sc = ld4(scale + 4 * cq), sh = ld4(shift + 4 * cq);
+      const float4 mu = ld4(mean + 4 * cq), is = ld4(invstd + 4 * cq);
+      const float4 s1 = ld4(sums + 4 * cq), s2 = ld4(sums + C + 4 * cq);
+      float4 k1, k2;  // dy = sc*(dz - k1 - xhat*k2)
+      k1.x = s1.x * invM; k1.y = s1.y * invM; k1.z = s1.z * invM; k1.w = s1.w * invM;
+      k2.x = s2.x * invM; k2.y = s2.y * invM; k2.z = s2.z * invM; k2.w = s2.w * invM;
+      auto emit = [&](long long off, float4 yv, float4 dz) {
+        float4 o;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float xh = (F4GET(yv, e) - F4GET(mu, e)) * F4GET(is, e);
+          const float v = F4GET(sc, e) * (F4GET(dz, e) - F4GET(k1, e) - xh * F4GET(k2, e));
+          if (e == 0) o.x = v;
+          if (e == 1) o.y = v;
+          if (e == 2) o.z = v;
+          if (e == 3) o.w = v;
+        }
+        st4(dy + off, o);
+        acc.x += o.x; acc.y += o.y; acc.z += o.z; acc.w += o.w;
+      };
+      for (long long px = (long long)blockIdx.x * ppb + pl; px < npix; px += (long long)gridDim.x * ppb) {
+        const float4 g = ld4(gout + px * C + 4 * cq);
+        if (!pool) {
+          const float4 yv = ld4(y + px * C + 4 * cq);
+          const float4 z = zout ? ld4(zout + px * C + 4 * cq) : affine_act(yv, sc, sh, relu);
+          float4 dz;
+          dz.x = (!relu || z.x > 0.f) ? g.x : 0.f;
+          dz.y = (!relu || z.y > 0.f) ? g.y : 0.f;
+          dz.z = (!relu || z.z > 0.f) ? g.z : 0.f;
+          dz.w = (!relu || z.w > 0.f) ? g.w : 0.f;
+          if (dres) st4(dres + px * C + 4 * cq, dz);
+          emit(px * C + 4 * cq, yv, dz);
+        } else {
+          const int wo = (int)(px % Wo);
+          const long long t = px / Wo;
+          const int ho = (int)(t % Ho);
+          const int n = (int)(t / Ho);
+          const long long o0 = (((long long)n * H + 2 * ho) * W + 2 * wo) * C + 4 * cq;
+          const long long o1 = o0 + C, o2 = o0 + (long long)W * C, o3 = o2 + C;
+          const float4 y0 = ld4(y + o0), y1 = ld4(y + o1), y2 = ld4(y + o2), y3 = ld4(y + o3);
+          const float4 z0 = affine_act(y0, sc, sh, relu), z1 = affine_act(y1, sc, sh, relu),
+                       z2 = affine_act(y2, sc, sh, relu), z3 = affine_act(y3, sc, sh, relu);
+          float4 d0, d1, d2, d3;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            float a, b, c, d;
+            pool_relu_grad(F4GET(z0, e), F4GET(z1, e), F4GET(z2, e), F4GET(z3, e), F4GET(g, e), relu, a, b, c, d);
+            if (e == 0) { d0.x = a; d1.x = b; d2.x = c; d3.x = d; }
+            if (e == 1) { d0.y = a; d1.y = b; d2.y = c; d3.y = d; }
+            if (e == 2) { d0.z = a; d1.z = b; d2.z = c; d3.z = d; }
+            if (e == 3) { d0.w = a; d1.w = b; d2.w = c; d3.w = d; }
+          }
+          emit(o0, y0, d0);
+          emit(o1, y1, d1);
+          emit(o2, y2, d2);
+          emit(o3, y3, d3);
+        }
+      }
+      // odd-size border under pooling: rows/cols not covered by any window get dz = 0
+      if (pool && ((H & 1) || (W & 1))) {
+        const long long nb = (long long)N * H * W;
+        for (long long px = (long long)blockIdx.x * ppb + pl; px < nb; px += (long long)gridDim.x * ppb) {
+          const int w = (int)(px % W);
+          const int h = (int)((px / W) % H);
+          if (h < 2 * Ho && w < 2 * Wo) continue;
+          emit(px * C + 4 * cq, ld4(y + px * C + 4 * cq), f4zero());
+        }
+      }
+    }
+    red[tid] = acc;
+    __syncthreads();
+    if (dbias_part && pl == 0 && cq < C4) {
+      float4 s = acc;
+      for (int k = 1; k < ppb; ++k) {
+        const float4 b = red[k * lanes_c + cq0];
+        s.x += b.x; s.y += b.y; s.z += b.z; s.w += b.w;
+      }
+      float* dst = dbias_part + ((long long)blockIdx.x * C + 4 * cq) * 2;
+      dst[0] = s.x; dst[1] = 0.f; dst[2] = s.y; dst[3] = 0.f;
+      dst[4] = s.z; dst[5] = 0.f; dst[6] = s.w; dst[7] = 0.f;
+    }
+    __syncthreads();
+  }
+}
+
+int act_grid(long long work_items) {
+  long long b = (work_items + 255) / 256;
+  if (b > 2048) b = 2048;
+  if (b < 1) b = 1;
+  return (int)b;
+}
+
+}  // namespace
+
+int bn_bwd_grid(int N, int H, int W, int C, bool pool) {
+  const int C4 = C / 4;
+  const int lanes_c = C4 < 256 ? C4 : 256;
+  const int ppb = 256 / lanes_c;
+  const long long npix = (long long)N * (pool ? (H / 2) * (W / 2) : H * W);
+  long long b = (npix + ppb - 1) / ppb;
+  // keep >= ~8 pixels per thread lane for reduction efficiency, <= 1024 partial rows
+  b = (b + 7) / 8;
+  if (b > 1024) b = 1024;
+  if (b < 1) b = 1;
+  return (int)b;
+}
+
+void bn_finalize_launch(const float* part, int nparts, int rpp, int M, int C, const float* gamma, const float* beta,
+                        float* running_mean, float* running_var, long long* nbt, float momentum, float eps,
+                        float* stats, hipStream_t st) {
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3(C), dim3(256), 0, st, part, nparts, rpp, M, C, gamma, beta,
+                     running_mean, running_var, nbt, momentum, eps, stats);
+}
+
+void bn_eval_stats_launch(int C, const float* gamma, const float* beta, const float* rm, const float* rv, float eps,
+                          float* stats, hipStream_t st) {
+  hipLaunchKernelGGL(bn_eval_stats_kernel, dim3((C + 255) / 256), dim3(256), 0, st, C, gamma, beta, rm, rv, eps,
+                     stats);
+}
+
+void bn_act_fwd_launch(const float* y, const float* stats, const float* res, float* out, int N, int H, int W, int C,
+                       bool pool, bool relu, hipStream_t st) {
+  const long long items = (long long)N * (pool ? (H / 2) * (W / 2) : H * W) * (C / 4);
+  hipLaunchKernelGGL(bn_act_fwd_kernel, dim3(act_grid(items)), dim3(256), 0, st, y, stats, res, out, N, H, W, C,
+                     pool ? 1 : 0, relu ? 1 : 0);
+}
+
+void bn_bwd_reduce_launch(const float* y, const float* gout, const float* stats, float* part, int nblocks, int N,
+                          int H, int W, int C, bool pool, bool relu, const float* zout, hipStream_t st) {
+  hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(nblocks), dim3(256), 0, st, y, gout, stats, part, N, H, W, C,
+                     pool ? 1 : 0, relu ? 1 : 0, zout);
+}
+
+void chan_finalize_launch(const float* part, int nparts, int C, float* out, float* g0, float* g1, bool accumulate,
+                          hipStream_t st) {
+  hipLaunchKernelGGL(chan_finalize_kernel, dim3(C), dim3(256), 0, st, part, nparts, C, out, g0, g1,
+                     accumulate ? 1 : 0);
+}
+
+void bn_bwd_apply_launch(const float* y, const float* gout, const float* stats, const float* sums, float* dy,
+                         float* dbias_part, int nblocks, int N, int H, int W, int C, bool pool, bool relu,
+                         const float* zout, float* dres, hipStream_t st) {
+  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(nblocks), dim3(256), 0, st, y, gout, stats, sums, dy, dbias_part, N,
+                     H, W, C, pool ? 1 : 0, relu ? 1 : 0, zout, dres);
+}
+
+}  // namespace cdp

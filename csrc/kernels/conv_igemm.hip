@@ -1,0 +1,410 @@
+// Implicit-GEMM convolution on fp32-input MFMA (v_mfma_f32_32x32x2_f32), gfx950.
+//
+// One kernel family serves:
+//   * conv forward          rows m = (n, p, q) output pixels, K = (kh, kw, c), N = Cout
+//   * conv data-gradient     rows m = (n, ih, iw) input pixels, K = (kh, kw, cout), N = Cin,
+//                            gathered "transposed" from dY with the pre-transposed weight
+//   * Linear forward         a 1x1 conv over [B,1,1,I]
+//
+// Reference semantics: nn.Conv2d(k=3,s=1,p=1,bias=True) at /root/reference/src/Part 1/model.py:18-23
+// (and the strided / 1x1 / 7x7 convs of the ResNet-50 config). The reference runs them through
+// ATen/oneDNN on CPU; here they are one LDS-tiled MFMA kernel with the bias add and the per-block
+// BatchNorm statistics (mean, M2 -- Chan's parallel form) fused into the epilogue, so the
+// following BatchNorm never re-reads the conv output for its statistics.
+//
+// Tile: BM x BN x 32, 256 threads = 4 waves as 2x2, each wave (BM/2)x(BN/2) built from 32x32
+// MFMA tiles. Operands are staged global -> registers -> LDS (double buffered, one barrier per
+// K-tile); the gather needs per-lane zero-padding, which LDS-DMA cannot express. Rows of both LDS
+// tiles are K-contiguous with a 16-byte pad (36 floats) so the ds_read_b128 fragment reads are
+// bank-conflict free (MI355X_MICROARCH.md §LDS, ds_read_b128 lane groups). The MFMA K index is
+// permuted: lanes 0-31 consume k = s, lanes 32-63 consume k = 16 + s at step s, so each lane
+// reads 4 consecutive k per ds_read_b128.
+#include "common.h"
+#include "kernels.h"
+
+namespace cdp {
+
+namespace {
+
+constexpr int BK = 32;
+constexpr int LDK = BK + 4;
+
+template <int BM, int BN, bool FAST, bool DGRAD>
+__global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvGemmParams p) {
+  constexpr int TM = BM / 64;  // 32-row MFMA tiles per wave
+  constexpr int TN = BN / 64;  // 32-col MFMA tiles per wave
+  constexpr int STAGE = (BM + BN) * LDK;
+  __shared__ __attribute__((aligned(16))) float smem[2 * STAGE];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wid = tid >> 6;
+  const int wm = wid >> 1, wn = wid & 1;
+
+  const int ntn = (p.Nout + BN - 1) / BN;
+  const int total = gridDim.x;
+  const int bid = xcd_remap(blockIdx.x, total);
+  // order: tn fastest, then split, then tm -> blocks sharing an A slice are adjacent
+  const int tn_idx = bid % ntn;
+  const int rest = bid / ntn;
+  const int split = rest % p.splits;
+  const int tm_idx = rest / p.splits;
+  const int m0 = tm_idx * BM, n0 = tn_idx * BN;
+
+  const int kt_begin = (int)(((long long)split * p.ktiles) / p.splits);
+  const int kt_end = (int)(((long long)(split + 1) * p.ktiles) / p.splits);
+
+  const int PQ = p.P * p.Q;
+
+  // ---------------- per-thread gather setup ----------------
+  // FAST: each thread owns BM/32 A rows (row = tid/8 + 32*i) and one float4 column (tid%8).
+  // generic: each thread owns one A row and CPT consecutive scalar columns.
+  constexpr int A_LD = FAST ? BM / 32 : 1;
+  constexpr int B_LD = FAST ? BN / 32 : 1;
+  constexpr int TPR_A = 256 / BM;            // generic: threads per A row
+  constexpr int CPT_A = BK / TPR_A;          // generic: columns per thread (A)
+  constexpr int TPR_B = 256 / BN;
+  constexpr int CPT_B = BK / TPR_B;
+
+  const float* a_base[A_LD];
+  int a_h[A_LD], a_w[A_LD];
+  bool a_ok[A_LD];
+#pragma unroll
+  for (int i = 0; i < A_LD; ++i) {
+    const int row = FAST ? ((tid >> 3) + 32 * i) : (tid / TPR_A);
+    const int m = m0 + row;
+    a_ok[i] = m < p.M;
+    const int mm = a_ok[i] ? m : 0;
+    const int n = mm / PQ;
+    const int rem = mm - n * PQ;
+    const int pp = rem / p.Q;
+    const int qq = rem - pp * p.Q;
+    a_base[i] = p.x + (long long)n * p.H * p.W * p.C;
+    if (DGRAD) {
+      a_h[i] = pp + p.pad;  // oh*stride = ih + pad - kh
+      a_w[i] = qq + p.pad;
+    } else {
+      a_h[i] = pp * p.stride - p.pad;
+      a_w[i] = qq * p.stride - p.pad;
+    }
+  }
+
+  float4 ra[FAST ? A_LD : 1];
+  float4 rb[FAST ? B_LD : 1];
+  float sa[FAST ? 1 : CPT_A];
+  float sb[FAST ? 1 : CPT_B];
+
+  auto pix_ok = [&](int i, int kh, int kw, int& ih, int& iw) -> bool {
+    if (DGRAD) {
+      int oh = a_h[i] - kh, ow = a_w[i] - kw;
+      if (oh < 0 || ow < 0) return false;
+      if (p.stride != 1) {
+        if ((oh % p.stride) | (ow % p.stride)) return false;
+        oh /= p.stride;
+        ow /= p.stride;
+      }
+      ih = oh;
+      iw = ow;
+      return oh < p.H && ow < p.W;
+    } else {
+      ih = a_h[i] + kh;
+      iw = a_w[i] + kw;
+      return (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W;
+    }
+  };
+
+  auto load_tile = [&](int kt) {
+    const int r0 = kt * BK;
+    if (FAST) {
+      const int tap = r0 / p.C;
+      const int c0 = r0 - tap * p.C + (tid & 7) * 4;
+      const int kh = tap / p.KW, kw = tap - (tap / p.KW) * p.KW;
+#pragma unroll
+      for (int i = 0; i < A_LD; ++i) {
+        int ih, iw;
+        const bool ok = a_ok[i] && pix_ok(i, kh, kw, ih, iw);
+        ra[i] = ok ? ld4(a_base[i] + ((long long)ih * p.W + iw) * p.C + c0) : f4zero();
+      }
+#pragma unroll
+      for (int i = 0; i < B_LD; ++i) {
+        const int n = n0 + (tid >> 3) + 32 * i;
+        rb[i] = (n < p.Nout) ? ld4(p.w + (long long)n * p.Kdim + r0 + (tid & 7) * 4) : f4zero();
+      }
+    } else {
+      const int cbase = (tid % TPR_A) * CPT_A;
+#pragma unroll
+      for (int j = 0; j < CPT_A; ++j) {
+        const int r = r0 + cbase + j;
+        float v = 0.f;
+        if (a_ok[0] && r < p.Kdim) {
+          const int tap = r / p.C;
+          const int c = r - tap * p.C;
+          const int kh = tap / p.KW, kw = tap - (tap / p.KW) * p.KW;
+          int ih, iw;
+          if (pix_ok(0, kh, kw, ih, iw)) v = a_base[0][((long long)ih * p.W + iw) * p.C + c];
+        }
+        sa[j] = v;
+      }
+      const int nrow = n0 + tid / TPR_B;
+      const int cb = (tid % TPR_B) * CPT_B;
+#pragma unroll
+      for (int j = 0; j < CPT_B; ++j) {
+        const int r = r0 + cb + j;
+        sb[j] = (nrow < p.Nout && r < p.Kdim) ? p.w[(long long)nrow * p.Kdim + r] : 0.f;
+      }
+    }
+  };
+
+  auto store_tile = [&](float* st) {
+    float* As = st;
+    float* Bs = st + BM * LDK;
+    if (FAST) {
+#pragma unroll
+      for (int i = 0; i < A_LD; ++i) st4(As + ((tid >> 3) + 32 * i) * LDK + (tid & 7) * 4, ra[i]);
+#pragma unroll
+      for (int i = 0; i < B_LD; ++i) st4(Bs + ((tid >> 3) + 32 * i) * LDK + (tid & 7) * 4, rb[i]);
+    } else {
+      const int arow = tid / TPR_A, acb = (tid % TPR_A) * CPT_A;
+#pragma unroll
+      for (int j = 0; j < CPT_A; ++j) As[arow * LDK + acb + j] = sa[j];
+      const int brow = tid / TPR_B, bcb = (tid % TPR_B) * CPT_B;
+#pragma unroll
+      for (int j = 0; j < CPT_B; ++j) Bs[brow * LDK + bcb + j] = sb[j];
+    }
+  };
+
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int a = 0; a < TM; ++a)
+#pragma unroll
+    for (int b = 0; b < TN; ++b)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
+
+  const int koff = (lane >> 5) * 16;
+  const int l32 = lane & 31;
+
+  if (kt_begin < kt_end) {
+    load_tile(kt_begin);
+    store_tile(smem);
+    __syncthreads();
+    for (int kt = kt_begin; kt < kt_end; ++kt) {
+      const int cur = (kt - kt_begin) & 1;
+      const bool more = kt + 1 < kt_end;
+      if (more) load_tile(kt + 1);
+      const float* As = smem + cur * STAGE;
+      const float* Bs = As + BM * LDK;
+#pragma unroll
+      for (int s4 = 0; s4 < 4; ++s4) {
+        float4 af[TM], bf[TN];
+#pragma unroll
+        for (int a = 0; a < TM; ++a) af[a] = ld4(As + (wm * (BM / 2) + a * 32 + l32) * LDK + koff + s4 * 4);
+#pragma unroll
+        for (int b = 0; b < TN; ++b) bf[b] = ld4(Bs + (wn * (BN / 2) + b * 32 + l32) * LDK + koff + s4 * 4);
+#pragma unroll
+        for (int a = 0; a < TM; ++a)
+#pragma unroll
+          for (int b = 0; b < TN; ++b) {
+            acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[a].x, bf[b].x, acc[a][b], 0, 0, 0);
+            acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[a].y, bf[b].y, acc[a][b], 0, 0, 0);
+            acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[a].z, bf[b].z, acc[a][b], 0, 0, 0);
+            acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[a].w, bf[b].w, acc[a][b], 0, 0, 0);
+          }
+      }
+      if (more) store_tile(smem + (cur ^ 1) * STAGE);
+      __syncthreads();
+    }
+  }
+
+  // ---------------- epilogue ----------------
+  const int hh = lane >> 5;
+  if (p.splits > 1) {
+    float* out = p.y + (long long)split * p.M * p.Nout;
+#pragma unroll
+    for (int a = 0; a < TM; ++a)
+#pragma unroll
+      for (int b = 0; b < TN; ++b) {
+        const int n = n0 + wn * (BN / 2) + b * 32 + l32;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int m = m0 + wm * (BM / 2) + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
+          if (m < p.M && n < p.Nout) out[(long long)m * p.Nout + n] = acc[a][b][r];
+        }
+      }
+    return;
+  }
+
+  float bias_v[TN];
+#pragma unroll
+  for (int b = 0; b < TN; ++b) {
+    const int n = n0 + wn * (BN / 2) + b * 32 + l32;
+    bias_v[b] = (p.bias && n < p.Nout) ? p.bias[n] : 0.f;
+  }
+#pragma unroll
+  for (int a = 0; a < TM; ++a)
+#pragma unroll
+    for (int b = 0; b < TN; ++b) {
+      const int n = n0 + wn * (BN / 2) + b * 32 + l32;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = m0 + wm * (BM / 2) + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
+        const float v = acc[a][b][r] + bias_v[b];
+        acc[a][b][r] = v;
+        if (m < p.M && n < p.Nout) p.y[(long long)m * p.Nout + n] = v;
+      }
+    }
+  if (!p.part) return;
+
+  // Per-block BatchNorm partials over this tile's valid rows: mean_b and M2_b per column.
+  // Two passes over the accumulators already in registers (exact two-pass variance per block).
+  __syncthreads();  // smem reuse
+  float* red = smem;  // [2][BN]
+  const int cnt = min(BM, p.M - m0);
+  float colsum[TN];
+#pragma unroll
+  for (int b = 0; b < TN; ++b) {
+    float s = 0.f;
+#pragma unroll
+    for (int a = 0; a < TM; ++a)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = m0 + wm * (BM / 2) + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
+        s += (m < p.M) ? acc[a][b][r] : 0.f;
+      }
+    s += __shfl_xor(s, 32, kWave);
+    colsum[b] = s;
+  }
+  if (hh == 0) {
+#pragma unroll
+    for (int b = 0; b < TN; ++b) red[wm * BN + wn * (BN / 2) + b * 32 + l32] = colsum[b];
+  }
+  __syncthreads();
+  float mean_b[TN];
+#pragma unroll
+  for (int b = 0; b < TN; ++b) {
+    const int c = wn * (BN / 2) + b * 32 + l32;
+    mean_b[b] = (red[c] + red[BN + c]) / (float)cnt;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int b = 0; b < TN; ++b) {
+    float s = 0.f;
+#pragma unroll
+    for (int a = 0; a < TM; ++a)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = m0 + wm * (BM / 2) + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
+        const float d = acc[a][b][r] - mean_b[b];
+        s += (m < p.M) ? d * d : 0.f;
+      }
+    s += __shfl_xor(s, 32, kWave);
+    colsum[b] = s;
+  }
+  if (hh == 0) {
+#pragma unroll
+    for (int b = 0; b < TN; ++b) red[wm * BN + wn * (BN / 2) + b * 32 + l32] = colsum[b];
+  }
+  __syncthreads();
+  if (wm == 0 && hh == 0) {
+#pragma unroll
+    for (int b = 0; b < TN; ++b) {
+      const int c = wn * (BN / 2) + b * 32 + l32;
+      const int n = n0 + c;
+      if (n < p.Nout) {
+        float* dst = p.part + ((long long)tm_idx * p.Nout + n) * 2;
+        dst[0] = mean_b[b];
+        dst[1] = red[c] + red[BN + c];
+      }
+    }
+  }
+}
+
+// Sum split-K slabs, add bias, store, and emit BatchNorm partials over RB-row groups.
+// Thread = one output column of a 64-column strip; 4 row lanes x RB/4 rows.
+constexpr int RB = 32;
+__global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restrict__ slab, int S, int M, int Nout,
+                                                            const float* __restrict__ bias, float* __restrict__ y,
+                                                            float* __restrict__ part) {
+  __shared__ float red[4][64];
+  const int col = threadIdx.x & 63;
+  const int rl = threadIdx.x >> 6;
+  const int n = blockIdx.x * 64 + col;
+  const int y0 = blockIdx.y * RB;
+  const bool nok = n < Nout;
+  const float bv = (bias && nok) ? bias[n] : 0.f;
+  float v[RB / 4];
+  const long long plane = (long long)M * Nout;
+#pragma unroll
+  for (int i = 0; i < RB / 4; ++i) {
+    const int m = y0 + rl + 4 * i;
+    float s = 0.f;
+    if (m < M && nok) {
+      const float* src = slab + (long long)m * Nout + n;
+      for (int z = 0; z < S; ++z) s += src[z * plane];
+      s += bv;
+      y[(long long)m * Nout + n] = s;
+    }
+    v[i] = s;
+  }
+  if (!part) return;
+  const int cnt = min(RB, M - y0);
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < RB / 4; ++i) s += (y0 + rl + 4 * i < M) ? v[i] : 0.f;
+  red[rl][col] = s;
+  __syncthreads();
+  const float mean = (red[0][col] + red[1][col] + red[2][col] + red[3][col]) / (float)cnt;
+  __syncthreads();
+  s = 0.f;
+#pragma unroll
+  for (int i = 0; i < RB / 4; ++i) {
+    const float d = v[i] - mean;
+    s += (y0 + rl + 4 * i < M) ? d * d : 0.f;
+  }
+  red[rl][col] = s;
+  __syncthreads();
+  if (rl == 0 && nok) {
+    float* dst = part + ((long long)blockIdx.y * Nout + n) * 2;
+    dst[0] = mean;
+    dst[1] = red[0][col] + red[1][col] + red[2][col] + red[3][col];
+  }
+}
+
+template <int BM, int BN, bool FAST, bool DGRAD>
+void launch_igemm(const ConvGemmParams& p, int ntiles, hipStream_t st) {
+  hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, FAST, DGRAD>), dim3(ntiles * p.splits), dim3(256), 0, st, p);
+}
+
+template <bool FAST, bool DGRAD>
+void dispatch_tile(const ConvGemmParams& p, int bm, int bn, hipStream_t st) {
+  const int ntm = (p.M + bm - 1) / bm, ntn = (p.Nout + bn - 1) / bn;
+  const int nt = ntm * ntn;
+  if (bm == 128 && bn == 128) launch_igemm<128, 128, FAST, DGRAD>(p, nt, st);
+  else if (bm == 128 && bn == 64) launch_igemm<128, 64, FAST, DGRAD>(p, nt, st);
+  else if (bm == 64 && bn == 128) launch_igemm<64, 128, FAST, DGRAD>(p, nt, st);
+  else launch_igemm<64, 64, FAST, DGRAD>(p, nt, st);
+}
+
+}  // namespace
+
+int conv_igemm_rows_per_part(int bm) { return bm; }
+int splitk_rows_per_part() { return RB; }
+
+void conv_igemm_launch(const ConvGemmParams& p, int bm, int bn, bool dgrad, hipStream_t st) {
+  const bool fast = (p.C % BK) == 0 && (p.Kdim % BK) == 0;
+  if (fast) {
+    if (dgrad) dispatch_tile<true, true>(p, bm, bn, st);
+    else dispatch_tile<true, false>(p, bm, bn, st);
+  } else {
+    if (dgrad) dispatch_tile<false, true>(p, bm, bn, st);
+    else dispatch_tile<false, false>(p, bm, bn, st);
+  }
+}
+
+void splitk_reduce_launch(const float* slab, int S, int M, int Nout, const float* bias, float* y, float* part,
+                          hipStream_t st) {
+  dim3 grid((Nout + 63) / 64, (M + RB - 1) / RB);
+  hipLaunchKernelGGL(splitk_reduce_kernel, grid, dim3(256), 0, st, slab, S, M, Nout, bias, y, part);
+}
+
+}  // namespace cdp

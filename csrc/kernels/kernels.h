@@ -1,0 +1,79 @@
+// Host-side launch API of the gfx950 kernels. Every launcher is asynchronous on the given
+// stream, allocates nothing and never synchronises, so any sequence of them can be captured
+// into a hipGraph (cdna_hip_programming.md Guideline 9).
+#pragma once
+#include <hip/hip_runtime.h>
+
+namespace cdp {
+
+struct ConvGemmParams {
+  const float* x;     // gather source, NHWC [N][H][W][C]
+  const float* w;     // B^T rows [Nout][Kdim], Kdim ordered (kh, kw, c)
+  float* y;           // [M][Nout] output, or split-K slab base [splits][M][Nout]
+  const float* bias;  // [Nout] or nullptr (ignored when splits > 1)
+  float* part;        // BN partials [ceil(M/BM)][Nout][2] (mean, M2) or nullptr
+  int N, H, W, C;     // source dims
+  int P, Q;           // GEMM-row spatial dims: rows m = (n, p, q)
+  int KH, KW, stride, pad;
+  int Nout, M, Kdim, ktiles, splits;
+};
+
+struct WgradParams {
+  const float* dy;  // [M][Cout]
+  const float* x;   // NHWC [N][H][W][C]
+  float* out;       // slab base [splits][Cout][Kdim]
+  int N, H, W, C, P, Q, KH, KW, stride, pad;
+  int Cout, Kdim, M, splits;
+};
+
+// conv_igemm.hip
+void conv_igemm_launch(const ConvGemmParams& p, int bm, int bn, bool dgrad, hipStream_t st);
+void splitk_reduce_launch(const float* slab, int S, int M, int Nout, const float* bias, float* y, float* part,
+                          hipStream_t st);
+int splitk_rows_per_part();
+
+// wgrad.hip
+void wgrad_launch(const WgradParams& p, hipStream_t st);
+void slab_sum_launch(const float* slab, int S, long long n, float* dst, bool accumulate, hipStream_t st);
+
+// bn.hip
+int bn_bwd_grid(int N, int H, int W, int C, bool pool);
+void bn_finalize_launch(const float* part, int nparts, int rpp, int M, int C, const float* gamma, const float* beta,
+                        float* running_mean, float* running_var, long long* nbt, float momentum, float eps,
+                        float* stats, hipStream_t st);
+void bn_eval_stats_launch(int C, const float* gamma, const float* beta, const float* rm, const float* rv, float eps,
+                          float* stats, hipStream_t st);
+void bn_act_fwd_launch(const float* y, const float* stats, const float* res, float* out, int N, int H, int W, int C,
+                       bool pool, bool relu, hipStream_t st);
+void bn_bwd_reduce_launch(const float* y, const float* gout, const float* stats, float* part, int nblocks, int N,
+                          int H, int W, int C, bool pool, bool relu, const float* zout, hipStream_t st);
+void chan_finalize_launch(const float* part, int nparts, int C, float* out, float* g0, float* g1, bool accumulate,
+                          hipStream_t st);
+void bn_bwd_apply_launch(const float* y, const float* gout, const float* stats, const float* sums, float* dy,
+                         float* dbias_part, int nblocks, int N, int H, int W, int C, bool pool, bool relu,
+                         const float* zout, float* dres, hipStream_t st);
+
+// misc.hip
+void xent_fwd_launch(const float* logits, const long long* tgt, int B, int C, float* loss, long long* correct,
+                     float* sum_out, hipStream_t st);
+void xent_bwd_launch(const float* logits, const long long* tgt, const float* gscale, int B, int C, float* dlogits,
+                     hipStream_t st);
+void sgd_launch(float* p, const float* g, float* buf, long long n, const float* lr_ptr, float lr, float momentum,
+                float dampening, float wd, float grad_scale, bool nesterov, bool first, bool maximize,
+                hipStream_t st);
+void augment_launch(const unsigned char* imgs, const long long* idx, long long idx_off, int B, int H, int W, int C,
+                    const float* mean, const float* inv_std, int pad, bool flip, const long long* counter,
+                    unsigned long long seed, float* out, hipStream_t st);
+void counter_inc_launch(long long* c, hipStream_t st);
+void wtrans_launch(const float* w, float* wt, int Co, int T, int Ci, hipStream_t st);
+void stack_mean_launch(const float* const* srcs, int k, long long n, float* dst, hipStream_t st);
+void scale_launch(float* x, long long n, float a, hipStream_t st);
+void colsum_launch(const float* x, int R, int C, float* out, bool accumulate, hipStream_t st);
+void avgpool_fwd_launch(const float* x, int N, int HW, int C, float* y, hipStream_t st);
+void avgpool_bwd_launch(const float* gy, int N, int HW, int C, float* gx, hipStream_t st);
+void maxpool_fwd_launch(const float* x, int N, int H, int W, int C, int k, int s, int p, int Ho, int Wo, float* y,
+                        int* arg, hipStream_t st);
+void maxpool_bwd_launch(const float* gy, const int* arg, int N, int H, int W, int C, int Ho, int Wo, float* gx,
+                        hipStream_t st);
+
+}  // namespace cdp

@@ -1,0 +1,356 @@
+// Small fused kernels: softmax cross-entropy (fwd / bwd / accuracy), fused SGD, CIFAR-style
+// augmentation, weight transpose for conv data-gradients, stack-mean for the gather/scatter
+// strategy, and generic scale / channel-sum helpers. gfx950, wave64.
+//
+// Reference anchors:
+//   CrossEntropyLoss            /root/reference/src/Part 1/main.py:110,39
+//   accuracy (max(1), eq, sum)  /root/reference/src/Part 1/main.py:70-71
+//   optim.SGD(lr .1, mom .9, wd 1e-4)   /root/reference/src/Part 1/main.py:114-115
+//   RandomCrop(32,4)+HFlip+Normalize    /root/reference/src/Part 1/main.py:82-93
+//   torch.mean(torch.stack(inputs), 0)  /root/reference/src/Part 2a/main.py:122
+#include "common.h"
+#include "kernels.h"
+
+namespace cdp {
+namespace {
+
+// ------------------------------------------------------------------ cross-entropy
+// One block. Each wave owns rows w, w+4, ...; per-row loss = logsumexp - logit[target].
+// Writes mean loss (and the number of correct top-1 predictions when `correct` != null).
+__global__ __launch_bounds__(256) void xent_fwd_kernel(const float* __restrict__ logits, const long long* __restrict__ tgt,
+                                                      int B, int C, float* __restrict__ loss,
+                                                      long long* __restrict__ correct, float* __restrict__ sum_out) {
+  __shared__ double red[4];
+  __shared__ int redc[4];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  double acc = 0.0;
+  int nc = 0;
+  for (int r = wid; r < B; r += 4) {
+    const float* row = logits + (long long)r * C;
+    float mx = -INFINITY;
+    int am = 0x7fffffff;
+    for (int c = lane; c < C; c += 64) {
+      const float v = row[c];
+      if (v > mx) { mx = v; am = c; }
+    }
+    // wave argmax: larger value wins, ties -> smaller index (first occurrence)
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const float omx = __shfl_xor(mx, o, kWave);
+      const int oam = __shfl_xor(am, o, kWave);
+      if (omx > mx || (omx == mx && oam < am)) { mx = omx; am = oam; }
+    }
+    float se = 0.f;
+    for (int c = lane; c < C; c += 64) se += expf(row[c] - mx);
+    se = wave_sum(se);
+    if (lane == 0) {
+      const long long t = tgt[r];
+      const bool tok = t >= 0 && t < C;  // out-of-range targets poison the loss instead of reading OOB
+      acc += tok ? (double)(logf(se) + mx - row[t]) : (double)NAN;
+      nc += (tok && am == (int)t) ? 1 : 0;
+    }
+  }
+  if (lane == 0) {
+    red[wid] = acc;
+    redc[wid] = nc;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const double s = red[0] + red[1] + red[2] + red[3];
+    if (loss) loss[0] = (float)(s / (double)B);
+    if (sum_out) sum_out[0] = (float)s;
+    if (correct) correct[0] += redc[0] + redc[1] + redc[2] + redc[3];
+  }
+}
+
+// dlogits = (softmax - onehot) * gscale[0] / B
+__global__ __launch_bounds__(256) void xent_bwd_kernel(const float* __restrict__ logits, const long long* __restrict__ tgt,
+                                                      const float* __restrict__ gscale, int B, int C,
+                                                      float* __restrict__ dlogits) {
+  const int lane = threadIdx.x & 63;
+  const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= B) return;
+  const float* row = logits + (long long)r * C;
+  float mx = -INFINITY;
+  for (int c = lane; c < C; c += 64) mx = fmaxf(mx, row[c]);
+  mx = wave_max(mx);
+  float se = 0.f;
+  for (int c = lane; c < C; c += 64) se += expf(row[c] - mx);
+  se = wave_sum(se);
+  const float k = gscale[0] / (float)B;
+  const float inv = 1.f / se;
+  const long long t = tgt[r];
+  for (int c = lane; c < C; c += 64) {
+    const float sm = expf(row[c] - mx) * inv;
+    dlogits[(long long)r * C + c] = (sm - (c == t ? 1.f : 0.f)) * k;
+  }
+}
+
+// ------------------------------------------------------------------ SGD (torch semantics)
+// d_p = g*gs (+wd*p); buf = first ? d_p : buf*m + (1-damp)*d_p; d_p = nesterov ? d_p + m*buf : buf;
+// p -= lr*d_p. Op order and fma placement follow ATen's add(alpha) (fmadd) so results match
+// torch.optim.SGD to the last ulp on the same inputs.
+__device__ __forceinline__ void sgd_one(float& p, float g, float& b, float lr, float m, float damp, float wd, float gs,
+                                        bool nesterov, bool first, bool maximize, bool has_mom) {
+  float d = g * gs;
+  if (maximize) d = -d;
+  if (wd != 0.f) d = fmaf(p, wd, d);
+  if (has_mom) {
+    if (first) b = d;
+    else b = fmaf(d, 1.f - damp, b * m);
+    d = nesterov ? fmaf(b, m, d) : b;
+  }
+  p = fmaf(d, -lr, p);
+}
+
+__global__ __launch_bounds__(256) void sgd_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ buf,
+                                                 long long n, const float* __restrict__ lr_ptr, float lr_host, float m,
+                                                 float damp, float wd, float gs, int flags) {
+  const bool nesterov = flags & 1, first = flags & 2, maximize = flags & 4, has_mom = flags & 8;
+  const float lr = lr_ptr ? lr_ptr[0] : lr_host;
+  const long long n4 = n >> 2;
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  float dummy = 0.f;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
+    float4 pv = ld4(p + 4 * i);
+    const float4 gv = ld4(g + 4 * i);
+    float4 bv = has_mom && !first ? ld4(buf + 4 * i) : f4zero();
+    sgd_one(pv.x, gv.x, bv.x, lr, m, damp, wd, gs, nesterov, first, maximize, has_mom);
+    sgd_one(pv.y, gv.y, bv.y, lr, m, damp, wd, gs, nesterov, first, maximize, has_mom);
+    sgd_one(pv.z, gv.z, bv.z, lr, m, damp, wd, gs, nesterov, first, maximize, has_mom);
+    sgd_one(pv.w, gv.w, bv.w, lr, m, damp, wd, gs, nesterov, first, maximize, has_mom);
+    st4(p + 4 * i, pv);
+    if (has_mom) st4(buf + 4 * i, bv);
+  }
+  if (blockIdx.x == 0 && threadIdx.x < (n & 3)) {
+    const long long i = (n4 << 2) + threadIdx.x;
+    float bb = has_mom && !first ? buf[i] : 0.f;
+    float pp = p[i];
+    sgd_one(pp, g[i], has_mom ? bb : dummy, lr, m, damp, wd, gs, nesterov, first, maximize, has_mom);
+    p[i] = pp;
+    if (has_mom) buf[i] = bb;
+  }
+}
+
+// ------------------------------------------------------------------ augmentation
+__device__ __forceinline__ unsigned long long splitmix64(unsigned long long x) {
+  x += 0x9E3779B97F4A7C15ull;
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+  return x ^ (x >> 31);
+}
+
+// out[b][h][w][c] (NHWC fp32) from uint8 HWC images[idx[b]], with optional RandomCrop(pad) and
+// RandomHorizontalFlip(0.5) drawn from a counter-based hash of (seed, *counter, b), then
+// ToTensor (/255) and Normalize(mean, std). Padding is zero in uint8 space (torchvision fill=0).
+__global__ __launch_bounds__(256) void augment_kernel(const unsigned char* __restrict__ imgs,
+                                                     const long long* __restrict__ idx, long long idx_off, int B,
+                                                     int H, int W, int C, float m0, float m1, float m2, float is0,
+                                                     float is1, float is2, int pad, int flip,
+                                                     const long long* __restrict__ counter, unsigned long long seed,
+                                                     float* __restrict__ out) {
+  const int b = blockIdx.y;
+  if (b >= B) return;
+  const long long src_i = idx ? idx[idx_off + b] : (idx_off + b);
+  const unsigned long long ctr = counter ? (unsigned long long)counter[0] : 0ull;
+  const unsigned long long r = splitmix64(seed ^ splitmix64(ctr * 0x100000001B3ull + (unsigned long long)b));
+  const int span = 2 * pad + 1;
+  const int oy = pad ? (int)(r % span) - pad : 0;
+  const int ox = pad ? (int)((r >> 16) % span) - pad : 0;
+  const bool fl = flip && ((r >> 40) & 1);
+  const unsigned char* src = imgs + src_i * (long long)H * W * C;
+  const float mean[3] = {m0, m1, m2};
+  const float istd[3] = {is0, is1, is2};
+  const int total = H * W * C;
+  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < total; e += gridDim.x * blockDim.x) {
+    const int c = e % C;
+    const int w = (e / C) % W;
+    const int h = e / (C * W);
+    const int ww = fl ? (W - 1 - w) : w;  // flip applied after the crop (torchvision order)
+    const int sh = h + oy, sw = ww + ox;
+    float v = 0.f;
+    if ((unsigned)sh < (unsigned)H && (unsigned)sw < (unsigned)W) v = (float)src[(sh * W + sw) * C + c] * (1.f / 255.f);
+    const int ci = c < 3 ? c : 2;
+    out[(long long)b * total + e] = (v - mean[ci]) * istd[ci];
+  }
+}
+
+__global__ void counter_inc_kernel(long long* c) { c[0] += 1; }
+
+// ------------------------------------------------------------------ weight transpose
+// W[co][tap][ci] -> Wt[ci][tap][co]   (tap = kh*KW+kw; conv data-gradient uses Wt as its B^T)
+__global__ __launch_bounds__(256) void wtrans_kernel(const float* __restrict__ w, float* __restrict__ wt, int Co,
+                                                     int T, int Ci) {
+  __shared__ float tile[32][33];
+  const int tap = blockIdx.z;
+  const int co0 = blockIdx.y * 32, ci0 = blockIdx.x * 32;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 32 x 8
+  for (int j = ty; j < 32; j += 8) {
+    const int co = co0 + j, ci = ci0 + tx;
+    tile[j][tx] = (co < Co && ci < Ci) ? w[((long long)co * T + tap) * Ci + ci] : 0.f;
+  }
+  __syncthreads();
+  for (int j = ty; j < 32; j += 8) {
+    const int ci = ci0 + j, co = co0 + tx;
+    if (ci < Ci && co < Co) wt[((long long)ci * T + tap) * Co + co] = tile[tx][j];
+  }
+}
+
+// ------------------------------------------------------------------ stack mean / scale / colsum
+__global__ __launch_bounds__(256) void stack_mean_kernel(const float* const* __restrict__ srcs, int k, long long n,
+                                                         float* __restrict__ dst) {
+  const float inv = 1.f / (float)k;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+    float s = 0.f;
+    for (int j = 0; j < k; ++j) s += srcs[j][i];
+    dst[i] = s * inv;
+  }
+}
+
+__global__ __launch_bounds__(256) void scale_kernel(float* __restrict__ x, long long n, float a) {
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x)
+    x[i] *= a;
+}
+
+// out[c] (+)= sum_r x[r][c]   (Linear bias gradient)
+__global__ __launch_bounds__(256) void colsum_kernel(const float* __restrict__ x, int R, int C, float* __restrict__ out,
+                                                     int accumulate) {
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int rl = threadIdx.x >> 6;
+  __shared__ float red[4][64];
+  float s = 0.f;
+  if (c < C)
+    for (int r = rl; r < R; r += 4) s += x[(long long)r * C + c];
+  red[rl][threadIdx.x & 63] = s;
+  __syncthreads();
+  if (rl == 0 && c < C) {
+    const float t = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
+    out[c] = accumulate ? out[c] + t : t;
+  }
+}
+
+// global average pool over HW of NHWC -> [N][C]; and its backward
+__global__ __launch_bounds__(256) void avgpool_fwd_kernel(const float* __restrict__ x, int N, int HW, int C,
+                                                          float* __restrict__ y) {
+  const long long total = (long long)N * C;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long long)gridDim.x * blockDim.x) {
+    const int c = (int)(i % C);
+    const long long n = i / C;
+    float s = 0.f;
+    for (int k = 0; k < HW; ++k) s += x[(n * HW + k) * C + c];
+    y[i] = s / (float)HW;
+  }
+}
+__global__ __launch_bounds__(256) void avgpool_bwd_kernel(const float* __restrict__ gy, int N, int HW, int C,
+                                                          float* __restrict__ gx) {
+  const long long total = (long long)N * HW * C;
+  const float inv = 1.f / (float)HW;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long long)gridDim.x * blockDim.x) {
+    const int c = (int)(i % C);
+    const long long n = i / ((long long)HW * C);
+    gx[i] = gy[n * C + c] * inv;
+  }
+}
+
+// MaxPool2d(k, s, p) forward on NHWC with int32 argmax (flat h*W+w), and backward (scatter-add).
+__global__ __launch_bounds__(256) void maxpool_fwd_kernel(const float* __restrict__ x, int N, int H, int W, int C,
+                                                          int k, int s, int pd, int Ho, int Wo, float* __restrict__ y,
+                                                          int* __restrict__ arg) {
+  const long long total = (long long)N * Ho * Wo * C;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long long)gridDim.x * blockDim.x) {
+    const int c = (int)(i % C);
+    long long t = i / C;
+    const int wo = (int)(t % Wo);
+    t /= Wo;
+    const int ho = (int)(t % Ho);
+    const int n = (int)(t / Ho);
+    float mx = -INFINITY;
+    int am = -1;
+    for (int dh = 0; dh < k; ++dh)
+      for (int dw = 0; dw < k; ++dw) {
+        const int h = ho * s - pd + dh, w = wo * s - pd + dw;
+        if ((unsigned)h >= (unsigned)H || (unsigned)w >= (unsigned)W) continue;
+        const float v = x[(((long long)n * H + h) * W + w) * C + c];
+        if (v > mx || am < 0) { mx = v; am = h * W + w; }
+      }
+    y[i] = mx;
+    arg[i] = am;
+  }
+}
+__global__ __launch_bounds__(256) void maxpool_bwd_kernel(const float* __restrict__ gy, const int* __restrict__ arg,
+                                                          int N, int H, int W, int C, int Ho, int Wo,
+                                                          float* __restrict__ gx) {
+  const long long total = (long long)N * Ho * Wo * C;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long long)gridDim.x * blockDim.x) {
+    const int c = (int)(i % C);
+    const long long n = i / ((long long)Ho * Wo * C);
+    atomicAdd(gx + ((n * H * W) + arg[i]) * C + c, gy[i]);
+  }
+}
+
+int grid_for(long long n) {
+  long long b = (n + 255) / 256;
+  if (b > 4096) b = 4096;
+  if (b < 1) b = 1;
+  return (int)b;
+}
+
+}  // namespace
+
+void xent_fwd_launch(const float* logits, const long long* tgt, int B, int C, float* loss, long long* correct,
+                     float* sum_out, hipStream_t st) {
+  hipLaunchKernelGGL(xent_fwd_kernel, dim3(1), dim3(256), 0, st, logits, tgt, B, C, loss, correct, sum_out);
+}
+void xent_bwd_launch(const float* logits, const long long* tgt, const float* gscale, int B, int C, float* dlogits,
+                     hipStream_t st) {
+  hipLaunchKernelGGL(xent_bwd_kernel, dim3((B + 3) / 4), dim3(256), 0, st, logits, tgt, gscale, B, C, dlogits);
+}
+void sgd_launch(float* p, const float* g, float* buf, long long n, const float* lr_ptr, float lr, float momentum,
+                float dampening, float wd, float grad_scale, bool nesterov, bool first, bool maximize,
+                hipStream_t st) {
+  const int flags = (nesterov ? 1 : 0) | (first ? 2 : 0) | (maximize ? 4 : 0) | (momentum != 0.f ? 8 : 0);
+  hipLaunchKernelGGL(sgd_kernel, dim3(grid_for((n + 3) / 4)), dim3(256), 0, st, p, g, buf, n, lr_ptr, lr, momentum,
+                     dampening, wd, grad_scale, flags);
+}
+void augment_launch(const unsigned char* imgs, const long long* idx, long long idx_off, int B, int H, int W, int C,
+                    const float* mean, const float* inv_std, int pad, bool flip, const long long* counter,
+                    unsigned long long seed, float* out, hipStream_t st) {
+  const int total = H * W * C;
+  dim3 grid((total + 255) / 256, B);
+  hipLaunchKernelGGL(augment_kernel, grid, dim3(256), 0, st, imgs, idx, idx_off, B, H, W, C, mean[0], mean[1],
+                     mean[2], inv_std[0], inv_std[1], inv_std[2], pad, flip ? 1 : 0, counter, seed, out);
+}
+void counter_inc_launch(long long* c, hipStream_t st) {
+  hipLaunchKernelGGL(counter_inc_kernel, dim3(1), dim3(1), 0, st, c);
+}
+void wtrans_launch(const float* w, float* wt, int Co, int T, int Ci, hipStream_t st) {
+  dim3 grid((Ci + 31) / 32, (Co + 31) / 32, T);
+  hipLaunchKernelGGL(wtrans_kernel, grid, dim3(256), 0, st, w, wt, Co, T, Ci);
+}
+void stack_mean_launch(const float* const* srcs, int k, long long n, float* dst, hipStream_t st) {
+  hipLaunchKernelGGL(stack_mean_kernel, dim3(grid_for(n)), dim3(256), 0, st, srcs, k, n, dst);
+}
+void scale_launch(float* x, long long n, float a, hipStream_t st) {
+  hipLaunchKernelGGL(scale_kernel, dim3(grid_for(n)), dim3(256), 0, st, x, n, a);
+}
+void colsum_launch(const float* x, int R, int C, float* out, bool accumulate, hipStream_t st) {
+  hipLaunchKernelGGL(colsum_kernel, dim3((C + 63) / 64), dim3(256), 0, st, x, R, C, out, accumulate ? 1 : 0);
+}
+void avgpool_fwd_launch(const float* x, int N, int HW, int C, float* y, hipStream_t st) {
+  hipLaunchKernelGGL(avgpool_fwd_kernel, dim3(grid_for((long long)N * C)), dim3(256), 0, st, x, N, HW, C, y);
+}
+void avgpool_bwd_launch(const float* gy, int N, int HW, int C, float* gx, hipStream_t st) {
+  hipLaunchKernelGGL(avgpool_bwd_kernel, dim3(grid_for((long long)N * HW * C)), dim3(256), 0, st, gy, N, HW, C, gx);
+}
+void maxpool_fwd_launch(const float* x, int N, int H, int W, int C, int k, int s, int p, int Ho, int Wo, float* y,
+                        int* arg, hipStream_t st) {
+  hipLaunchKernelGGL(maxpool_fwd_kernel, dim3(grid_for((long long)N * Ho * Wo * C)), dim3(256), 0, st, x, N, H, W, C,
+                     k, s, p, Ho, Wo, y, arg);
+}
+void maxpool_bwd_launch(const float* gy, const int* arg, int N, int H, int W, int C, int Ho, int Wo, float* gx,
+                        hipStream_t st) {
+  hipLaunchKernelGGL(maxpool_bwd_kernel, dim3(grid_for((long long)N * Ho * Wo * C)), dim3(256), 0, st, gy, arg, N, H,
+                     W, C, Ho, Wo, gx);
+}
+
+}  // namespace cdp

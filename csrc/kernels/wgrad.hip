@@ -1,0 +1,205 @@
+// Convolution weight-gradient on fp32-input MFMA (v_mfma_f32_32x32x2_f32), gfx950.
+//
+//   dW[co][(kh,kw,c)] = sum_m dY[m][co] * Xcol[m][(kh,kw,c)]     m = (n, p, q)
+//
+// This is the autograd weight-gradient of nn.Conv2d used by every reference stage
+// (/root/reference/src/Part 1/main.py:40 `loss.backward()`), with the long reduction over
+// N*P*Q split across workgroups (split-K) into fp32 slabs that a second kernel sums straight into
+// the flat gradient arena (optionally accumulating, for gradient accumulation).
+//
+// Tile: 128 (co) x 128 (k) x 32 (m), 256 threads = 2x2 waves of 64x64. Both operands are staged
+// m-major ([m][co] and [m][k]) exactly as they sit in memory, so no transpose is needed: an MFMA
+// operand lane (i, h) reads row m = 2s + h, column i -- 32 consecutive floats per half-wave,
+// conflict-free ds_read_b32.
+#include "common.h"
+#include "kernels.h"
+
+namespace cdp {
+namespace {
+
+constexpr int WBM = 128, WBN = 128, WBK = 32;
+constexpr int WLD = WBM + 4;
+
+template <bool FAST>
+__global__ __launch_bounds__(256, 2) void wgrad_kernel(WgradParams p) {
+  constexpr int STAGE = WBK * WLD * 2;  // A tile + B tile
+  __shared__ __attribute__((aligned(16))) float smem[2 * STAGE];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid >> 1, wn = wid & 1;
+
+  const int ntn = (p.Kdim + WBN - 1) / WBN;
+  const int ntm = (p.Cout + WBM - 1) / WBM;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  // tile (tm, tn) fastest, split slowest: blocks of one split share the dY/X row window in L2
+  const int tile = bid % (ntm * ntn);
+  const int split = bid / (ntm * ntn);
+  const int tm_idx = tile / ntn, tn_idx = tile % ntn;
+  const int co0 = tm_idx * WBM, r0 = tn_idx * WBN;
+  const int mt_total = (p.M + WBK - 1) / WBK;
+  const int kt_begin = (int)(((long long)split * mt_total) / p.splits);
+  const int kt_end = (int)(((long long)(split + 1) * mt_total) / p.splits);
+  const int PQ = p.P * p.Q;
+
+  // A (dY) tile: 32 rows x 128 cols = 1024 float4; thread -> rows tid/32 + 8i, col4 tid%32
+  // B (Xcol) tile: same geometry over k.
+  float4 ra[4], rb[4];
+  const int c4 = tid & 31;
+  // per-thread B column decode (fixed for the whole kernel): k = r0 + 4*c4 .. +3
+  const int kcol = r0 + c4 * 4;
+  int b_kh = 0, b_kw = 0, b_c = 0;
+  bool b_kok = kcol < p.Kdim;
+  if (FAST && b_kok) {
+    const int tap = kcol / p.C;
+    b_c = kcol - tap * p.C;
+    b_kh = tap / p.KW;
+    b_kw = tap - b_kh * p.KW;
+  }
+
+  auto load_tile = [&](int kt) {
+    const int mb = kt * WBK;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int m = mb + (tid >> 5) + 8 * i;
+      const bool mok = m < p.M;
+      const int co = co0 + c4 * 4;
+      if (FAST) {
+        ra[i] = (mok && co < p.Cout) ? ld4(p.dy + (long long)m * p.Cout + co) : f4zero();
+      } else {
+        float e[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) e[j] = (mok && co + j < p.Cout) ? p.dy[(long long)m * p.Cout + co + j] : 0.f;
+        ra[i] = make_float4(e[0], e[1], e[2], e[3]);
+      }
+      const int mm = mok ? m : 0;
+      const int n = mm / PQ;
+      const int rem = mm - n * PQ;
+      const int pp = rem / p.Q, qq = rem - (rem / p.Q) * p.Q;
+      const int ih0 = pp * p.stride - p.pad, iw0 = qq * p.stride - p.pad;
+      const float* xb = p.x + (long long)n * p.H * p.W * p.C;
+      if (FAST) {
+        const int ih = ih0 + b_kh, iw = iw0 + b_kw;
+        const bool ok = mok && b_kok && (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W;
+        rb[i] = ok ? ld4(xb + ((long long)ih * p.W + iw) * p.C + b_c) : f4zero();
+      } else {
+        float e[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int k = kcol + j;
+          float v = 0.f;
+          if (mok && k < p.Kdim) {
+            const int tap = k / p.C;
+            const int c = k - tap * p.C;
+            const int kh = tap / p.KW, kw = tap - (tap / p.KW) * p.KW;
+            const int ih = ih0 + kh, iw = iw0 + kw;
+            if ((unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W)
+              v = xb[((long long)ih * p.W + iw) * p.C + c];
+          }
+          e[j] = v;
+        }
+        rb[i] = make_float4(e[0], e[1], e[2], e[3]);
+      }
+    }
+  };
+  auto store_tile = [&](float* st) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int row = (tid >> 5) + 8 * i;
+      st4(st + row * WLD + c4 * 4, ra[i]);
+      st4(st + WBK * WLD + row * WLD + c4 * 4, rb[i]);
+    }
+  };
+
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
+
+  const int l32 = lane & 31, hh = lane >> 5;
+  if (kt_begin < kt_end) {
+    load_tile(kt_begin);
+    store_tile(smem);
+    __syncthreads();
+    for (int kt = kt_begin; kt < kt_end; ++kt) {
+      const int cur = (kt - kt_begin) & 1;
+      const bool more = kt + 1 < kt_end;
+      if (more) load_tile(kt + 1);
+      const float* As = smem + cur * STAGE;
+      const float* Bs = As + WBK * WLD;
+#pragma unroll
+      for (int s = 0; s < WBK / 2; ++s) {
+        const int row = 2 * s + hh;
+        float af[2], bf[2];
+#pragma unroll
+        for (int a = 0; a < 2; ++a) af[a] = As[row * WLD + wm * 64 + a * 32 + l32];
+#pragma unroll
+        for (int b = 0; b < 2; ++b) bf[b] = Bs[row * WLD + wn * 64 + b * 32 + l32];
+#pragma unroll
+        for (int a = 0; a < 2; ++a)
+#pragma unroll
+          for (int b = 0; b < 2; ++b)
+            acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[a], bf[b], acc[a][b], 0, 0, 0);
+      }
+      if (more) store_tile(smem + (cur ^ 1) * STAGE);
+      __syncthreads();
+    }
+  }
+
+  float* out = p.out + (long long)split * p.Cout * p.Kdim;
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+      const int k = r0 + wn * 64 + b * 32 + l32;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int co = co0 + wm * 64 + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
+        if (co < p.Cout && k < p.Kdim) out[(long long)co * p.Kdim + k] = acc[a][b][r];
+      }
+    }
+}
+
+// dst[i] = (accumulate ? dst[i] : 0) + sum_z slab[z][i]
+__global__ __launch_bounds__(256) void slab_sum_kernel(const float* __restrict__ slab, int S, long long n,
+                                                       float* __restrict__ dst, int accumulate) {
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  if (n & 3) {  // unaligned slab planes: scalar path
+    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+      float s = accumulate ? dst[i] : 0.f;
+      for (int z = 0; z < S; ++z) s += slab[(long long)z * n + i];
+      dst[i] = s;
+    }
+    return;
+  }
+  const long long n4 = n >> 2;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
+    float4 s = accumulate ? ld4(dst + 4 * i) : f4zero();
+    for (int z = 0; z < S; ++z) {
+      const float4 v = ld4(slab + (long long)z * n + 4 * i);
+      s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+    }
+    st4(dst + 4 * i, s);
+  }
+}
+
+}  // namespace
+
+void wgrad_launch(const WgradParams& p, hipStream_t st) {
+  const int ntn = (p.Kdim + WBN - 1) / WBN;
+  const int ntm = (p.Cout + WBM - 1) / WBM;
+  const bool fast = (p.C % 4) == 0 && (p.Cout % 4) == 0;
+  dim3 grid(ntm * ntn * p.splits);
+  if (fast) hipLaunchKernelGGL(wgrad_kernel<true>, grid, dim3(256), 0, st, p);
+  else hipLaunchKernelGGL(wgrad_kernel<false>, grid, dim3(256), 0, st, p);
+}
+
+void slab_sum_launch(const float* slab, int S, long long n, float* dst, bool accumulate, hipStream_t st) {
+  long long n4 = (n + 3) / 4;
+  int blocks = (int)std::min<long long>((n4 + 255) / 256, 4096);
+  if (blocks < 1) blocks = 1;
+  hipLaunchKernelGGL(slab_sum_kernel, dim3(blocks), dim3(256), 0, st, slab, S, n, dst, accumulate ? 1 : 0);
+}
+
+}  // namespace cdp

@@ -1,0 +1,90 @@
+// Python bindings of the native runtime: kernels (ops.cpp), RCCL communicator, bucketed reducer.
+#include <torch/csrc/utils/pybind.h>
+#include <torch/extension.h>
+
+#include "ops.h"
+#include "rccl_comm.h"
+#include "reducer.h"
+
+namespace py = pybind11;
+using namespace cdp;
+
+PYBIND11_MODULE(_C, m) {
+  m.doc() = "cs744_distributed_data_parallel_amd native runtime (gfx950 kernels, RCCL comm, reducer)";
+  m.attr("ARCH") = "gfx950";
+
+  // -------------------------------------------------------------- kernels
+  m.def("conv2d_fwd", &conv2d_fwd, py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("stride"), py::arg("pad"),
+        py::arg("want_stats") = false);
+  m.def("conv2d_dgrad", &conv2d_dgrad);
+  m.def("conv2d_wgrad", &conv2d_wgrad, py::arg("dy"), py::arg("x"), py::arg("w_shape"), py::arg("stride"),
+        py::arg("pad"), py::arg("out") = py::none(), py::arg("accumulate") = false);
+  m.def("conv_bn_act_fwd", &conv_bn_act_fwd);
+  m.def("conv_bn_act_bwd", &conv_bn_act_bwd);
+  m.def("linear_fwd", &linear_fwd);
+  m.def("linear_bwd", &linear_bwd);
+  m.def("xent_fwd", &xent_fwd, py::arg("logits"), py::arg("target"), py::arg("correct") = py::none());
+  m.def("xent_bwd", &xent_bwd);
+  m.def("sgd_step", &sgd_step);
+  m.def("augment", &augment);
+  m.def("counter_inc", &counter_inc);
+  m.def("stack_mean", &stack_mean);
+  m.def("scale_", &scale_);
+  m.def("maxpool2d_fwd", &maxpool2d_fwd);
+  m.def("maxpool2d_bwd", &maxpool2d_bwd);
+  m.def("avgpool_fwd", &avgpool_fwd);
+  m.def("avgpool_bwd", &avgpool_bwd);
+
+  // -------------------------------------------------------------- RCCL
+  py::class_<RcclWork, std::shared_ptr<RcclWork>>(m, "RcclWork")
+      .def("wait", &RcclWork::wait)
+      .def("synchronize", &RcclWork::synchronize, py::call_guard<py::gil_scoped_release>())
+      .def("is_completed", &RcclWork::is_completed);
+
+  py::class_<RcclComm, std::shared_ptr<RcclComm>>(m, "RcclComm")
+      .def_static("unique_id", [] { return py::bytes(RcclComm::unique_id()); })
+      .def(py::init([](py::bytes uid, int rank, int world, int device, double timeout) {
+             return std::make_shared<RcclComm>(std::string(uid), rank, world, device, timeout);
+           }),
+           py::arg("uid"), py::arg("rank"), py::arg("world"), py::arg("device"), py::arg("timeout") = 1800.0,
+           py::call_guard<py::gil_scoped_release>())
+      .def_property_readonly("rank", &RcclComm::rank)
+      .def_property_readonly("size", &RcclComm::size)
+      .def_property_readonly("device", &RcclComm::device)
+      .def_property_readonly("stream_ptr", [](RcclComm& c) { return reinterpret_cast<intptr_t>(c.stream()); })
+      .def("healthy", &RcclComm::healthy)
+      .def("error", &RcclComm::error)
+      .def("abort", &RcclComm::abort)
+      .def("shutdown", &RcclComm::shutdown, py::call_guard<py::gil_scoped_release>())
+      .def("set_timeout", &RcclComm::set_timeout)
+      .def("timeout", &RcclComm::timeout)
+      .def("all_reduce", &RcclComm::all_reduce, py::arg("t"), py::arg("op") = "sum", py::arg("async_op") = false)
+      .def("broadcast", &RcclComm::broadcast, py::arg("t"), py::arg("root") = 0, py::arg("async_op") = false)
+      .def("reduce", &RcclComm::reduce, py::arg("t"), py::arg("root") = 0, py::arg("op") = "sum",
+           py::arg("async_op") = false)
+      .def("all_gather", &RcclComm::all_gather, py::arg("out"), py::arg("inp"), py::arg("async_op") = false)
+      .def("reduce_scatter", &RcclComm::reduce_scatter, py::arg("out"), py::arg("inp"), py::arg("op") = "sum",
+           py::arg("async_op") = false)
+      .def("gather", &RcclComm::gather, py::arg("t"), py::arg("outs"), py::arg("root") = 0,
+           py::arg("async_op") = false)
+      .def("scatter", &RcclComm::scatter, py::arg("t"), py::arg("ins"), py::arg("root") = 0,
+           py::arg("async_op") = false)
+      .def("all_to_all", &RcclComm::all_to_all, py::arg("out"), py::arg("inp"), py::arg("async_op") = false)
+      .def("send", &RcclComm::send, py::arg("t"), py::arg("peer"), py::arg("async_op") = false)
+      .def("recv", &RcclComm::recv, py::arg("t"), py::arg("peer"), py::arg("async_op") = false)
+      .def("barrier", &RcclComm::barrier, py::call_guard<py::gil_scoped_release>());
+
+  // -------------------------------------------------------------- reducer
+  py::class_<Reducer, std::shared_ptr<Reducer>>(m, "Reducer")
+      .def(py::init<std::vector<at::Tensor>, std::vector<at::Tensor>, std::vector<at::Tensor>, std::vector<int64_t>,
+                    std::shared_ptr<RcclComm>, c10::intrusive_ptr<c10d::ProcessGroup>, bool, bool>(),
+           py::arg("params"), py::arg("grad_views"), py::arg("bucket_views"), py::arg("bucket_starts"),
+           py::arg("rccl"), py::arg("pg"), py::arg("find_unused"), py::arg("average"))
+      .def("prepare_for_backward", &Reducer::prepare_for_backward)
+      .def("remove_hooks", &Reducer::remove_hooks)
+      .def("ready_order", &Reducer::ready_order)
+      .def("disarm", &Reducer::disarm)
+      .def_property_readonly("iterations", &Reducer::iterations)
+      .def_property_readonly("launched_total", &Reducer::launched_total)
+      .def_property_readonly("num_buckets", &Reducer::num_buckets);
+}

@@ -1,0 +1,507 @@
+// Torch-facing wrappers around the gfx950 kernels: shape checks, workspace allocation through
+// PyTorch's caching allocator (graph-capture safe), tile / split-K selection, and the fused
+// Conv -> BatchNorm -> ReLU [-> MaxPool] block used by the VGG model family
+// (/root/reference/src/Part 1/model.py:11-27).
+//
+// Layout contract: activations are logical NCHW tensors in channels_last memory format (physical
+// NHWC); conv weights are logical [Co, Ci, KH, KW] in channels_last format (physical OHWI =
+// GEMM B^T rows). Outputs follow the same contract, so every op is a drop-in for its torch.nn
+// counterpart on channels_last tensors.
+#include "ops.h"
+
+#include <c10/hip/HIPStream.h>
+#include <torch/extension.h>
+
+#include <algorithm>
+
+#include "../kernels/kernels.h"
+
+namespace cdp {
+
+namespace {
+
+hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
+
+void check_f32_cuda(const at::Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda(), name, " must be a GPU tensor");
+  TORCH_CHECK(t.scalar_type() == at::kFloat, name, " must be float32");
+}
+
+at::Tensor nhwc(const at::Tensor& t) {
+  if (t.dim() == 4 && t.is_contiguous(at::MemoryFormat::ChannelsLast)) return t;
+  return t.contiguous(at::MemoryFormat::ChannelsLast);
+}
+
+const float* fptr(const c10::optional<at::Tensor>& t) {
+  return (t.has_value() && t->defined()) ? t->data_ptr<float>() : nullptr;
+}
+float* fptr_mut(const c10::optional<at::Tensor>& t) {
+  return (t.has_value() && t->defined()) ? t->data_ptr<float>() : nullptr;
+}
+
+struct GemmPlan {
+  int bm, bn, splits, ktiles;
+};
+
+int num_cus() {
+  static int cus = [] {
+    int dev = 0;
+    hipGetDevice(&dev);
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, dev) != hipSuccess) return 256;
+    return prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
+  }();
+  return cus;
+}
+
+// Tile + split-K choice for the implicit GEMM: fill >= 2 workgroups per CU (the 128x128 tile
+// runs 2 per CU: 72 KiB LDS, 160 VGPRs), keeping >= 4 K-tiles per split.
+GemmPlan plan_gemm(long long M, int Nout, int Kdim) {
+  GemmPlan g;
+  g.ktiles = (Kdim + 31) / 32;
+  g.bn = (Nout % 128 == 0) ? 128 : 64;
+  const int target = 2 * num_cus();
+  long long tiles128 = ((M + 127) / 128) * ((Nout + g.bn - 1) / g.bn);
+  g.bm = (tiles128 >= target || M > 4096) ? 128 : 64;
+  const long long tiles = ((M + g.bm - 1) / g.bm) * ((Nout + g.bn - 1) / g.bn);
+  int s = 1;
+  if (tiles < target) {
+    s = (int)((target + tiles - 1) / tiles);
+    s = std::min(s, std::max(1, g.ktiles / 4));
+    s = std::min(s, 16);
+  }
+  g.splits = std::max(1, s);
+  return g;
+}
+
+int plan_wgrad_splits(int Cout, int Kdim, long long M) {
+  const long long tiles = ((Cout + 127) / 128) * (long long)((Kdim + 127) / 128);
+  const long long mt = (M + 31) / 32;
+  long long s = (4LL * num_cus() + tiles - 1) / tiles;
+  s = std::min<long long>(s, std::max<long long>(1, mt / 8));
+  s = std::min<long long>(s, 256);
+  return (int)std::max<long long>(1, s);
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------- conv forward
+// Returns y (channels_last [N, Cout, P, Q]). When `part` is requested the per-tile BatchNorm
+// partials are returned in a second tensor [nparts, Cout, 2] together with rows-per-part.
+std::vector<at::Tensor> conv2d_fwd(const at::Tensor& x_, const at::Tensor& w_, const c10::optional<at::Tensor>& bias,
+                                   int64_t stride, int64_t pad, bool want_stats) {
+  check_f32_cuda(x_, "x");
+  check_f32_cuda(w_, "weight");
+  TORCH_CHECK(x_.dim() == 4 && w_.dim() == 4, "conv2d_fwd expects 4-D input and weight");
+  const at::Tensor x = nhwc(x_);
+  const at::Tensor w = nhwc(w_);
+  const int N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
+  const int Co = w.size(0), KH = w.size(2), KW = w.size(3);
+  TORCH_CHECK(w.size(1) == C, "weight in-channels mismatch: ", w.size(1), " vs ", C);
+  const int P = (H + 2 * pad - KH) / stride + 1;
+  const int Q = (W + 2 * pad - KW) / stride + 1;
+  TORCH_CHECK(P > 0 && Q > 0, "empty conv output");
+  const long long M = (long long)N * P * Q;
+  TORCH_CHECK(M < (1LL << 31), "conv rows overflow int32");
+  const int Kdim = KH * KW * C;
+  auto opts = x.options();
+  at::Tensor y = at::empty({N, Co, P, Q}, opts.memory_format(at::MemoryFormat::ChannelsLast));
+  GemmPlan g = plan_gemm(M, Co, Kdim);
+  ConvGemmParams p{};
+  p.x = x.data_ptr<float>();
+  p.w = w.data_ptr<float>();
+  p.N = N; p.H = H; p.W = W; p.C = C; p.P = P; p.Q = Q;
+  p.KH = KH; p.KW = KW; p.stride = (int)stride; p.pad = (int)pad;
+  p.Nout = Co; p.M = (int)M; p.Kdim = Kdim; p.ktiles = g.ktiles; p.splits = g.splits;
+  at::Tensor part, rpp;
+  hipStream_t st = cur_stream();
+  if (g.splits == 1) {
+    p.y = y.data_ptr<float>();
+    p.bias = fptr(bias);
+    if (want_stats) {
+      const int nparts = (int)((M + g.bm - 1) / g.bm);
+      part = at::empty({nparts, Co, 2}, opts);
+      p.part = part.data_ptr<float>();
+      rpp = at::full({1}, g.bm, opts.dtype(at::kInt).device(at::kCPU));
+    }
+    conv_igemm_launch(p, g.bm, g.bn, false, st);
+  } else {
+    at::Tensor slab = at::empty({g.splits, M, Co}, opts);
+    p.y = slab.data_ptr<float>();
+    conv_igemm_launch(p, g.bm, g.bn, false, st);
+    float* partp = nullptr;
+    if (want_stats) {
+      const int rb = splitk_rows_per_part();
+      const int nparts = (int)((M + rb - 1) / rb);
+      part = at::empty({nparts, Co, 2}, opts);
+      partp = part.data_ptr<float>();
+      rpp = at::full({1}, rb, opts.dtype(at::kInt).device(at::kCPU));
+    }
+    splitk_reduce_launch(slab.data_ptr<float>(), g.splits, (int)M, Co, fptr(bias), y.data_ptr<float>(), partp, st);
+  }
+  if (want_stats) return {y, part, rpp};
+  return {y};
+}
+
+// ---------------------------------------------------------------- conv data gradient
+// dX[N, C, H, W] from dY[N, Co, P, Q] and W[Co, C, KH, KW] (any stride / padding).
+at::Tensor conv2d_dgrad(const at::Tensor& dy_, const at::Tensor& w_, std::vector<int64_t> in_shape, int64_t stride,
+                        int64_t pad) {
+  check_f32_cuda(dy_, "grad_output");
+  check_f32_cuda(w_, "weight");
+  const at::Tensor dy = nhwc(dy_);
+  const at::Tensor w = nhwc(w_);
+  const int N = in_shape[0], C = in_shape[1], H = in_shape[2], W = in_shape[3];
+  const int Co = w.size(0), KH = w.size(2), KW = w.size(3);
+  const int P = dy.size(2), Q = dy.size(3);
+  TORCH_CHECK(dy.size(1) == Co && dy.size(0) == N, "dgrad shape mismatch");
+  auto opts = dy.options();
+  hipStream_t st = cur_stream();
+  // Wt[ci][tap][co] = W[co][tap][ci]
+  at::Tensor wt = at::empty({C, KH * KW * Co}, opts);
+  wtrans_launch(w.data_ptr<float>(), wt.data_ptr<float>(), Co, KH * KW, C, st);
+  at::Tensor dx = at::empty({N, C, H, W}, opts.memory_format(at::MemoryFormat::ChannelsLast));
+  const long long M = (long long)N * H * W;
+  const int Kdim = KH * KW * Co;
+  GemmPlan g = plan_gemm(M, C, Kdim);
+  ConvGemmParams p{};
+  p.x = dy.data_ptr<float>();
+  p.w = wt.data_ptr<float>();
+  p.N = N; p.H = P; p.W = Q; p.C = Co; p.P = H; p.Q = W;
+  p.KH = KH; p.KW = KW; p.stride = (int)stride; p.pad = (int)pad;
+  p.Nout = C; p.M = (int)M; p.Kdim = Kdim; p.ktiles = g.ktiles; p.splits = g.splits;
+  if (g.splits == 1) {
+    p.y = dx.data_ptr<float>();
+    conv_igemm_launch(p, g.bm, g.bn, true, st);
+  } else {
+    at::Tensor slab = at::empty({g.splits, M, C}, opts);
+    p.y = slab.data_ptr<float>();
+    conv_igemm_launch(p, g.bm, g.bn, true, st);
+    splitk_reduce_launch(slab.data_ptr<float>(), g.splits, (int)M, C, nullptr, dx.data_ptr<float>(), nullptr, st);
+  }
+  return dx;
+}
+
+// ---------------------------------------------------------------- conv weight gradient
+// dW (channels_last [Co, C, KH, KW]); written into `out` when given (accumulating if asked).
+at::Tensor conv2d_wgrad(const at::Tensor& dy_, const at::Tensor& x_, std::vector<int64_t> w_shape, int64_t stride,
+                        int64_t pad, const c10::optional<at::Tensor>& out, bool accumulate) {
+  check_f32_cuda(dy_, "grad_output");
+  check_f32_cuda(x_, "input");
+  const at::Tensor dy = nhwc(dy_);
+  const at::Tensor x = nhwc(x_);
+  const int N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
+  const int Co = w_shape[0], KH = w_shape[2], KW = w_shape[3];
+  const int P = dy.size(2), Q = dy.size(3);
+  const long long M = (long long)N * P * Q;
+  const int Kdim = KH * KW * C;
+  auto opts = x.options();
+  at::Tensor dw;
+  if (out.has_value() && out->defined()) {
+    dw = *out;
+    TORCH_CHECK(dw.is_contiguous(at::MemoryFormat::ChannelsLast) && dw.numel() == (long long)Co * Kdim,
+                "wgrad out must be channels_last contiguous");
+  } else {
+    dw = at::empty({Co, C, KH, KW}, opts.memory_format(at::MemoryFormat::ChannelsLast));
+    accumulate = false;
+  }
+  hipStream_t st = cur_stream();
+  WgradParams p{};
+  p.dy = dy.data_ptr<float>();
+  p.x = x.data_ptr<float>();
+  p.N = N; p.H = H; p.W = W; p.C = C; p.P = P; p.Q = Q;
+  p.KH = KH; p.KW = KW; p.stride = (int)stride; p.pad = (int)pad;
+  p.Cout = Co; p.Kdim = Kdim; p.M = (int)M;
+  p.splits = plan_wgrad_splits(Co, Kdim, M);
+  if (p.splits == 1 && !accumulate) {
+    p.out = dw.data_ptr<float>();
+    wgrad_launch(p, st);
+  } else {
+    at::Tensor slab = at::empty({p.splits, Co, Kdim}, opts);
+    p.out = slab.data_ptr<float>();
+    wgrad_launch(p, st);
+    slab_sum_launch(slab.data_ptr<float>(), p.splits, (long long)Co * Kdim, dw.data_ptr<float>(), accumulate, st);
+  }
+  return dw;
+}
+
+// ---------------------------------------------------------------- fused block forward
+// out = [maxpool2](act(BN(conv3x3(x) + b) [+ residual])), training or eval BatchNorm.
+// Returns {out, y (conv output), stats [4, C] = (mean, invstd, scale, shift)}.
+std::vector<at::Tensor> conv_bn_act_fwd(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tensor>& b,
+                                        const c10::optional<at::Tensor>& gamma,
+                                        const c10::optional<at::Tensor>& beta,
+                                        const c10::optional<at::Tensor>& running_mean,
+                                        const c10::optional<at::Tensor>& running_var,
+                                        const c10::optional<at::Tensor>& num_batches_tracked, double momentum,
+                                        double eps, bool training, int64_t stride, int64_t pad, bool pool, bool relu,
+                                        const c10::optional<at::Tensor>& residual) {
+  std::vector<at::Tensor> r = conv2d_fwd(x, w, b, stride, pad, training);
+  at::Tensor y = r[0];
+  const int N = y.size(0), C = y.size(1), H = y.size(2), W = y.size(3);
+  TORCH_CHECK(C % 4 == 0, "BatchNorm channel count must be a multiple of 4");
+  auto opts = y.options();
+  at::Tensor stats = at::empty({4, C}, opts);
+  hipStream_t st = cur_stream();
+  if (training) {
+    const int nparts = r[1].size(0);
+    const int rpp = r[2].item<int>();
+    long long* nbt = nullptr;
+    if (num_batches_tracked.has_value() && num_batches_tracked->defined()) {
+      TORCH_CHECK(num_batches_tracked->scalar_type() == at::kLong, "num_batches_tracked must be int64");
+      nbt = reinterpret_cast<long long*>(num_batches_tracked->data_ptr<int64_t>());
+    }
+    bn_finalize_launch(r[1].data_ptr<float>(), nparts, rpp, N * H * W, C, fptr(gamma), fptr(beta),
+                       fptr_mut(running_mean), fptr_mut(running_var), nbt, (float)momentum, (float)eps,
+                       stats.data_ptr<float>(), st);
+  } else {
+    TORCH_CHECK(running_mean.has_value() && running_var.has_value(), "eval BatchNorm needs running stats");
+    bn_eval_stats_launch(C, fptr(gamma), fptr(beta), running_mean->data_ptr<float>(), running_var->data_ptr<float>(),
+                         (float)eps, stats.data_ptr<float>(), st);
+  }
+  at::Tensor res;
+  if (residual.has_value() && residual->defined()) {
+    TORCH_CHECK(!pool, "residual + pool not supported");
+    res = nhwc(*residual);
+  }
+  at::Tensor out = at::empty({N, C, pool ? H / 2 : H, pool ? W / 2 : W},
+                             opts.memory_format(at::MemoryFormat::ChannelsLast));
+  bn_act_fwd_launch(y.data_ptr<float>(), stats.data_ptr<float>(), res.defined() ? res.data_ptr<float>() : nullptr,
+                    out.data_ptr<float>(), N, H, W, C, pool, relu, st);
+  return {out, y, stats};
+}
+
+// ---------------------------------------------------------------- fused block backward
+// Returns {dx (undefined when !need_dx), dw, db, dgamma, dbeta, dresidual (when zout given)}.
+std::vector<at::Tensor> conv_bn_act_bwd(const at::Tensor& gout_, const at::Tensor& x, const at::Tensor& w,
+                                        const at::Tensor& y, const at::Tensor& stats, int64_t stride, int64_t pad,
+                                        bool pool, bool relu, bool need_dx, bool has_bias,
+                                        const c10::optional<at::Tensor>& zout_, bool training) {
+  check_f32_cuda(gout_, "grad_output");
+  const at::Tensor gout = nhwc(gout_);
+  const int N = y.size(0), C = y.size(1), H = y.size(2), W = y.size(3);
+  auto opts = y.options();
+  hipStream_t st = cur_stream();
+  at::Tensor zout;
+  if (zout_.has_value() && zout_->defined()) zout = nhwc(*zout_);
+  const int nblk = bn_bwd_grid(N, H, W, C, pool);
+  at::Tensor part = at::empty({nblk, C, 2}, opts);
+  bn_bwd_reduce_launch(y.data_ptr<float>(), gout.data_ptr<float>(), stats.data_ptr<float>(), part.data_ptr<float>(),
+                       nblk, N, H, W, C, pool, relu, zout.defined() ? zout.data_ptr<float>() : nullptr, st);
+  at::Tensor sums = at::empty({2, C}, opts);
+  at::Tensor dgamma = at::empty({C}, opts), dbeta = at::empty({C}, opts);
+  chan_finalize_launch(part.data_ptr<float>(), nblk, C, sums.data_ptr<float>(), dbeta.data_ptr<float>(),
+                       dgamma.data_ptr<float>(), false, st);
+  // eval-mode BatchNorm is a fixed affine map: dy = scale * dz (no batch-statistics terms)
+  if (!training) sums.zero_();
+  at::Tensor dy = at::empty({N, C, H, W}, opts.memory_format(at::MemoryFormat::ChannelsLast));
+  at::Tensor dbpart;
+  if (has_bias) dbpart = at::empty({nblk, C, 2}, opts);
+  at::Tensor dres;
+  if (zout.defined()) dres = at::empty({N, C, H, W}, opts.memory_format(at::MemoryFormat::ChannelsLast));
+  bn_bwd_apply_launch(y.data_ptr<float>(), gout.data_ptr<float>(), stats.data_ptr<float>(), sums.data_ptr<float>(),
+                      dy.data_ptr<float>(), has_bias ? dbpart.data_ptr<float>() : nullptr, nblk, N, H, W, C, pool,
+                      relu, zout.defined() ? zout.data_ptr<float>() : nullptr,
+                      dres.defined() ? dres.data_ptr<float>() : nullptr, st);
+  at::Tensor db;
+  if (has_bias) {
+    db = at::empty({C}, opts);
+    chan_finalize_launch(dbpart.data_ptr<float>(), nblk, C, nullptr, db.data_ptr<float>(), nullptr, false, st);
+  }
+  at::Tensor dx;
+  if (need_dx) dx = conv2d_dgrad(dy, w, {x.size(0), x.size(1), x.size(2), x.size(3)}, stride, pad);
+  at::Tensor dw = conv2d_wgrad(dy, x, {w.size(0), w.size(1), w.size(2), w.size(3)}, stride, pad, c10::nullopt, false);
+  return {dx, dw, db, dgamma, dbeta, dres};
+}
+
+// ---------------------------------------------------------------- linear
+// y[B, O] = x[B, I] @ W[O, I]^T + b  (1x1 implicit GEMM)
+at::Tensor linear_fwd(const at::Tensor& x_, const at::Tensor& w_, const c10::optional<at::Tensor>& b) {
+  check_f32_cuda(x_, "input");
+  check_f32_cuda(w_, "weight");
+  const at::Tensor x = x_.contiguous(), w = w_.contiguous();
+  const int B = x.size(0), I = x.size(1), O = w.size(0);
+  TORCH_CHECK(w.size(1) == I, "linear shape mismatch");
+  at::Tensor y = at::empty({B, O}, x.options());
+  GemmPlan g = plan_gemm(B, O, I);
+  ConvGemmParams p{};
+  p.x = x.data_ptr<float>();
+  p.w = w.data_ptr<float>();
+  p.N = B; p.H = 1; p.W = 1; p.C = I; p.P = 1; p.Q = 1; p.KH = 1; p.KW = 1; p.stride = 1; p.pad = 0;
+  p.Nout = O; p.M = B; p.Kdim = I; p.ktiles = g.ktiles; p.splits = g.splits;
+  hipStream_t st = cur_stream();
+  if (g.splits == 1) {
+    p.y = y.data_ptr<float>();
+    p.bias = fptr(b);
+    conv_igemm_launch(p, g.bm, g.bn, false, st);
+  } else {
+    at::Tensor slab = at::empty({g.splits, B, O}, x.options());
+    p.y = slab.data_ptr<float>();
+    conv_igemm_launch(p, g.bm, g.bn, false, st);
+    splitk_reduce_launch(slab.data_ptr<float>(), g.splits, B, O, fptr(b), y.data_ptr<float>(), nullptr, st);
+  }
+  return y;
+}
+
+// {dx, dw, db}
+std::vector<at::Tensor> linear_bwd(const at::Tensor& gy_, const at::Tensor& x_, const at::Tensor& w_, bool need_dx,
+                                   bool has_bias) {
+  const at::Tensor gy = gy_.contiguous(), x = x_.contiguous(), w = w_.contiguous();
+  const int B = x.size(0), I = x.size(1), O = w.size(0);
+  hipStream_t st = cur_stream();
+  at::Tensor dx;
+  if (need_dx) {
+    // dx[B, I] = gy[B, O] @ W[O, I]  ->  B^T = W^T [I][O]
+    at::Tensor wt = at::empty({I, O}, x.options());
+    wtrans_launch(w.data_ptr<float>(), wt.data_ptr<float>(), O, 1, I, st);
+    dx = linear_fwd(gy, wt, c10::nullopt);
+  }
+  // dW[O, I] = gy^T x  (1x1 wgrad over B rows)
+  at::Tensor dw = at::empty({O, I}, x.options());
+  WgradParams p{};
+  p.dy = gy.data_ptr<float>();
+  p.x = x.data_ptr<float>();
+  p.N = B; p.H = 1; p.W = 1; p.C = I; p.P = 1; p.Q = 1; p.KH = 1; p.KW = 1; p.stride = 1; p.pad = 0;
+  p.Cout = O; p.Kdim = I; p.M = B;
+  p.splits = plan_wgrad_splits(O, I, B);
+  if (p.splits == 1) {
+    p.out = dw.data_ptr<float>();
+    wgrad_launch(p, st);
+  } else {
+    at::Tensor slab = at::empty({p.splits, O, I}, x.options());
+    p.out = slab.data_ptr<float>();
+    wgrad_launch(p, st);
+    slab_sum_launch(slab.data_ptr<float>(), p.splits, (long long)O * I, dw.data_ptr<float>(), false, st);
+  }
+  at::Tensor db;
+  if (has_bias) {
+    db = at::empty({O}, x.options());
+    colsum_launch(gy.data_ptr<float>(), B, O, db.data_ptr<float>(), false, st);
+  }
+  return {dx, dw, db};
+}
+
+// ---------------------------------------------------------------- cross entropy
+// {loss (0-dim), correct (int64 [1], accumulated in place when given)}
+at::Tensor xent_fwd(const at::Tensor& logits_, const at::Tensor& target, const c10::optional<at::Tensor>& correct) {
+  check_f32_cuda(logits_, "logits");
+  TORCH_CHECK(target.scalar_type() == at::kLong, "target must be int64");
+  const at::Tensor logits = logits_.contiguous();
+  const at::Tensor tgt = target.contiguous();
+  const int B = logits.size(0), C = logits.size(1);
+  at::Tensor loss = at::empty({}, logits.options());
+  long long* cp = nullptr;
+  if (correct.has_value() && correct->defined()) cp = reinterpret_cast<long long*>(correct->data_ptr<int64_t>());
+  xent_fwd_launch(logits.data_ptr<float>(), reinterpret_cast<const long long*>(tgt.data_ptr<int64_t>()), B, C, loss.data_ptr<float>(), cp, nullptr,
+                  cur_stream());
+  return loss;
+}
+
+at::Tensor xent_bwd(const at::Tensor& gloss, const at::Tensor& logits_, const at::Tensor& target) {
+  const at::Tensor logits = logits_.contiguous();
+  const at::Tensor g = gloss.to(at::kFloat).contiguous();
+  const int B = logits.size(0), C = logits.size(1);
+  at::Tensor d = at::empty_like(logits);
+  xent_bwd_launch(logits.data_ptr<float>(), reinterpret_cast<const long long*>(target.contiguous().data_ptr<int64_t>()), g.data_ptr<float>(), B, C,
+                  d.data_ptr<float>(), cur_stream());
+  return d;
+}
+
+// ---------------------------------------------------------------- SGD over a flat arena
+void sgd_step(at::Tensor p, const at::Tensor& g, c10::optional<at::Tensor> buf, const c10::optional<at::Tensor>& lr_t,
+              double lr, double momentum, double dampening, double wd, double grad_scale, bool nesterov, bool first,
+              bool maximize) {
+  check_f32_cuda(p, "param");
+  TORCH_CHECK(p.is_contiguous() && g.is_contiguous() && p.numel() == g.numel(), "sgd: flat contiguous tensors required");
+  float* bp = nullptr;
+  if (momentum != 0.0) {
+    TORCH_CHECK(buf.has_value() && buf->numel() == p.numel(), "sgd: momentum buffer required");
+    bp = buf->data_ptr<float>();
+  }
+  sgd_launch(p.data_ptr<float>(), g.data_ptr<float>(), bp, p.numel(), fptr(lr_t), (float)lr, (float)momentum,
+             (float)dampening, (float)wd, (float)grad_scale, nesterov, first, maximize, cur_stream());
+}
+
+// ---------------------------------------------------------------- data augmentation
+at::Tensor augment(const at::Tensor& images, const c10::optional<at::Tensor>& indices, int64_t idx_offset, int64_t batch,
+                   std::vector<double> mean, std::vector<double> std_, int64_t pad, bool flip,
+                   const c10::optional<at::Tensor>& counter, int64_t seed, c10::optional<at::Tensor> out) {
+  TORCH_CHECK(images.is_cuda() && images.scalar_type() == at::kByte && images.dim() == 4,
+              "images must be uint8 [N, H, W, C] on the GPU");
+  const int H = images.size(1), W = images.size(2), C = images.size(3);
+  at::Tensor o;
+  if (out.has_value() && out->defined()) o = *out;
+  else
+    o = at::empty({batch, C, H, W}, images.options().dtype(at::kFloat).memory_format(at::MemoryFormat::ChannelsLast));
+  float m[3], is[3];
+  for (int i = 0; i < 3; ++i) {
+    m[i] = (float)mean[std::min<size_t>(i, mean.size() - 1)];
+    is[i] = (float)(1.0 / std_[std::min<size_t>(i, std_.size() - 1)]);
+  }
+  const long long* ip = nullptr;
+  if (indices.has_value() && indices->defined()) ip = reinterpret_cast<const long long*>(indices->data_ptr<int64_t>());
+  const long long* cp = nullptr;
+  if (counter.has_value() && counter->defined()) cp = reinterpret_cast<const long long*>(counter->data_ptr<int64_t>());
+  augment_launch(images.data_ptr<uint8_t>(), ip, idx_offset, (int)batch, H, W, C, m, is, (int)pad, flip, cp,
+                 (unsigned long long)seed, o.data_ptr<float>(), cur_stream());
+  return o;
+}
+
+void counter_inc(at::Tensor c) { counter_inc_launch(reinterpret_cast<long long*>(c.data_ptr<int64_t>()), cur_stream()); }
+
+// ---------------------------------------------------------------- misc
+void stack_mean(const std::vector<at::Tensor>& srcs, at::Tensor dst) {
+  TORCH_CHECK(!srcs.empty(), "stack_mean: empty list");
+  const int k = srcs.size();
+  std::vector<int64_t> ptrs(k);
+  for (int i = 0; i < k; ++i) {
+    TORCH_CHECK(srcs[i].is_contiguous() && srcs[i].numel() == dst.numel(), "stack_mean: shape mismatch");
+    ptrs[i] = reinterpret_cast<int64_t>(srcs[i].data_ptr<float>());
+  }
+  at::Tensor dptrs = at::tensor(ptrs, at::TensorOptions().dtype(at::kLong)).to(dst.device(), /*non_blocking=*/true);
+  stack_mean_launch(reinterpret_cast<const float* const*>(dptrs.data_ptr<int64_t>()), k, dst.numel(),
+                    dst.data_ptr<float>(), cur_stream());
+}
+
+void scale_(at::Tensor x, double a) {
+  TORCH_CHECK(x.is_contiguous(), "scale_: contiguous tensor required");
+  scale_launch(x.data_ptr<float>(), x.numel(), (float)a, cur_stream());
+}
+
+std::vector<at::Tensor> maxpool2d_fwd(const at::Tensor& x_, int64_t k, int64_t s, int64_t p) {
+  const at::Tensor x = nhwc(x_);
+  const int N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
+  const int Ho = (H + 2 * p - k) / s + 1, Wo = (W + 2 * p - k) / s + 1;
+  at::Tensor y = at::empty({N, C, Ho, Wo}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  at::Tensor arg = at::empty({N, C, Ho, Wo}, x.options().dtype(at::kInt).memory_format(at::MemoryFormat::ChannelsLast));
+  maxpool_fwd_launch(x.data_ptr<float>(), N, H, W, C, k, s, p, Ho, Wo, y.data_ptr<float>(), arg.data_ptr<int>(),
+                     cur_stream());
+  return {y, arg};
+}
+
+at::Tensor maxpool2d_bwd(const at::Tensor& gy_, const at::Tensor& arg, std::vector<int64_t> in_shape) {
+  const at::Tensor gy = nhwc(gy_);
+  const int N = in_shape[0], C = in_shape[1], H = in_shape[2], W = in_shape[3];
+  at::Tensor gx = at::zeros({N, C, H, W}, gy.options().memory_format(at::MemoryFormat::ChannelsLast));
+  maxpool_bwd_launch(gy.data_ptr<float>(), arg.data_ptr<int>(), N, H, W, C, gy.size(2), gy.size(3),
+                     gx.data_ptr<float>(), cur_stream());
+  return gx;
+}
+
+at::Tensor avgpool_fwd(const at::Tensor& x_) {
+  const at::Tensor x = nhwc(x_);
+  const int N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
+  at::Tensor y = at::empty({N, C}, x.options());
+  avgpool_fwd_launch(x.data_ptr<float>(), N, H * W, C, y.data_ptr<float>(), cur_stream());
+  return y;
+}
+
+at::Tensor avgpool_bwd(const at::Tensor& gy_, std::vector<int64_t> in_shape) {
+  const at::Tensor gy = gy_.contiguous();
+  const int N = in_shape[0], C = in_shape[1], H = in_shape[2], W = in_shape[3];
+  at::Tensor gx = at::empty({N, C, H, W}, gy.options().memory_format(at::MemoryFormat::ChannelsLast));
+  avgpool_bwd_launch(gy.data_ptr<float>(), N, H * W, C, gx.data_ptr<float>(), cur_stream());
+  return gx;
+}
+
+}  // namespace cdp

@@ -1,0 +1,45 @@
+#pragma once
+#include <ATen/ATen.h>
+#include <c10/util/Optional.h>
+
+#include <vector>
+
+namespace cdp {
+
+std::vector<at::Tensor> conv2d_fwd(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tensor>& bias,
+                                   int64_t stride, int64_t pad, bool want_stats);
+at::Tensor conv2d_dgrad(const at::Tensor& dy, const at::Tensor& w, std::vector<int64_t> in_shape, int64_t stride,
+                        int64_t pad);
+at::Tensor conv2d_wgrad(const at::Tensor& dy, const at::Tensor& x, std::vector<int64_t> w_shape, int64_t stride,
+                        int64_t pad, const c10::optional<at::Tensor>& out, bool accumulate);
+std::vector<at::Tensor> conv_bn_act_fwd(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tensor>& b,
+                                        const c10::optional<at::Tensor>& gamma, const c10::optional<at::Tensor>& beta,
+                                        const c10::optional<at::Tensor>& running_mean,
+                                        const c10::optional<at::Tensor>& running_var,
+                                        const c10::optional<at::Tensor>& num_batches_tracked, double momentum,
+                                        double eps, bool training, int64_t stride, int64_t pad, bool pool, bool relu,
+                                        const c10::optional<at::Tensor>& residual);
+std::vector<at::Tensor> conv_bn_act_bwd(const at::Tensor& gout, const at::Tensor& x, const at::Tensor& w,
+                                        const at::Tensor& y, const at::Tensor& stats, int64_t stride, int64_t pad,
+                                        bool pool, bool relu, bool need_dx, bool has_bias,
+                                        const c10::optional<at::Tensor>& zout, bool training);
+at::Tensor linear_fwd(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tensor>& b);
+std::vector<at::Tensor> linear_bwd(const at::Tensor& gy, const at::Tensor& x, const at::Tensor& w, bool need_dx,
+                                   bool has_bias);
+at::Tensor xent_fwd(const at::Tensor& logits, const at::Tensor& target, const c10::optional<at::Tensor>& correct);
+at::Tensor xent_bwd(const at::Tensor& gloss, const at::Tensor& logits, const at::Tensor& target);
+void sgd_step(at::Tensor p, const at::Tensor& g, c10::optional<at::Tensor> buf, const c10::optional<at::Tensor>& lr_t,
+              double lr, double momentum, double dampening, double wd, double grad_scale, bool nesterov, bool first,
+              bool maximize);
+at::Tensor augment(const at::Tensor& images, const c10::optional<at::Tensor>& indices, int64_t idx_offset, int64_t batch,
+                   std::vector<double> mean, std::vector<double> std_, int64_t pad, bool flip,
+                   const c10::optional<at::Tensor>& counter, int64_t seed, c10::optional<at::Tensor> out);
+void counter_inc(at::Tensor c);
+void stack_mean(const std::vector<at::Tensor>& srcs, at::Tensor dst);
+void scale_(at::Tensor x, double a);
+std::vector<at::Tensor> maxpool2d_fwd(const at::Tensor& x, int64_t k, int64_t s, int64_t p);
+at::Tensor maxpool2d_bwd(const at::Tensor& gy, const at::Tensor& arg, std::vector<int64_t> in_shape);
+at::Tensor avgpool_fwd(const at::Tensor& x);
+at::Tensor avgpool_bwd(const at::Tensor& gy, std::vector<int64_t> in_shape);
+
+}  // namespace cdp

@@ -1,0 +1,110 @@
+// Native RCCL communicator: one per process/GPU, its own high-priority HIP stream, stream-ordered
+// collectives, and a watchdog thread that aborts the communicator when a collective outlives
+// its timeout (the reference has no failure detection at all: a dead rank hangs gloo forever,
+// SURVEY.md §5.3).
+#pragma once
+#include <ATen/ATen.h>
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <atomic>
+#include <chrono>
+#include <deque>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+namespace cdp {
+
+class RcclComm;
+
+// A pooled HIP event, returned to its communicator's pool when the last owner drops it.
+// Holds only a weak reference so the watchdog's pending list never owns the communicator.
+struct PooledEvent {
+  PooledEvent(std::weak_ptr<RcclComm> c, hipEvent_t e) : comm(std::move(c)), ev(e) {}
+  ~PooledEvent();
+  std::weak_ptr<RcclComm> comm;
+  hipEvent_t ev;
+};
+
+// Completion handle of an asynchronous collective.
+class RcclWork {
+ public:
+  RcclWork(std::shared_ptr<RcclComm> comm, std::shared_ptr<PooledEvent> done, std::vector<at::Tensor> keep)
+      : comm_(std::move(comm)), done_(std::move(done)), keep_(std::move(keep)) {}
+  // Make the caller's current stream wait for the collective (no host block).
+  void wait();
+  // Block the host until the collective finished (raises on communicator failure / timeout).
+  void synchronize();
+  bool is_completed();
+
+ private:
+  std::shared_ptr<RcclComm> comm_;
+  std::shared_ptr<PooledEvent> done_;
+  std::vector<at::Tensor> keep_;  // keeps the buffers alive until the work is dropped
+};
+
+class RcclComm : public std::enable_shared_from_this<RcclComm> {
+ public:
+  static std::string unique_id();
+  RcclComm(const std::string& uid, int rank, int world, int device, double timeout_s);
+  ~RcclComm();
+
+  int rank() const { return rank_; }
+  int size() const { return world_; }
+  int device() const { return device_; }
+  hipStream_t stream() const { return stream_; }
+  bool healthy() const { return !failed_.load(); }
+  std::string error() const;
+  void abort(const std::string& why);
+  void set_timeout(double s) { timeout_s_ = s; }
+  double timeout() const { return timeout_s_.load(); }
+  void shutdown();
+
+  std::shared_ptr<RcclWork> all_reduce(at::Tensor t, const std::string& op, bool async);
+  std::shared_ptr<RcclWork> broadcast(at::Tensor t, int root, bool async);
+  std::shared_ptr<RcclWork> reduce(at::Tensor t, int root, const std::string& op, bool async);
+  std::shared_ptr<RcclWork> all_gather(at::Tensor out, at::Tensor in, bool async);
+  std::shared_ptr<RcclWork> reduce_scatter(at::Tensor out, at::Tensor in, const std::string& op, bool async);
+  std::shared_ptr<RcclWork> gather(at::Tensor t, std::vector<at::Tensor> outs, int root, bool async);
+  std::shared_ptr<RcclWork> scatter(at::Tensor t, std::vector<at::Tensor> ins, int root, bool async);
+  std::shared_ptr<RcclWork> all_to_all(at::Tensor out, at::Tensor in, bool async);
+  std::shared_ptr<RcclWork> send(at::Tensor t, int peer, bool async);
+  std::shared_ptr<RcclWork> recv(at::Tensor t, int peer, bool async);
+  void barrier();
+
+  hipEvent_t get_event();
+  void put_event(hipEvent_t e);
+  void check() const;
+
+ private:
+  hipStream_t begin();  // order the comm stream after the current stream; returns current stream
+  std::shared_ptr<RcclWork> end(hipStream_t cur, bool async, std::vector<at::Tensor> keep, const char* what);
+  void watchdog_loop();
+
+  ncclComm_t comm_ = nullptr;
+  int rank_, world_, device_;
+  hipStream_t stream_ = nullptr;
+  hipEvent_t start_ev_ = nullptr;
+  std::mutex mu_;
+  std::mutex ev_mu_;
+  std::vector<hipEvent_t> free_events_;
+
+  struct Pending {
+    std::shared_ptr<PooledEvent> ev;
+    std::chrono::steady_clock::time_point t0;
+    std::string what;
+  };
+  std::mutex wd_mu_;
+  std::deque<Pending> pending_;
+  std::thread wd_thread_;
+  std::atomic<bool> stop_{false};
+  std::atomic<bool> failed_{false};
+  std::atomic<double> timeout_s_;
+  mutable std::mutex err_mu_;
+  std::string err_;
+};
+
+}  // namespace cdp

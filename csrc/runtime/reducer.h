@@ -1,0 +1,61 @@
+#pragma once
+#include <ATen/ATen.h>
+#include <torch/csrc/autograd/function.h>
+#include <torch/csrc/distributed/c10d/ProcessGroup.hpp>
+
+#include <memory>
+#include <mutex>
+#include <vector>
+
+#include "rccl_comm.h"
+
+namespace cdp {
+
+class Reducer {
+ public:
+  // params[i] / grad_views[i]: parameter i and its arena-backed gradient view.
+  // bucket_views[b]: flat arena range of bucket b (launch order), covering parameter indices
+  // [bucket_starts[b], bucket_starts[b+1]) (either direction).
+  Reducer(std::vector<at::Tensor> params, std::vector<at::Tensor> grad_views, std::vector<at::Tensor> bucket_views,
+          std::vector<int64_t> bucket_starts, std::shared_ptr<RcclComm> rccl, c10::intrusive_ptr<c10d::ProcessGroup> pg,
+          bool find_unused, bool average);
+  ~Reducer();
+
+  void prepare_for_backward(const std::vector<at::Tensor>& outputs);
+  void mark_ready(size_t i);
+  void finalize();
+  void remove_hooks();
+  std::vector<int64_t> ready_order() const;
+  int64_t iterations() const { return iterations_; }
+  int64_t launched_total() const { return launched_total_; }
+  int num_buckets() const { return (int)bucket_views_.size(); }
+  void disarm() {
+    std::lock_guard<std::mutex> g(mu_);
+    armed_ = false;
+  }
+
+ private:
+  void reset_state();
+  void mark_ready_locked(size_t i, bool from_hook);
+  void launch(int b);
+
+  std::vector<at::Tensor> params_, grad_views_, bucket_views_;
+  std::shared_ptr<RcclComm> rccl_;
+  c10::intrusive_ptr<c10d::ProcessGroup> pg_;
+  bool find_unused_, average_;
+  int world_ = 1;
+  std::vector<int> bucket_of_, bucket_size_, pending_;
+  std::vector<char> ready_flag_;
+  std::vector<std::shared_ptr<RcclWork>> works_;
+  std::vector<c10::intrusive_ptr<c10d::Work>> pg_works_;
+  std::vector<std::shared_ptr<torch::autograd::Node>> accumulators_;
+  std::vector<uintptr_t> hook_keys_;
+  std::vector<size_t> unused_;
+  std::vector<int64_t> order_;
+  mutable std::mutex mu_;
+  int next_launch_ = 0;
+  bool armed_ = false, callback_queued_ = false, record_order_ = true, have_order_ = false;
+  int64_t iterations_ = 0, launched_total_ = 0;
+};
+
+}  // namespace cdp

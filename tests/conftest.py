@@ -1,0 +1,31 @@
+import os
+import sys
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if REPO not in sys.path:
+    sys.path.insert(0, REPO)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (gfx950) GPU and the native extension")
+    config.addinivalue_line("markers", "slow: multi-process / long-running test")
+
+
+def _gpu_ok():
+    try:
+        import torch
+
+        return torch.cuda.is_available()
+    except Exception:
+        return False
+
+
+def pytest_collection_modifyitems(config, items):
+    if _gpu_ok():
+        return
+    skip = pytest.mark.skip(reason="no GPU available")
+    for it in items:
+        if "gpu" in it.keywords:
+            it.add_marker(skip)
