@@ -45,7 +45,15 @@ def parse():
     return p.parse_args()
 
 
+def _dbg(msg):
+    if os.environ.get("CDP_BENCH_DEBUG"):
+        print(f"[bench] {msg}", file=sys.stderr, flush=True)
+
+
 def main():
+    import faulthandler
+
+    faulthandler.enable()
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -118,8 +126,9 @@ def main():
     n_eager_warm = max(3, args.warmup)
     for i in range(n_eager_warm):
         step(i)
-        loss = body()
+        body()
     torch.cuda.synchronize()
+    _dbg("eager warmup done")
 
     graph = None
     use_graph = not args.no_graph and args.strategy in ("ddp", "bucketed_overlap")
@@ -132,10 +141,12 @@ def main():
                     body()
             torch.cuda.current_stream().wait_stream(s)
             torch.cuda.synchronize()
+            _dbg("side-stream warmup done")
             graph = torch.cuda.CUDAGraph()
             with torch.cuda.graph(graph):
                 static_loss = body()
             torch.cuda.synchronize()
+            _dbg("captured")
             for i in range(2):  # warm replays
                 step(i)
                 graph.replay()

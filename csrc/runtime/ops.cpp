@@ -482,7 +482,9 @@ std::vector<at::Tensor> maxpool2d_fwd(const at::Tensor& x_, int64_t k, int64_t s
 at::Tensor maxpool2d_bwd(const at::Tensor& gy_, const at::Tensor& arg, std::vector<int64_t> in_shape) {
   const at::Tensor gy = nhwc(gy_);
   const int N = in_shape[0], C = in_shape[1], H = in_shape[2], W = in_shape[3];
-  at::Tensor gx = at::zeros({N, C, H, W}, gy.options().memory_format(at::MemoryFormat::ChannelsLast));
+  // at::zeros ignores TensorOptions::memory_format -> allocate channels_last explicitly, then clear
+  at::Tensor gx = at::empty({N, C, H, W}, gy.options().memory_format(at::MemoryFormat::ChannelsLast));
+  gx.zero_();
   maxpool_bwd_launch(gy.data_ptr<float>(), arg.data_ptr<int>(), N, H, W, C, gy.size(2), gy.size(3),
                      gx.data_ptr<float>(), cur_stream());
   return gx;
