@@ -193,10 +193,11 @@ def scatter(tensor, scatter_list: Optional[List[torch.Tensor]] = None, src: int 
 
 
 def all_gather(tensor_list: List[torch.Tensor], tensor, group=None, async_op=False):
-    out = torch.empty((len(tensor_list),) + tuple(tensor.shape), dtype=tensor.dtype, device=tensor.device)
-    communicator_for(tensor).all_gather(out, tensor.contiguous())
+    inp = tensor.contiguous().reshape(-1)
+    out = torch.empty(len(tensor_list) * inp.numel(), dtype=tensor.dtype, device=tensor.device)
+    communicator_for(tensor).all_gather(out, inp)
     for i, t in enumerate(tensor_list):
-        t.copy_(out[i])
+        t.copy_(out[i * inp.numel() : (i + 1) * inp.numel()].view_as(t))
 
 
 def all_gather_into_tensor(output, tensor, group=None, async_op=False):

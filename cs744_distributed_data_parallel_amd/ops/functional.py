@@ -32,6 +32,14 @@ def use_native(*tensors) -> bool:
     return _native.require(*tensors)
 
 
+def _slot(p, needed: bool):
+    """Arena view to write ``p``'s gradient into directly (None -> let the kernel allocate)."""
+    if not needed or p is None:
+        return None
+    a = getattr(p, "_cdp_arena", None)
+    return a.claim(p) if a is not None else None
+
+
 def _bn_momentum(bn) -> float:
     return -1.0 if bn.momentum is None else float(bn.momentum)
 
@@ -45,6 +53,7 @@ class _ConvBNAct(torch.autograd.Function):
             x, w, b, gamma, beta, rm, rv, nbt, momentum, eps, training, stride, pad, pool, relu, residual
         )
         ctx.cfg = (stride, pad, pool, relu, training, b is not None, residual is not None)
+        ctx.params = (w, b, gamma, beta)
         zout = out if residual is not None else None
         ctx.save_for_backward(x, w, y, stats, zout)
         return out
@@ -54,8 +63,11 @@ class _ConvBNAct(torch.autograd.Function):
         x, w, y, stats, zout = ctx.saved_tensors
         stride, pad, pool, relu, training, has_bias, has_res = ctx.cfg
         C = _native.lib()
+        wp, bp, gp, betap = ctx.params
+        nig = ctx.needs_input_grad
         dx, dw, db, dgamma, dbeta, dres = C.conv_bn_act_bwd(
-            gout, x, w, y, stats, stride, pad, pool, relu, ctx.needs_input_grad[0], has_bias, zout, training
+            gout, x, w, y, stats, stride, pad, pool, relu, nig[0], has_bias, zout, training,
+            _slot(wp, nig[1]), _slot(bp, nig[2] and has_bias), _slot(gp, nig[3]), _slot(betap, nig[4]),
         )
         return (
             dx if ctx.needs_input_grad[0] else None,
@@ -114,12 +126,16 @@ class _Linear(torch.autograd.Function):
     def forward(ctx, x, w, b):
         ctx.save_for_backward(x, w)
         ctx.has_bias = b is not None
+        ctx.params = (w, b)
         return _native.lib().linear_fwd(x, w, b)
 
     @staticmethod
     def backward(ctx, gy):
         x, w = ctx.saved_tensors
-        dx, dw, db = _native.lib().linear_bwd(gy, x, w, ctx.needs_input_grad[0], ctx.has_bias)
+        wp, bp = ctx.params
+        nig = ctx.needs_input_grad
+        dx, dw, db = _native.lib().linear_bwd(gy, x, w, nig[0], ctx.has_bias, _slot(wp, nig[1]),
+                                              _slot(bp, nig[2] and ctx.has_bias))
         return (dx if ctx.needs_input_grad[0] else None), dw, (db if ctx.has_bias else None)
 
 

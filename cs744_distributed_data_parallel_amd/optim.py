@@ -81,11 +81,11 @@ class SGD(Optimizer):
 
     # ------------------------------------------------------------------ zero_grad
     def zero_grad(self, set_to_none: bool = True):
-        if self._arena is not None and self._arena.grad is not None:
-            # in-place: keeps p.grad as arena views (zero-copy bucketed all-reduce)
-            self._arena.zero_grad()
-            return
+        # set_to_none (torch's default) lets the next backward's kernels write each gradient straight
+        # into its arena slot, which autograd then adopts as p.grad without a copy (FlatArena.claim).
         super().zero_grad(set_to_none=set_to_none)
+        if self._arena is not None:
+            self._arena.reset_claims()
 
     # ------------------------------------------------------------------ step
     @torch.no_grad()
@@ -118,6 +118,8 @@ class SGD(Optimizer):
         rng = None
         if arena is not None and len(params) == len(group["params"]):
             rng = arena.contiguous_range(params)
+            if rng is not None:
+                arena.ensure_grads_in_arena(params)
         if rng is not None and m != 0.0:
             # momentum buffers must be the arena's views (first step: buf = d_p)
             firsts = self._first_flags(params)

@@ -56,6 +56,7 @@ class FlatArena:
             p.data = v
         self.grad = None
         self.momentum = None
+        self.claimed = [False] * len(params)
         if with_grad:
             self.attach_grads()
         for i, p in enumerate(params):
@@ -86,6 +87,38 @@ class FlatArena:
                 v.copy_(p.grad)
             p.grad = v
         return self.grad
+
+    # ------------------------------------------------------------------ direct-write gradient slots
+    def claim(self, p) -> torch.Tensor | None:
+        """Arena slot for a kernel to write ``p``'s gradient into directly.
+
+        Valid only while ``p.grad is None`` (after ``zero_grad(set_to_none=True)``): the returned view is
+        handed to autograd as the gradient, and AccumulateGrad *steals* it (no copy, no add), so
+        ``p.grad`` ends up as the arena view. Each slot is claimed at most once per iteration (a
+        parameter used twice gets a fresh tensor for its second use and autograd sums them).
+        """
+        i = p._cdp_index
+        if self.grad is None or p.grad is not None or self.claimed[i]:
+            return None
+        self.claimed[i] = True
+        return _view_like(self.grad, self.offsets[i], p.data)
+
+    def reset_claims(self):
+        self.claimed = [False] * len(self.params)
+
+    def ensure_grads_in_arena(self, params=None) -> bool:
+        """Make every ``p.grad`` (of ``params``) its arena view, copying foreign tensors in."""
+        ok = True
+        for p in (params if params is not None else self.params):
+            if p.grad is None:
+                ok = False
+                continue
+            i = p._cdp_index
+            v = _view_like(self.grad, self.offsets[i], p.data)
+            if p.grad.data_ptr() != v.data_ptr():
+                v.copy_(p.grad)
+                p.grad = v
+        return ok
 
     def grad_views(self) -> List[torch.Tensor]:
         return [_view_like(self.grad, off, p.data) for p, off in zip(self.params, self.offsets)]
@@ -152,8 +185,11 @@ class FlatArena:
             if old_mom is not None:
                 _view_like(self.momentum, n_off, p.data).copy_(_view_like(old_mom, o_off, p.data))
             p._cdp_index = new_i
+        self.claimed = [False] * len(params)
         if old_grad is not None:
-            self.attach_grads()
+            for p, off in zip(self.params, self.offsets):
+                if p.grad is not None:
+                    p.grad = _view_like(self.grad, off, p.data)
         for cb in getattr(self, "_relayout_callbacks", []):
             cb(self)
 

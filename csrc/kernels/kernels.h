@@ -35,6 +35,8 @@ int splitk_rows_per_part();
 // wgrad.hip
 void wgrad_launch(const WgradParams& p, hipStream_t st);
 void slab_sum_launch(const float* slab, int S, long long n, float* dst, bool accumulate, hipStream_t st);
+void slab_sum_strided_launch(const float* slab, int S, long long n_src, int src_cols, int dst_cols, float* dst,
+                             bool accumulate, hipStream_t st);
 
 // bn.hip
 int bn_bwd_grid(int N, int H, int W, int C, bool pool);

@@ -15,51 +15,78 @@ namespace cdp {
 namespace {
 
 // ------------------------------------------------------------------ cross-entropy
-// One block. Each wave owns rows w, w+4, ...; per-row loss = logsumexp - logit[target].
-// Writes mean loss (and the number of correct top-1 predictions when `correct` != null).
-__global__ __launch_bounds__(256) void xent_fwd_kernel(const float* __restrict__ logits, const long long* __restrict__ tgt,
-                                                      int B, int C, float* __restrict__ loss,
-                                                      long long* __restrict__ correct, float* __restrict__ sum_out) {
-  __shared__ double red[4];
-  __shared__ int redc[4];
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+// One block of 1024 threads. Narrow rows (C <= 64, e.g. CIFAR's 10 classes): one row per thread;
+// wide rows (ImageNet's 1000): one row per wave. Per-row loss = logsumexp - logit[target]; the mean
+// (fp64 block reduction, deterministic) and the top-1 correct count are written once.
+__global__ __launch_bounds__(1024) void xent_fwd_kernel(const float* __restrict__ logits, const long long* __restrict__ tgt,
+                                                       int B, int C, float* __restrict__ loss,
+                                                       long long* __restrict__ correct, float* __restrict__ sum_out) {
+  __shared__ double red[16];
+  __shared__ int redc[16];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   double acc = 0.0;
   int nc = 0;
-  for (int r = wid; r < B; r += 4) {
-    const float* row = logits + (long long)r * C;
-    float mx = -INFINITY;
-    int am = 0x7fffffff;
-    for (int c = lane; c < C; c += 64) {
-      const float v = row[c];
-      if (v > mx) { mx = v; am = c; }
-    }
-    // wave argmax: larger value wins, ties -> smaller index (first occurrence)
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-      const float omx = __shfl_xor(mx, o, kWave);
-      const int oam = __shfl_xor(am, o, kWave);
-      if (omx > mx || (omx == mx && oam < am)) { mx = omx; am = oam; }
-    }
-    float se = 0.f;
-    for (int c = lane; c < C; c += 64) se += expf(row[c] - mx);
-    se = wave_sum(se);
-    if (lane == 0) {
+  if (C <= 64) {
+    for (int r = tid; r < B; r += 1024) {
+      const float* row = logits + (long long)r * C;
+      float mx = row[0];
+      int am = 0;
+      for (int c = 1; c < C; ++c) {
+        const float v = row[c];
+        if (v > mx) { mx = v; am = c; }
+      }
+      float se = 0.f;
+      for (int c = 0; c < C; ++c) se += expf(row[c] - mx);
       const long long t = tgt[r];
       const bool tok = t >= 0 && t < C;  // out-of-range targets poison the loss instead of reading OOB
       acc += tok ? (double)(logf(se) + mx - row[t]) : (double)NAN;
       nc += (tok && am == (int)t) ? 1 : 0;
     }
+  } else {
+    for (int r = wid; r < B; r += 16) {
+      const float* row = logits + (long long)r * C;
+      float mx = -INFINITY;
+      int am = 0x7fffffff;
+      for (int c = lane; c < C; c += 64) {
+        const float v = row[c];
+        if (v > mx) { mx = v; am = c; }
+      }
+      // wave argmax: larger value wins, ties -> smaller index (first occurrence)
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) {
+        const float omx = __shfl_xor(mx, o, kWave);
+        const int oam = __shfl_xor(am, o, kWave);
+        if (omx > mx || (omx == mx && oam < am)) { mx = omx; am = oam; }
+      }
+      float se = 0.f;
+      for (int c = lane; c < C; c += 64) se += expf(row[c] - mx);
+      se = wave_sum(se);
+      if (lane == 0) {
+        const long long t = tgt[r];
+        const bool tok = t >= 0 && t < C;
+        acc += tok ? (double)(logf(se) + mx - row[t]) : (double)NAN;
+        nc += (tok && am == (int)t) ? 1 : 0;
+      }
+    }
   }
+  acc = wave_sum_d(acc);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) nc += __shfl_xor(nc, o, kWave);
   if (lane == 0) {
     red[wid] = acc;
     redc[wid] = nc;
   }
   __syncthreads();
-  if (threadIdx.x == 0) {
-    const double s = red[0] + red[1] + red[2] + red[3];
+  if (tid == 0) {
+    double s = 0.0;
+    long long n = 0;
+    for (int i = 0; i < 16; ++i) {
+      s += red[i];
+      n += redc[i];
+    }
     if (loss) loss[0] = (float)(s / (double)B);
     if (sum_out) sum_out[0] = (float)s;
-    if (correct) correct[0] += redc[0] + redc[1] + redc[2] + redc[3];
+    if (correct) correct[0] += n;
   }
 }
 
@@ -299,7 +326,7 @@ int grid_for(long long n) {
 
 void xent_fwd_launch(const float* logits, const long long* tgt, int B, int C, float* loss, long long* correct,
                      float* sum_out, hipStream_t st) {
-  hipLaunchKernelGGL(xent_fwd_kernel, dim3(1), dim3(256), 0, st, logits, tgt, B, C, loss, correct, sum_out);
+  hipLaunchKernelGGL(xent_fwd_kernel, dim3(1), dim3(1024), 0, st, logits, tgt, B, C, loss, correct, sum_out);
 }
 void xent_bwd_launch(const float* logits, const long long* tgt, const float* gscale, int B, int C, float* dlogits,
                      hipStream_t st) {

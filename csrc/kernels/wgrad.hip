@@ -161,26 +161,40 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(WgradParams p) {
     }
 }
 
-// dst[i] = (accumulate ? dst[i] : 0) + sum_z slab[z][i]
-__global__ __launch_bounds__(256) void slab_sum_kernel(const float* __restrict__ slab, int S, long long n,
-                                                       float* __restrict__ dst, int accumulate) {
-  const long long stride = (long long)gridDim.x * blockDim.x;
-  if (n & 3) {  // unaligned slab planes: scalar path
-    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-      float s = accumulate ? dst[i] : 0.f;
-      for (int z = 0; z < S; ++z) s += slab[(long long)z * n + i];
-      dst[i] = s;
+// dst[r][c] = (accumulate ? dst : 0) + sum_z slab[z][r][c]  over rows x src_cols, keeping the first
+// dst_cols of each row (dst_cols < src_cols strips channel padding). Block = CB column slots x SL
+// split lanes; the SL partial sums meet in LDS, so short slabs with many splits still spread over
+// many workgroups.
+template <int CB>
+__global__ __launch_bounds__(256) void slab_sum_kernel(const float* __restrict__ slab, int S, long long n_src,
+                                                       int src_cols, int dst_cols, float* __restrict__ dst,
+                                                       int accumulate) {
+  constexpr int SL = 256 / CB;
+  __shared__ float red[SL][CB];
+  const int cl = threadIdx.x % CB, sl = threadIdx.x / CB;
+  const long long i = (long long)blockIdx.x * CB + cl;
+  float s = 0.f;
+  if (i < n_src) {
+    int z = sl;
+    for (; z + 3 * SL < S; z += 4 * SL) {
+      const float a = slab[(long long)z * n_src + i], b = slab[(long long)(z + SL) * n_src + i];
+      const float c = slab[(long long)(z + 2 * SL) * n_src + i], d = slab[(long long)(z + 3 * SL) * n_src + i];
+      s += (a + b) + (c + d);
     }
-    return;
+    for (; z < S; z += SL) s += slab[(long long)z * n_src + i];
   }
-  const long long n4 = n >> 2;
-  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
-    float4 s = accumulate ? ld4(dst + 4 * i) : f4zero();
-    for (int z = 0; z < S; ++z) {
-      const float4 v = ld4(slab + (long long)z * n + 4 * i);
-      s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+  red[sl][cl] = s;
+  __syncthreads();
+  if (sl == 0 && i < n_src) {
+    float t = 0.f;
+#pragma unroll
+    for (int k = 0; k < SL; ++k) t += red[k][cl];
+    const long long r = i / src_cols;
+    const int c = (int)(i - r * src_cols);
+    if (c < dst_cols) {
+      float* d = dst + r * dst_cols + c;
+      *d = accumulate ? *d + t : t;
     }
-    st4(dst + 4 * i, s);
   }
 }
 
@@ -196,10 +210,18 @@ void wgrad_launch(const WgradParams& p, hipStream_t st) {
 }
 
 void slab_sum_launch(const float* slab, int S, long long n, float* dst, bool accumulate, hipStream_t st) {
-  long long n4 = (n + 3) / 4;
-  int blocks = (int)std::min<long long>((n4 + 255) / 256, 4096);
-  if (blocks < 1) blocks = 1;
-  hipLaunchKernelGGL(slab_sum_kernel, dim3(blocks), dim3(256), 0, st, slab, S, n, dst, accumulate ? 1 : 0);
+  slab_sum_strided_launch(slab, S, n, 1, 1, dst, accumulate, st);
+}
+
+void slab_sum_strided_launch(const float* slab, int S, long long n_src, int src_cols, int dst_cols, float* dst,
+                             bool accumulate, hipStream_t st) {
+  if (S >= 16 && n_src < (1 << 18)) {
+    hipLaunchKernelGGL(slab_sum_kernel<16>, dim3((unsigned)((n_src + 15) / 16)), dim3(256), 0, st, slab, S, n_src,
+                       src_cols, dst_cols, dst, accumulate ? 1 : 0);
+  } else {
+    hipLaunchKernelGGL(slab_sum_kernel<64>, dim3((unsigned)((n_src + 63) / 64)), dim3(256), 0, st, slab, S, n_src,
+                       src_cols, dst_cols, dst, accumulate ? 1 : 0);
+  }
 }
 
 }  // namespace cdp

@@ -20,9 +20,13 @@ PYBIND11_MODULE(_C, m) {
   m.def("conv2d_wgrad", &conv2d_wgrad, py::arg("dy"), py::arg("x"), py::arg("w_shape"), py::arg("stride"),
         py::arg("pad"), py::arg("out") = py::none(), py::arg("accumulate") = false);
   m.def("conv_bn_act_fwd", &conv_bn_act_fwd);
-  m.def("conv_bn_act_bwd", &conv_bn_act_bwd);
+  m.def("conv_bn_act_bwd", &conv_bn_act_bwd, py::arg("gout"), py::arg("x"), py::arg("w"), py::arg("y"),
+        py::arg("stats"), py::arg("stride"), py::arg("pad"), py::arg("pool"), py::arg("relu"), py::arg("need_dx"),
+        py::arg("has_bias"), py::arg("zout") = py::none(), py::arg("training") = true, py::arg("dw_out") = py::none(),
+        py::arg("db_out") = py::none(), py::arg("dgamma_out") = py::none(), py::arg("dbeta_out") = py::none());
   m.def("linear_fwd", &linear_fwd);
-  m.def("linear_bwd", &linear_bwd);
+  m.def("linear_bwd", &linear_bwd, py::arg("gy"), py::arg("x"), py::arg("w"), py::arg("need_dx"),
+        py::arg("has_bias"), py::arg("dw_out") = py::none(), py::arg("db_out") = py::none());
   m.def("xent_fwd", &xent_fwd, py::arg("logits"), py::arg("target"), py::arg("correct") = py::none());
   m.def("xent_bwd", &xent_bwd);
   m.def("sgd_step", &sgd_step);

@@ -75,11 +75,13 @@ GemmPlan plan_gemm(long long M, int Nout, int Kdim) {
 }
 
 int plan_wgrad_splits(int Cout, int Kdim, long long M) {
+  // ~2 workgroups per CU, >= 16 K-tiles (512 rows) per split: the fp32 slab traffic
+  // (splits x Cout x Kdim x 8 B) stays well under the GEMM time.
   const long long tiles = ((Cout + 127) / 128) * (long long)((Kdim + 127) / 128);
   const long long mt = (M + 31) / 32;
-  long long s = (4LL * num_cus() + tiles - 1) / tiles;
-  s = std::min<long long>(s, std::max<long long>(1, mt / 8));
-  s = std::min<long long>(s, 256);
+  long long s = (2LL * num_cus() + tiles - 1) / tiles;
+  s = std::min<long long>(s, std::max<long long>(1, mt / 16));
+  s = std::min<long long>(s, 128);
   return (int)std::max<long long>(1, s);
 }
 
@@ -276,7 +278,11 @@ std::vector<at::Tensor> conv_bn_act_fwd(const at::Tensor& x, const at::Tensor& w
 std::vector<at::Tensor> conv_bn_act_bwd(const at::Tensor& gout_, const at::Tensor& x, const at::Tensor& w,
                                         const at::Tensor& y, const at::Tensor& stats, int64_t stride, int64_t pad,
                                         bool pool, bool relu, bool need_dx, bool has_bias,
-                                        const c10::optional<at::Tensor>& zout_, bool training) {
+                                        const c10::optional<at::Tensor>& zout_, bool training,
+                                        const c10::optional<at::Tensor>& dw_out,
+                                        const c10::optional<at::Tensor>& db_out,
+                                        const c10::optional<at::Tensor>& dgamma_out,
+                                        const c10::optional<at::Tensor>& dbeta_out) {
   check_f32_cuda(gout_, "grad_output");
   const at::Tensor gout = nhwc(gout_);
   const int N = y.size(0), C = y.size(1), H = y.size(2), W = y.size(3);
@@ -289,7 +295,12 @@ std::vector<at::Tensor> conv_bn_act_bwd(const at::Tensor& gout_, const at::Tenso
   bn_bwd_reduce_launch(y.data_ptr<float>(), gout.data_ptr<float>(), stats.data_ptr<float>(), part.data_ptr<float>(),
                        nblk, N, H, W, C, pool, relu, zout.defined() ? zout.data_ptr<float>() : nullptr, st);
   at::Tensor sums = at::empty({2, C}, opts);
-  at::Tensor dgamma = at::empty({C}, opts), dbeta = at::empty({C}, opts);
+  // gradients go straight into the caller's slots (flat-arena views) when provided
+  auto slot = [&](const c10::optional<at::Tensor>& o, std::initializer_list<int64_t> shape, bool cl) {
+    if (o.has_value() && o->defined()) return *o;
+    return cl ? at::empty(shape, opts.memory_format(at::MemoryFormat::ChannelsLast)) : at::empty(shape, opts);
+  };
+  at::Tensor dgamma = slot(dgamma_out, {C}, false), dbeta = slot(dbeta_out, {C}, false);
   chan_finalize_launch(part.data_ptr<float>(), nblk, C, sums.data_ptr<float>(), dbeta.data_ptr<float>(),
                        dgamma.data_ptr<float>(), false, st);
   // eval-mode BatchNorm is a fixed affine map: dy = scale * dz (no batch-statistics terms)
@@ -305,12 +316,12 @@ std::vector<at::Tensor> conv_bn_act_bwd(const at::Tensor& gout_, const at::Tenso
                       dres.defined() ? dres.data_ptr<float>() : nullptr, st);
   at::Tensor db;
   if (has_bias) {
-    db = at::empty({C}, opts);
+    db = slot(db_out, {C}, false);
     chan_finalize_launch(dbpart.data_ptr<float>(), nblk, C, nullptr, db.data_ptr<float>(), nullptr, false, st);
   }
   at::Tensor dx;
   if (need_dx) dx = conv2d_dgrad(dy, w, {x.size(0), x.size(1), x.size(2), x.size(3)}, stride, pad);
-  at::Tensor dw = conv2d_wgrad(dy, x, {w.size(0), w.size(1), w.size(2), w.size(3)}, stride, pad, c10::nullopt, false);
+  at::Tensor dw = conv2d_wgrad(dy, x, {w.size(0), w.size(1), w.size(2), w.size(3)}, stride, pad, dw_out, false);
   return {dx, dw, db, dgamma, dbeta, dres};
 }
 
@@ -345,7 +356,8 @@ at::Tensor linear_fwd(const at::Tensor& x_, const at::Tensor& w_, const c10::opt
 
 // {dx, dw, db}
 std::vector<at::Tensor> linear_bwd(const at::Tensor& gy_, const at::Tensor& x_, const at::Tensor& w_, bool need_dx,
-                                   bool has_bias) {
+                                   bool has_bias, const c10::optional<at::Tensor>& dw_out,
+                                   const c10::optional<at::Tensor>& db_out) {
   const at::Tensor gy = gy_.contiguous(), x = x_.contiguous(), w = w_.contiguous();
   const int B = x.size(0), I = x.size(1), O = w.size(0);
   hipStream_t st = cur_stream();
@@ -357,7 +369,8 @@ std::vector<at::Tensor> linear_bwd(const at::Tensor& gy_, const at::Tensor& x_, 
     dx = linear_fwd(gy, wt, c10::nullopt);
   }
   // dW[O, I] = gy^T x  (1x1 wgrad over B rows)
-  at::Tensor dw = at::empty({O, I}, x.options());
+  at::Tensor dw = (dw_out.has_value() && dw_out->defined()) ? *dw_out : at::empty({O, I}, x.options());
+  TORCH_CHECK(dw.is_contiguous() && dw.numel() == (int64_t)O * I, "linear dW slot must be contiguous [O, I]");
   WgradParams p{};
   p.dy = gy.data_ptr<float>();
   p.x = x.data_ptr<float>();
@@ -375,7 +388,7 @@ std::vector<at::Tensor> linear_bwd(const at::Tensor& gy_, const at::Tensor& x_, 
   }
   at::Tensor db;
   if (has_bias) {
-    db = at::empty({O}, x.options());
+    db = (db_out.has_value() && db_out->defined()) ? *db_out : at::empty({O}, x.options());
     colsum_launch(gy.data_ptr<float>(), B, O, db.data_ptr<float>(), false, st);
   }
   return {dx, dw, db};

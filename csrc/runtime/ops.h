@@ -22,10 +22,15 @@ std::vector<at::Tensor> conv_bn_act_fwd(const at::Tensor& x, const at::Tensor& w
 std::vector<at::Tensor> conv_bn_act_bwd(const at::Tensor& gout, const at::Tensor& x, const at::Tensor& w,
                                         const at::Tensor& y, const at::Tensor& stats, int64_t stride, int64_t pad,
                                         bool pool, bool relu, bool need_dx, bool has_bias,
-                                        const c10::optional<at::Tensor>& zout, bool training);
+                                        const c10::optional<at::Tensor>& zout, bool training,
+                                        const c10::optional<at::Tensor>& dw_out,
+                                        const c10::optional<at::Tensor>& db_out,
+                                        const c10::optional<at::Tensor>& dgamma_out,
+                                        const c10::optional<at::Tensor>& dbeta_out);
 at::Tensor linear_fwd(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tensor>& b);
 std::vector<at::Tensor> linear_bwd(const at::Tensor& gy, const at::Tensor& x, const at::Tensor& w, bool need_dx,
-                                   bool has_bias);
+                                   bool has_bias, const c10::optional<at::Tensor>& dw_out,
+                                   const c10::optional<at::Tensor>& db_out);
 at::Tensor xent_fwd(const at::Tensor& logits, const at::Tensor& target, const c10::optional<at::Tensor>& correct);
 at::Tensor xent_bwd(const at::Tensor& gloss, const at::Tensor& logits, const at::Tensor& target);
 void sgd_step(at::Tensor p, const at::Tensor& g, c10::optional<at::Tensor> buf, const c10::optional<at::Tensor>& lr_t,
