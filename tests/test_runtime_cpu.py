@@ -1,0 +1,252 @@
+"""Single-process CPU tests: optimizer, flat arenas, bucket planning, data pipeline, checkpoints,
+timers/tracing, the training CLI (log-format parity) and the native extension surface."""
+import io
+import json
+import os
+import re
+from contextlib import redirect_stdout
+
+import numpy as np
+import pytest
+import torch
+
+import cs744_distributed_data_parallel_amd as cdp
+from cs744_distributed_data_parallel_amd.data import (
+    DeviceLoader,
+    DistributedSampler,
+    cifar10_binary,
+    synthetic_cifar10,
+)
+from cs744_distributed_data_parallel_amd.parallel.buckets import plan_buckets
+from cs744_distributed_data_parallel_amd.utils import FlatArena, load_checkpoint, save_checkpoint
+from cs744_distributed_data_parallel_amd.utils.profiling import TraceRecorder
+from cs744_distributed_data_parallel_amd.utils.timer import PhaseTimer
+
+
+# ----------------------------------------------------------------------------- optimizer
+@pytest.mark.parametrize("kw", [dict(momentum=0.9, weight_decay=1e-4), dict(momentum=0.9, nesterov=True),
+                                dict(momentum=0.5, dampening=0.1, weight_decay=1e-3), dict(), dict(maximize=True)])
+def test_sgd_matches_torch_reference(kw):
+    torch.manual_seed(0)
+    a = torch.nn.Linear(5, 3)
+    b = torch.nn.Linear(5, 3)
+    b.load_state_dict(a.state_dict())
+    o1 = cdp.SGD(a.parameters(), lr=0.1, **kw)
+    o2 = torch.optim.SGD(b.parameters(), lr=0.1, **kw)
+    for _ in range(4):
+        x = torch.randn(7, 5)
+        for m, o in ((a, o1), (b, o2)):
+            o.zero_grad()
+            m(x).pow(2).sum().backward()
+            o.step()
+    for p, q in zip(a.parameters(), b.parameters()):
+        assert torch.allclose(p, q, atol=1e-7)
+
+
+def test_sgd_state_dict_is_torch_compatible():
+    m = torch.nn.Linear(4, 2)
+    o = cdp.SGD(m.parameters(), lr=0.1, momentum=0.9, weight_decay=1e-4)
+    m(torch.randn(3, 4)).sum().backward()
+    o.step()
+    sd = o.state_dict()
+    g = sd["param_groups"][0]
+    assert g["lr"] == 0.1 and g["momentum"] == 0.9 and g["weight_decay"] == 1e-4 and g["dampening"] == 0
+    assert g["nesterov"] is False
+    assert set(sd["state"][0]) == {"momentum_buffer"}
+    o2 = torch.optim.SGD(torch.nn.Linear(4, 2).parameters(), lr=0.1, momentum=0.9, weight_decay=1e-4)
+    o2.load_state_dict(sd)
+
+
+def test_sgd_rejects_bad_hparams():
+    p = [torch.nn.Parameter(torch.zeros(2))]
+    with pytest.raises(ValueError):
+        cdp.SGD(p, lr=-1)
+    with pytest.raises(ValueError):
+        cdp.SGD(p, lr=0.1, nesterov=True)
+
+
+# ----------------------------------------------------------------------------- arenas
+def test_flat_arena_views_and_relayout():
+    m = cdp.VGG11()
+    before = [p.detach().clone() for p in m.parameters()]
+    ar = FlatArena(list(m.parameters()))
+    for p, b in zip(m.parameters(), before):
+        assert torch.equal(p.detach(), b)
+        assert p.data_ptr() >= ar.data.data_ptr()
+        assert p.data_ptr() % 16 == 0
+    assert m.layers[0].weight.is_contiguous(memory_format=torch.channels_last)
+    for p in m.parameters():
+        p.grad.fill_(float(p._cdp_index))
+    ar.momentum_buffer().copy_(ar.grad)
+    order = list(range(len(ar.params)))[::-1]
+    ar.relayout(order)
+    for p, b in zip(m.parameters(), before):
+        assert torch.equal(p.detach(), b)
+        assert torch.all(p.grad == float(len(order) - 1 - p._cdp_index))
+    mv = ar.momentum_views()
+    for p in m.parameters():
+        assert torch.equal(mv[p._cdp_index], p.grad)
+
+
+def test_arena_claims_once_per_iteration():
+    m = torch.nn.Linear(3, 2)
+    ar = FlatArena(list(m.parameters()))
+    for p in m.parameters():
+        p.grad = None
+    s = ar.claim(m.weight)
+    assert s is not None and s.shape == m.weight.shape
+    assert ar.claim(m.weight) is None
+    ar.reset_claims()
+    m.weight.grad = torch.zeros_like(m.weight)
+    assert ar.claim(m.weight) is None
+
+
+# ----------------------------------------------------------------------------- buckets
+def test_bucket_plan_matches_torch_assignment():
+    sizes = [6912, 256, 256, 256, 294912, 512, 512, 512, 1179648, 1024, 1024, 1024, 2359296, 1024, 1024, 1024,
+             4718592, 2048, 2048, 2048, 9437184, 2048, 2048, 2048, 9437184, 2048, 2048, 2048, 9437184, 2048, 2048,
+             2048, 20480, 40]
+    rev = sizes[::-1]
+    b = plan_buckets(rev, cap_mb=25.0, first_cap_mb=1.0)
+    assert sum(len(x) for x in b) == len(sizes)
+    tensors = [torch.empty(n // 4) for n in rev]
+    ref = torch.distributed._compute_bucket_assignment_by_size(tensors, [1024 * 1024, 25 * 1024 * 1024])
+    ref = ref[0] if isinstance(ref, tuple) else ref
+    assert [list(x) for x in b] == [list(x) for x in ref]
+
+
+# ----------------------------------------------------------------------------- data
+@pytest.mark.parametrize("n,world,shuffle,drop_last", [(50000, 2, True, False), (10, 4, True, False),
+                                                       (103, 3, False, False), (103, 3, True, True)])
+def test_distributed_sampler_matches_torch(n, world, shuffle, drop_last):
+    ds = list(range(n))
+    for r in range(world):
+        ours = DistributedSampler(ds, num_replicas=world, rank=r, shuffle=shuffle, drop_last=drop_last)
+        ref = torch.utils.data.distributed.DistributedSampler(ds, num_replicas=world, rank=r, shuffle=shuffle,
+                                                              drop_last=drop_last)
+        for ep in (0, 3):
+            ours.set_epoch(ep)
+            ref.set_epoch(ep)
+            assert list(ours) == list(ref)
+        assert len(ours) == len(ref)
+
+
+def test_reference_epoch_arithmetic():
+    ds = synthetic_cifar10(50000)
+    for w in (1, 2, 4, 8):
+        s = DistributedSampler(ds, num_replicas=w, rank=0) if w > 1 else None
+        ld = DeviceLoader(ds, int(256 / w), sampler=s)
+        assert len(ld) == 196
+
+
+def test_cpu_loader_normalisation_and_augment():
+    ds = synthetic_cifar10(32)
+    x, y = next(iter(DeviceLoader(ds, 8, train=False)))
+    ref = (ds.images[:8].permute(0, 3, 1, 2).float() / 255 - torch.tensor(ds.mean).view(1, 3, 1, 1)) / torch.tensor(
+        ds.std).view(1, 3, 1, 1)
+    assert torch.allclose(x, ref, atol=1e-6) and torch.equal(y, ds.labels[:8])
+    xa, _ = next(iter(DeviceLoader(ds, 8, train=True, seed=1)))
+    assert xa.shape == (8, 3, 32, 32)
+    assert not torch.allclose(xa, x)
+
+
+def test_cifar10_binary_reader(tmp_path):
+    d = tmp_path / "cifar-10-batches-bin"
+    d.mkdir()
+    rng = np.random.default_rng(0)
+    recs = {}
+    for f in [f"data_batch_{i}.bin" for i in range(1, 6)] + ["test_batch.bin"]:
+        a = rng.integers(0, 256, size=(3, 3073), dtype=np.uint8)
+        a[:, 0] = rng.integers(0, 10, size=3)
+        a.tofile(d / f)
+        recs[f] = a
+    tr = cifar10_binary(str(tmp_path), train=True)
+    te = cifar10_binary(str(tmp_path), train=False)
+    assert len(tr) == 15 and len(te) == 3
+    a = recs["data_batch_1.bin"]
+    assert int(tr.labels[0]) == int(a[0, 0])
+    img = a[0, 1:].reshape(3, 32, 32).transpose(1, 2, 0)
+    assert np.array_equal(tr.images[0].numpy(), img)
+
+
+# ----------------------------------------------------------------------------- checkpoint
+def test_checkpoint_roundtrip_and_torch_compat(tmp_path):
+    torch.manual_seed(0)
+    m = cdp.VGG11()
+    o = cdp.SGD(m.parameters(), lr=0.1, momentum=0.9, weight_decay=1e-4)
+    cdp.CrossEntropyLoss()(m(torch.randn(2, 3, 32, 32)), torch.tensor([1, 2])).backward()
+    o.step()
+    path = save_checkpoint(str(tmp_path / "c.pt"), m, o, epoch=3, iteration=7)
+    raw = torch.load(path, weights_only=True)
+    assert raw["epoch"] == 3 and len(raw["model"]) == 58
+    ref = cdp.VGG11(channels_last=False)
+    ref.load_state_dict(raw["model"])  # plain torch layout
+    m2 = cdp.VGG11()
+    o2 = cdp.SGD(m2.parameters(), lr=0.1, momentum=0.9, weight_decay=1e-4)
+    st = load_checkpoint(path, m2, o2)
+    assert st["iteration"] == 7
+    for a, b in zip(m.parameters(), m2.parameters()):
+        assert torch.equal(a, b)
+    ddp_sd = {"module." + k: v for k, v in raw["model"].items()}
+    torch.save({"model": ddp_sd}, str(tmp_path / "ddp.pt"))
+    m3 = cdp.VGG11()
+    load_checkpoint(str(tmp_path / "ddp.pt"), m3)  # module. prefix stripped
+    for a, b in zip(m.parameters(), m3.parameters()):
+        assert torch.equal(a, b)
+
+
+# ----------------------------------------------------------------------------- timers / tracing
+def test_phase_timer_and_trace(tmp_path):
+    t = PhaseTimer(None)
+    t.mark("start")
+    t.mark("forward")
+    t.mark("backward")
+    assert t.pop("forward") >= 0 and t.pop("backward") >= 0
+    tr = TraceRecorder(0, None)
+    with tr.phase("fwd"):
+        pass
+    p = tr.dump(str(tmp_path / "t.json"))
+    ev = json.load(open(p))["traceEvents"]
+    assert ev[0]["name"] == "fwd"
+
+
+# ----------------------------------------------------------------------------- CLI
+def test_train_cli_single_process_log_format():
+    from cs744_distributed_data_parallel_amd import train
+
+    buf = io.StringIO()
+    with redirect_stdout(buf):
+        train.main(["--epochs", "1", "--iters", "40", "--batch-size", "8", "--synthetic-size", "400",
+                    "--device", "cpu"])
+    out = buf.getvalue()
+    assert "Size of training set is 50" in out
+    assert re.search(r"Training loss after 20 iterations is \d", out)
+    assert re.search(r"Forward Pass time in iter 40 is ", out)
+    assert re.search(r"Backward Pass time in iter 40 is ", out)
+    assert re.search(r"Average Pass time in iter 40 is ", out)
+    assert "Forward Pass time in iter 20" not in out  # first window discarded like the reference
+    assert re.search(r"Training time after 1 epoch is ", out)
+    assert re.search(r"Test set: Average loss: \d+\.\d{4}, Accuracy: \d+/400 \(\d+%\)", out)
+
+
+# ----------------------------------------------------------------------------- native surface
+def test_native_extension_surface():
+    if not cdp.native_available():
+        pytest.skip("native extension not built")
+    C = cdp._native.lib()
+    for name in ["conv2d_fwd", "conv2d_dgrad", "conv2d_wgrad", "conv_bn_act_fwd", "conv_bn_act_bwd", "linear_fwd",
+                 "linear_bwd", "xent_fwd", "xent_bwd", "sgd_step", "augment", "RcclComm", "Reducer"]:
+        assert hasattr(C, name)
+    assert C.ARCH == "gfx950"
+
+
+def test_gpu_tensor_without_extension_raises(monkeypatch):
+    from cs744_distributed_data_parallel_amd import _native
+
+    class Fake:
+        is_cuda = True
+
+    monkeypatch.setattr(_native, "_C", None)
+    monkeypatch.setattr(_native, "_err", RuntimeError("missing"))
+    with pytest.raises(RuntimeError, match="native runtime"):
+        _native.require(Fake())
