@@ -48,10 +48,11 @@ PYBIND11_MODULE(_C, m) {
   py::class_<RcclComm, std::shared_ptr<RcclComm>>(m, "RcclComm")
       .def_static("unique_id", [] { return py::bytes(RcclComm::unique_id()); })
       .def(py::init([](py::bytes uid, int rank, int world, int device, double timeout) {
-             return std::make_shared<RcclComm>(std::string(uid), rank, world, device, timeout);
+             std::string id = uid;  // copy while holding the GIL
+             py::gil_scoped_release nogil;
+             return std::make_shared<RcclComm>(id, rank, world, device, timeout);
            }),
-           py::arg("uid"), py::arg("rank"), py::arg("world"), py::arg("device"), py::arg("timeout") = 1800.0,
-           py::call_guard<py::gil_scoped_release>())
+           py::arg("uid"), py::arg("rank"), py::arg("world"), py::arg("device"), py::arg("timeout") = 1800.0)
       .def_property_readonly("rank", &RcclComm::rank)
       .def_property_readonly("size", &RcclComm::size)
       .def_property_readonly("device", &RcclComm::device)
