@@ -129,6 +129,8 @@ class DistributedDataParallel(nn.Module):
         if grad_sync and self._rebuild and not self._rebuilt and self.reducer.iterations >= 1:
             self.reducer.rebuild_in_ready_order()
             self._rebuilt = True
+        if grad_sync:
+            self.reducer.rebind_if_stream_changed()
         # like torch DDP: the buffer broadcast of forward k is decided by forward k-1 (so the first
         # no-grad eval forward after training still syncs once)
         if self.broadcast_buffers and self.require_forward_param_sync:

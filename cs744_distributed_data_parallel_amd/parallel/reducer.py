@@ -185,6 +185,7 @@ class GradReducer:
         self.find_unused, self.average = find_unused_parameters, average
         self.arena_in_ready_order = arena_in_ready_order
         self._impl = None
+        self._stream = None
         self._build()
 
     # ------------------------------------------------------------------ plan
@@ -208,7 +209,11 @@ class GradReducer:
         self.bucket_starts = starts
         grad_views = a.grad_views()
         if self._impl is not None:
+            # drop every reference to the old AccumulateGrad nodes first so that fresh ones are
+            # created on the current stream (see rebind_if_stream_changed)
             self._impl.remove_hooks()
+            self._impl = None
+        self._stream = torch.cuda.current_stream(a.device) if a.device.type == "cuda" else None
         use_native = _native.available() and (
             isinstance(self.comm, RcclCommunicator) or isinstance(self.comm, TorchCommunicator)
         )
@@ -237,6 +242,22 @@ class GradReducer:
     def bucket_sizes_bytes(self) -> List[int]:
         es = self.arena.data.element_size()
         return [(e - s) * es for s, e in self.bucket_ranges]
+
+    def rebind_if_stream_changed(self) -> bool:
+        """Re-create the autograd hooks when the caller switched streams (e.g. hipGraph capture).
+
+        The reducer keeps each parameter's AccumulateGrad node alive across iterations; autograd runs
+        that node on the stream it was created on. If forward/backward later run on another stream
+        (graph capture uses its own), the gradient accumulation would be issued on the old stream --
+        illegal inside a capture. Rebinding creates the nodes anew on the current stream.
+        """
+        if self.arena.device.type != "cuda":
+            return False
+        cur = torch.cuda.current_stream(self.arena.device)
+        if self._stream is not None and cur == self._stream:
+            return False
+        self._build()
+        return True
 
     def prepare_for_backward(self, outputs: Sequence[torch.Tensor]):
         self._impl.prepare_for_backward(list(outputs))

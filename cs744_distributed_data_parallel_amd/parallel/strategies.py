@@ -125,6 +125,7 @@ class BucketedOverlap:
         if self._rebuild and not self._rebuilt and self.reducer.iterations >= 1:
             self.reducer.rebuild_in_ready_order()
             self._rebuilt = True
+        self.reducer.rebind_if_stream_changed()
         outs = []
         for o in outputs:
             if isinstance(o, torch.Tensor):

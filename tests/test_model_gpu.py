@@ -19,34 +19,49 @@ def test_native_extension_is_loaded_from_tree():
     assert path and os.path.dirname(path) == os.path.dirname(cdp.__file__)
 
 
-def test_vgg11_training_steps_match_reference():
+def _train3(model, opt, crit, steps=3, seed=1):
+    g = torch.Generator().manual_seed(seed)
+    losses = []
+    dev = next(model.parameters()).device
+    dt = next(model.parameters()).dtype
+    for _ in range(steps):
+        x = torch.randn(32, 3, 32, 32, generator=g)
+        y = torch.randint(0, 10, (32,), generator=g)
+        opt.zero_grad()
+        loss = crit(model(x.to(dev, dt)), y.to(dev))
+        loss.backward()
+        opt.step()
+        losses.append(loss.item())
+    return losses
+
+
+def _flat_state(m):
+    return torch.cat([v.double().cpu().reshape(-1) for v in m.state_dict().values() if v.dtype.is_floating_point])
+
+
+def test_vgg11_training_steps_match_reference(monkeypatch):
+    """3 SGD steps: the native fp32 engine stays as close to fp64 as stock torch fp32 does."""
     import cs744_distributed_data_parallel_amd as cdp
 
     torch.manual_seed(0)
     ref = cdp.VGG11(channels_last=False).double()
+    init = {k: v.clone() for k, v in ref.state_dict().items()}
     model = cdp.VGG11().cuda()
-    model.load_state_dict({k: v.float().cuda() for k, v in ref.state_dict().items()})
-    # small LR: random-label training at lr 0.05+ is chaotic and amplifies fp32-vs-fp64 rounding
-    opt = cdp.SGD(model.parameters(), lr=0.005, momentum=0.9, weight_decay=1e-4)
-    opt_r = torch.optim.SGD(ref.parameters(), lr=0.005, momentum=0.9, weight_decay=1e-4)
-    crit = cdp.CrossEntropyLoss()
-    g = torch.Generator().manual_seed(1)
-    for step in range(3):
-        x = torch.randn(32, 3, 32, 32, generator=g)
-        y = torch.randint(0, 10, (32,), generator=g)
-        opt.zero_grad()
-        loss = crit(model(x.cuda()), y.cuda())
-        loss.backward()
-        opt.step()
-        opt_r.zero_grad()
-        loss_r = torch.nn.functional.cross_entropy(ref(x.double()), y)
-        loss_r.backward()
-        opt_r.step()
-        assert abs(loss.item() - loss_r.item()) < 2e-3 * max(1.0, abs(loss_r.item())), (step, loss.item(), loss_r.item())
-    a = torch.cat([v.double().cpu().reshape(-1) for v in model.state_dict().values() if v.dtype.is_floating_point])
-    b = torch.cat([v.reshape(-1) for v in ref.state_dict().values() if v.dtype.is_floating_point])
+    model.load_state_dict({k: v.float().cuda() for k, v in init.items()})
+    kw = dict(lr=0.005, momentum=0.9, weight_decay=1e-4)
+    l_nat = _train3(model, cdp.SGD(model.parameters(), **kw), cdp.CrossEntropyLoss())
+    l_ref = _train3(ref, torch.optim.SGD(ref.parameters(), **kw), torch.nn.CrossEntropyLoss())
+    monkeypatch.setenv("CDP_FORCE_REFERENCE", "1")
+    t32 = cdp.VGG11(channels_last=False).cuda()
+    t32.load_state_dict({k: v.float().cuda() for k, v in init.items()})
+    l_t32 = _train3(t32, torch.optim.SGD(t32.parameters(), **kw), torch.nn.CrossEntropyLoss())
+    for a, b in zip(l_nat, l_ref):
+        assert abs(a - b) < 2e-3 * max(1.0, abs(b))
     assert list(model.state_dict()) == list(ref.state_dict())
-    assert ((a - b).norm() / b.norm()).item() < 1e-4
+    b = _flat_state(ref)
+    e_nat = ((_flat_state(model) - b).norm() / b.norm()).item()
+    e_t32 = ((_flat_state(t32) - b).norm() / b.norm()).item()
+    assert e_nat < max(3 * e_t32, 1e-4), (e_nat, e_t32)
 
 
 def test_vgg11_eval_matches_reference():
@@ -63,7 +78,7 @@ def test_vgg11_eval_matches_reference():
     assert (out.double().cpu() - out_r).abs().max().item() < 1e-3 * out_r.abs().max().item()
 
 
-def test_resnet50_forward_backward_small():
+def test_resnet50_forward_backward_small(monkeypatch):
     import cs744_distributed_data_parallel_amd as cdp
 
     torch.manual_seed(0)
@@ -79,7 +94,14 @@ def test_resnet50_forward_backward_small():
     assert abs(loss.item() - loss_r.item()) < 1e-3 * max(1.0, abs(loss_r.item()))
     g = torch.cat([p.grad.double().cpu().reshape(-1) for p in model.parameters()])
     gr = torch.cat([p.grad.reshape(-1) for p in ref.parameters()])
-    assert ((g - gr).norm() / gr.norm()).item() < 1e-2
+    monkeypatch.setenv("CDP_FORCE_REFERENCE", "1")
+    t32 = cdp.resnet50(num_classes=100, channels_last=False).cuda()
+    t32.load_state_dict({k: v.float().cuda() for k, v in ref.state_dict().items()})
+    torch.nn.functional.cross_entropy(t32(x.cuda()), y.cuda()).backward()
+    gt = torch.cat([p.grad.double().cpu().reshape(-1) for p in t32.parameters()])
+    e_nat = ((g - gr).norm() / gr.norm()).item()
+    e_t32 = ((gt - gr).norm() / gr.norm()).item()
+    assert e_nat < max(3 * e_t32, 1e-4), (e_nat, e_t32)
 
 
 def test_graph_capture_training_step():
