@@ -49,13 +49,13 @@ class _ConvBNAct(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, b, gamma, beta, rm, rv, nbt, momentum, eps, training, stride, pad, pool, relu, residual):
         C = _native.lib()
-        out, y, stats = C.conv_bn_act_fwd(
+        out, y, stats, xsave = C.conv_bn_act_fwd(
             x, w, b, gamma, beta, rm, rv, nbt, momentum, eps, training, stride, pad, pool, relu, residual
         )
         ctx.cfg = (stride, pad, pool, relu, training, b is not None, residual is not None)
         ctx.params = (w, b, gamma, beta)
         zout = out if residual is not None else None
-        ctx.save_for_backward(x, w, y, stats, zout)
+        ctx.save_for_backward(xsave, w, y, stats, zout)  # xsave: x, or x zero-padded to 4k channels
         return out
 
     @staticmethod

@@ -29,7 +29,10 @@ namespace {
 constexpr int BK = 32;
 constexpr int LDK = BK + 4;
 
-template <int BM, int BN, bool FAST, bool DGRAD>
+// MODE 0: C % 32 == 0 (a K-tile lies in one filter tap: one decode per tile)
+// MODE 1: C % 4 == 0  (float4 gathers, per-float4 tap decode; e.g. the channel-padded RGB stem)
+// MODE 2: anything   (scalar gathers)
+template <int BM, int BN, int MODE, bool DGRAD>
 __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvGemmParams p) {
   constexpr int TM = BM / 64;  // 32-row MFMA tiles per wave
   constexpr int TN = BN / 64;  // 32-col MFMA tiles per wave
@@ -57,10 +60,11 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvGemmParams p) {
   const int PQ = p.P * p.Q;
 
   // ---------------- per-thread gather setup ----------------
-  // FAST: each thread owns BM/32 A rows (row = tid/8 + 32*i) and one float4 column (tid%8).
-  // generic: each thread owns one A row and CPT consecutive scalar columns.
-  constexpr int A_LD = FAST ? BM / 32 : 1;
-  constexpr int B_LD = FAST ? BN / 32 : 1;
+  // vector modes: each thread owns BM/32 A rows (row = tid/8 + 32*i) and one float4 column (tid%8).
+  // scalar mode: each thread owns one A row and CPT consecutive scalar columns.
+  constexpr bool VEC = MODE != 2;
+  constexpr int A_LD = VEC ? BM / 32 : 1;
+  constexpr int B_LD = VEC ? BN / 32 : 1;
   constexpr int TPR_A = 256 / BM;            // generic: threads per A row
   constexpr int CPT_A = BK / TPR_A;          // generic: columns per thread (A)
   constexpr int TPR_B = 256 / BN;
@@ -71,13 +75,13 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvGemmParams p) {
   bool a_ok[A_LD];
 #pragma unroll
   for (int i = 0; i < A_LD; ++i) {
-    const int row = FAST ? ((tid >> 3) + 32 * i) : (tid / TPR_A);
+    const int row = VEC ? ((tid >> 3) + 32 * i) : (tid / TPR_A);
     const int m = m0 + row;
     a_ok[i] = m < p.M;
     const int mm = a_ok[i] ? m : 0;
-    const int n = mm / PQ;
+    const int n = fdiv(mm, p.fd_PQ);
     const int rem = mm - n * PQ;
-    const int pp = rem / p.Q;
+    const int pp = fdiv(rem, p.fd_Q);
     const int qq = rem - pp * p.Q;
     a_base[i] = p.x + (long long)n * p.H * p.W * p.C;
     if (DGRAD) {
@@ -89,10 +93,10 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvGemmParams p) {
     }
   }
 
-  float4 ra[FAST ? A_LD : 1];
-  float4 rb[FAST ? B_LD : 1];
-  float sa[FAST ? 1 : CPT_A];
-  float sb[FAST ? 1 : CPT_B];
+  float4 ra[VEC ? A_LD : 1];
+  float4 rb[VEC ? B_LD : 1];
+  float sa[VEC ? 1 : CPT_A];
+  float sb[VEC ? 1 : CPT_B];
 
   auto pix_ok = [&](int i, int kh, int kw, int& ih, int& iw) -> bool {
     if (DGRAD) {
@@ -115,10 +119,27 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvGemmParams p) {
 
   auto load_tile = [&](int kt) {
     const int r0 = kt * BK;
-    if (FAST) {
-      const int tap = r0 / p.C;
+    if (MODE == 1) {
+      const int r = r0 + (tid & 7) * 4;
+      const bool rok = r < p.Kdim;
+      const int tap = fdiv(r, p.fd_C);
+      const int c = r - tap * p.C;
+      const int kh = fdiv(tap, p.fd_KW), kw = tap - kh * p.KW;
+#pragma unroll
+      for (int i = 0; i < A_LD; ++i) {
+        int ih, iw;
+        const bool ok = rok && a_ok[i] && pix_ok(i, kh, kw, ih, iw);
+        ra[i] = ok ? ld4(a_base[i] + ((long long)ih * p.W + iw) * p.C + c) : f4zero();
+      }
+#pragma unroll
+      for (int i = 0; i < B_LD; ++i) {
+        const int n = n0 + (tid >> 3) + 32 * i;
+        rb[i] = (rok && n < p.Nout) ? ld4(p.w + (long long)n * p.Kdim + r) : f4zero();
+      }
+    } else if (MODE == 0) {
+      const int tap = fdiv(r0, p.fd_C);
       const int c0 = r0 - tap * p.C + (tid & 7) * 4;
-      const int kh = tap / p.KW, kw = tap - (tap / p.KW) * p.KW;
+      const int kh = fdiv(tap, p.fd_KW), kw = tap - kh * p.KW;
 #pragma unroll
       for (int i = 0; i < A_LD; ++i) {
         int ih, iw;
@@ -137,9 +158,9 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvGemmParams p) {
         const int r = r0 + cbase + j;
         float v = 0.f;
         if (a_ok[0] && r < p.Kdim) {
-          const int tap = r / p.C;
+          const int tap = fdiv(r, p.fd_C);
           const int c = r - tap * p.C;
-          const int kh = tap / p.KW, kw = tap - (tap / p.KW) * p.KW;
+          const int kh = fdiv(tap, p.fd_KW), kw = tap - kh * p.KW;
           int ih, iw;
           if (pix_ok(0, kh, kw, ih, iw)) v = a_base[0][((long long)ih * p.W + iw) * p.C + c];
         }
@@ -158,7 +179,7 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvGemmParams p) {
   auto store_tile = [&](float* st) {
     float* As = st;
     float* Bs = st + BM * LDK;
-    if (FAST) {
+    if (VEC) {
 #pragma unroll
       for (int i = 0; i < A_LD; ++i) st4(As + ((tid >> 3) + 32 * i) * LDK + (tid & 7) * 4, ra[i]);
 #pragma unroll
@@ -370,19 +391,19 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
   }
 }
 
-template <int BM, int BN, bool FAST, bool DGRAD>
+template <int BM, int BN, int MODE, bool DGRAD>
 void launch_igemm(const ConvGemmParams& p, int ntiles, hipStream_t st) {
-  hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, FAST, DGRAD>), dim3(ntiles * p.splits), dim3(256), 0, st, p);
+  hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, MODE, DGRAD>), dim3(ntiles * p.splits), dim3(256), 0, st, p);
 }
 
-template <bool FAST, bool DGRAD>
+template <int MODE, bool DGRAD>
 void dispatch_tile(const ConvGemmParams& p, int bm, int bn, hipStream_t st) {
   const int ntm = (p.M + bm - 1) / bm, ntn = (p.Nout + bn - 1) / bn;
   const int nt = ntm * ntn;
-  if (bm == 128 && bn == 128) launch_igemm<128, 128, FAST, DGRAD>(p, nt, st);
-  else if (bm == 128 && bn == 64) launch_igemm<128, 64, FAST, DGRAD>(p, nt, st);
-  else if (bm == 64 && bn == 128) launch_igemm<64, 128, FAST, DGRAD>(p, nt, st);
-  else launch_igemm<64, 64, FAST, DGRAD>(p, nt, st);
+  if (bm == 128 && bn == 128) launch_igemm<128, 128, MODE, DGRAD>(p, nt, st);
+  else if (bm == 128 && bn == 64) launch_igemm<128, 64, MODE, DGRAD>(p, nt, st);
+  else if (bm == 64 && bn == 128) launch_igemm<64, 128, MODE, DGRAD>(p, nt, st);
+  else launch_igemm<64, 64, MODE, DGRAD>(p, nt, st);
 }
 
 }  // namespace
@@ -391,13 +412,15 @@ int conv_igemm_rows_per_part(int bm) { return bm; }
 int splitk_rows_per_part() { return RB; }
 
 void conv_igemm_launch(const ConvGemmParams& p, int bm, int bn, bool dgrad, hipStream_t st) {
-  const bool fast = (p.C % BK) == 0 && (p.Kdim % BK) == 0;
-  if (fast) {
-    if (dgrad) dispatch_tile<true, true>(p, bm, bn, st);
-    else dispatch_tile<true, false>(p, bm, bn, st);
+  if ((p.C % BK) == 0 && (p.Kdim % BK) == 0) {
+    if (dgrad) dispatch_tile<0, true>(p, bm, bn, st);
+    else dispatch_tile<0, false>(p, bm, bn, st);
+  } else if ((p.C % 4) == 0 && (p.Kdim % 4) == 0) {
+    if (dgrad) dispatch_tile<1, true>(p, bm, bn, st);
+    else dispatch_tile<1, false>(p, bm, bn, st);
   } else {
-    if (dgrad) dispatch_tile<false, true>(p, bm, bn, st);
-    else dispatch_tile<false, false>(p, bm, bn, st);
+    if (dgrad) dispatch_tile<2, true>(p, bm, bn, st);
+    else dispatch_tile<2, false>(p, bm, bn, st);
   }
 }
 

@@ -6,6 +6,31 @@
 
 namespace cdp {
 
+// Exact division by a runtime-invariant divisor for dividends in [0, 2^31):
+// q = umulhi(n, mul) >> shift with mul = ceil(2^(31+l) / d), l = ceil(log2 d) (the CUTLASS
+// FastDivmod construction). Turns the ~30-instruction integer divide of the implicit-GEMM
+// gathers into two VALU ops.
+struct FastDiv {
+  unsigned d, mul, shift;
+};
+
+inline FastDiv make_fastdiv(int d) {
+  FastDiv f{(unsigned)d, 0u, 0u};
+  if (d <= 1) return f;
+  unsigned l = 0;
+  while ((1ull << l) < (unsigned long long)d) ++l;
+  const unsigned long long p = 31ull + l;
+  f.mul = (unsigned)(((1ull << p) + (unsigned long long)d - 1ull) / (unsigned long long)d);
+  f.shift = (unsigned)(p - 32ull);
+  return f;
+}
+
+#if defined(__HIPCC__)
+__device__ __forceinline__ int fdiv(int n, const FastDiv& f) {
+  return f.d == 1u ? n : (int)(__umulhi((unsigned)n, f.mul) >> f.shift);
+}
+#endif
+
 struct ConvGemmParams {
   const float* x;     // gather source, NHWC [N][H][W][C]
   const float* w;     // B^T rows [Nout][Kdim], Kdim ordered (kh, kw, c)
@@ -16,6 +41,7 @@ struct ConvGemmParams {
   int P, Q;           // GEMM-row spatial dims: rows m = (n, p, q)
   int KH, KW, stride, pad;
   int Nout, M, Kdim, ktiles, splits;
+  FastDiv fd_PQ, fd_Q, fd_C, fd_KW;
 };
 
 struct WgradParams {
@@ -24,6 +50,7 @@ struct WgradParams {
   float* out;       // slab base [splits][Cout][Kdim]
   int N, H, W, C, P, Q, KH, KW, stride, pad;
   int Cout, Kdim, M, splits;
+  FastDiv fd_PQ, fd_Q, fd_C, fd_KW;
 };
 
 // conv_igemm.hip

@@ -49,9 +49,9 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(WgradParams p) {
   int b_kh = 0, b_kw = 0, b_c = 0;
   bool b_kok = kcol < p.Kdim;
   if (FAST && b_kok) {
-    const int tap = kcol / p.C;
+    const int tap = fdiv(kcol, p.fd_C);
     b_c = kcol - tap * p.C;
-    b_kh = tap / p.KW;
+    b_kh = fdiv(tap, p.fd_KW);
     b_kw = tap - b_kh * p.KW;
   }
 
@@ -71,9 +71,9 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(WgradParams p) {
         ra[i] = make_float4(e[0], e[1], e[2], e[3]);
       }
       const int mm = mok ? m : 0;
-      const int n = mm / PQ;
+      const int n = fdiv(mm, p.fd_PQ);
       const int rem = mm - n * PQ;
-      const int pp = rem / p.Q, qq = rem - (rem / p.Q) * p.Q;
+      const int pp = fdiv(rem, p.fd_Q), qq = rem - pp * p.Q;
       const int ih0 = pp * p.stride - p.pad, iw0 = qq * p.stride - p.pad;
       const float* xb = p.x + (long long)n * p.H * p.W * p.C;
       if (FAST) {
@@ -87,9 +87,9 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(WgradParams p) {
           const int k = kcol + j;
           float v = 0.f;
           if (mok && k < p.Kdim) {
-            const int tap = k / p.C;
+            const int tap = fdiv(k, p.fd_C);
             const int c = k - tap * p.C;
-            const int kh = tap / p.KW, kw = tap - (tap / p.KW) * p.KW;
+            const int kh = fdiv(tap, p.fd_KW), kw = tap - kh * p.KW;
             const int ih = ih0 + kh, iw = iw0 + kw;
             if ((unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W)
               v = xb[((long long)ih * p.W + iw) * p.C + c];

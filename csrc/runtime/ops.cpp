@@ -85,6 +85,24 @@ int plan_wgrad_splits(int Cout, int Kdim, long long M) {
   return (int)std::max<long long>(1, s);
 }
 
+template <class P>
+void set_divs(P& p) {
+  p.fd_PQ = make_fastdiv(p.P * p.Q);
+  p.fd_Q = make_fastdiv(p.Q);
+  p.fd_C = make_fastdiv(p.C);
+  p.fd_KW = make_fastdiv(p.KW);
+}
+
+// Zero-pad the channel dim of a channels_last 4-D tensor up to a multiple of 4 (RGB stems:
+// 3 -> 4) so the float4 gather paths apply.
+at::Tensor pad_channels4(const at::Tensor& t) {
+  const int64_t C = t.size(1), C4 = (C + 3) / 4 * 4;
+  at::Tensor o = at::empty({t.size(0), C4, t.size(2), t.size(3)}, t.options().memory_format(at::MemoryFormat::ChannelsLast));
+  o.zero_();
+  o.narrow(1, 0, C).copy_(t);
+  return o;
+}
+
 }  // namespace
 
 // ---------------------------------------------------------------- conv forward
@@ -115,6 +133,7 @@ std::vector<at::Tensor> conv2d_fwd(const at::Tensor& x_, const at::Tensor& w_, c
   p.N = N; p.H = H; p.W = W; p.C = C; p.P = P; p.Q = Q;
   p.KH = KH; p.KW = KW; p.stride = (int)stride; p.pad = (int)pad;
   p.Nout = Co; p.M = (int)M; p.Kdim = Kdim; p.ktiles = g.ktiles; p.splits = g.splits;
+  set_divs(p);
   at::Tensor part, rpp;
   hipStream_t st = cur_stream();
   if (g.splits == 1) {
@@ -172,6 +191,7 @@ at::Tensor conv2d_dgrad(const at::Tensor& dy_, const at::Tensor& w_, std::vector
   p.N = N; p.H = P; p.W = Q; p.C = Co; p.P = H; p.Q = W;
   p.KH = KH; p.KW = KW; p.stride = (int)stride; p.pad = (int)pad;
   p.Nout = C; p.M = (int)M; p.Kdim = Kdim; p.ktiles = g.ktiles; p.splits = g.splits;
+  set_divs(p);
   if (g.splits == 1) {
     p.y = dx.data_ptr<float>();
     conv_igemm_launch(p, g.bm, g.bn, true, st);
@@ -188,6 +208,14 @@ at::Tensor conv2d_dgrad(const at::Tensor& dy_, const at::Tensor& w_, std::vector
 // dW (channels_last [Co, C, KH, KW]); written into `out` when given (accumulating if asked).
 at::Tensor conv2d_wgrad(const at::Tensor& dy_, const at::Tensor& x_, std::vector<int64_t> w_shape, int64_t stride,
                         int64_t pad, const c10::optional<at::Tensor>& out, bool accumulate) {
+  return conv2d_wgrad_keep(dy_, x_, w_shape, stride, pad, out, accumulate, -1);
+}
+
+// keep_c >= 0: x carries zero-padded channels; only the first keep_c input channels of dW are
+// written (the strip is fused into the split-K slab reduction).
+at::Tensor conv2d_wgrad_keep(const at::Tensor& dy_, const at::Tensor& x_, std::vector<int64_t> w_shape,
+                             int64_t stride, int64_t pad, const c10::optional<at::Tensor>& out, bool accumulate,
+                             int64_t keep_c) {
   check_f32_cuda(dy_, "grad_output");
   check_f32_cuda(x_, "input");
   const at::Tensor dy = nhwc(dy_);
@@ -197,14 +225,15 @@ at::Tensor conv2d_wgrad(const at::Tensor& dy_, const at::Tensor& x_, std::vector
   const int P = dy.size(2), Q = dy.size(3);
   const long long M = (long long)N * P * Q;
   const int Kdim = KH * KW * C;
+  const int Ckeep = keep_c >= 0 ? (int)keep_c : C;
   auto opts = x.options();
   at::Tensor dw;
   if (out.has_value() && out->defined()) {
     dw = *out;
-    TORCH_CHECK(dw.is_contiguous(at::MemoryFormat::ChannelsLast) && dw.numel() == (long long)Co * Kdim,
+    TORCH_CHECK(dw.is_contiguous(at::MemoryFormat::ChannelsLast) && dw.numel() == (long long)Co * KH * KW * Ckeep,
                 "wgrad out must be channels_last contiguous");
   } else {
-    dw = at::empty({Co, C, KH, KW}, opts.memory_format(at::MemoryFormat::ChannelsLast));
+    dw = at::empty({Co, Ckeep, KH, KW}, opts.memory_format(at::MemoryFormat::ChannelsLast));
     accumulate = false;
   }
   hipStream_t st = cur_stream();
@@ -215,14 +244,16 @@ at::Tensor conv2d_wgrad(const at::Tensor& dy_, const at::Tensor& x_, std::vector
   p.KH = KH; p.KW = KW; p.stride = (int)stride; p.pad = (int)pad;
   p.Cout = Co; p.Kdim = Kdim; p.M = (int)M;
   p.splits = plan_wgrad_splits(Co, Kdim, M);
-  if (p.splits == 1 && !accumulate) {
+  set_divs(p);
+  if (p.splits == 1 && !accumulate && Ckeep == C) {
     p.out = dw.data_ptr<float>();
     wgrad_launch(p, st);
   } else {
     at::Tensor slab = at::empty({p.splits, Co, Kdim}, opts);
     p.out = slab.data_ptr<float>();
     wgrad_launch(p, st);
-    slab_sum_launch(slab.data_ptr<float>(), p.splits, (long long)Co * Kdim, dw.data_ptr<float>(), accumulate, st);
+    slab_sum_strided_launch(slab.data_ptr<float>(), p.splits, (long long)Co * Kdim, C, Ckeep, dw.data_ptr<float>(),
+                            accumulate, st);
   }
   return dw;
 }
@@ -238,7 +269,12 @@ std::vector<at::Tensor> conv_bn_act_fwd(const at::Tensor& x, const at::Tensor& w
                                         const c10::optional<at::Tensor>& num_batches_tracked, double momentum,
                                         double eps, bool training, int64_t stride, int64_t pad, bool pool, bool relu,
                                         const c10::optional<at::Tensor>& residual) {
-  std::vector<at::Tensor> r = conv2d_fwd(x, w, b, stride, pad, training);
+  // RGB stem: zero-pad 3 -> 4 channels so the float4 gather path runs (the padded input is what
+  // backward needs, so it is returned for saving)
+  const bool padc = (x.size(1) % 4) != 0;
+  const at::Tensor xin = padc ? pad_channels4(nhwc(x)) : x;
+  const at::Tensor win = padc ? pad_channels4(nhwc(w)) : w;
+  std::vector<at::Tensor> r = conv2d_fwd(xin, win, b, stride, pad, training);
   at::Tensor y = r[0];
   const int N = y.size(0), C = y.size(1), H = y.size(2), W = y.size(3);
   TORCH_CHECK(C % 4 == 0, "BatchNorm channel count must be a multiple of 4");
@@ -270,7 +306,7 @@ std::vector<at::Tensor> conv_bn_act_fwd(const at::Tensor& x, const at::Tensor& w
                              opts.memory_format(at::MemoryFormat::ChannelsLast));
   bn_act_fwd_launch(y.data_ptr<float>(), stats.data_ptr<float>(), res.defined() ? res.data_ptr<float>() : nullptr,
                     out.data_ptr<float>(), N, H, W, C, pool, relu, st);
-  return {out, y, stats};
+  return {out, y, stats, xin};
 }
 
 // ---------------------------------------------------------------- fused block backward
@@ -319,9 +355,19 @@ std::vector<at::Tensor> conv_bn_act_bwd(const at::Tensor& gout_, const at::Tenso
     db = slot(db_out, {C}, false);
     chan_finalize_launch(dbpart.data_ptr<float>(), nblk, C, nullptr, db.data_ptr<float>(), nullptr, false, st);
   }
+  // x may carry zero-padded channels (RGB stem, see conv_bn_act_fwd)
+  const bool padc = x.size(1) != w.size(1);
   at::Tensor dx;
-  if (need_dx) dx = conv2d_dgrad(dy, w, {x.size(0), x.size(1), x.size(2), x.size(3)}, stride, pad);
-  at::Tensor dw = conv2d_wgrad(dy, x, {w.size(0), w.size(1), w.size(2), w.size(3)}, stride, pad, dw_out, false);
+  if (need_dx) {
+    if (padc) {
+      at::Tensor dx4 = conv2d_dgrad(dy, pad_channels4(nhwc(w)), {x.size(0), x.size(1), x.size(2), x.size(3)}, stride, pad);
+      dx = dx4.narrow(1, 0, w.size(1)).contiguous(at::MemoryFormat::ChannelsLast);
+    } else {
+      dx = conv2d_dgrad(dy, w, {x.size(0), x.size(1), x.size(2), x.size(3)}, stride, pad);
+    }
+  }
+  at::Tensor dw = conv2d_wgrad_keep(dy, x, {w.size(0), x.size(1), w.size(2), w.size(3)}, stride, pad, dw_out, false,
+                                    padc ? w.size(1) : -1);
   return {dx, dw, db, dgamma, dbeta, dres};
 }
 
@@ -340,6 +386,7 @@ at::Tensor linear_fwd(const at::Tensor& x_, const at::Tensor& w_, const c10::opt
   p.w = w.data_ptr<float>();
   p.N = B; p.H = 1; p.W = 1; p.C = I; p.P = 1; p.Q = 1; p.KH = 1; p.KW = 1; p.stride = 1; p.pad = 0;
   p.Nout = O; p.M = B; p.Kdim = I; p.ktiles = g.ktiles; p.splits = g.splits;
+  set_divs(p);
   hipStream_t st = cur_stream();
   if (g.splits == 1) {
     p.y = y.data_ptr<float>();
@@ -377,6 +424,7 @@ std::vector<at::Tensor> linear_bwd(const at::Tensor& gy_, const at::Tensor& x_, 
   p.N = B; p.H = 1; p.W = 1; p.C = I; p.P = 1; p.Q = 1; p.KH = 1; p.KW = 1; p.stride = 1; p.pad = 0;
   p.Cout = O; p.Kdim = I; p.M = B;
   p.splits = plan_wgrad_splits(O, I, B);
+  set_divs(p);
   if (p.splits == 1) {
     p.out = dw.data_ptr<float>();
     wgrad_launch(p, st);

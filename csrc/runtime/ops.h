@@ -12,6 +12,8 @@ at::Tensor conv2d_dgrad(const at::Tensor& dy, const at::Tensor& w, std::vector<i
                         int64_t pad);
 at::Tensor conv2d_wgrad(const at::Tensor& dy, const at::Tensor& x, std::vector<int64_t> w_shape, int64_t stride,
                         int64_t pad, const c10::optional<at::Tensor>& out, bool accumulate);
+at::Tensor conv2d_wgrad_keep(const at::Tensor& dy, const at::Tensor& x, std::vector<int64_t> w_shape, int64_t stride,
+                             int64_t pad, const c10::optional<at::Tensor>& out, bool accumulate, int64_t keep_c);
 std::vector<at::Tensor> conv_bn_act_fwd(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tensor>& b,
                                         const c10::optional<at::Tensor>& gamma, const c10::optional<at::Tensor>& beta,
                                         const c10::optional<at::Tensor>& running_mean,

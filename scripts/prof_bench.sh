@@ -1,10 +1,13 @@
+#!/bin/bash
+# rocprofv3 kernel-trace + stats of a short eager bench run; summary -> gpurun_out/<tag>/summary.md
 set -o pipefail
-mkdir -p gpurun_out/prof1
+TAG=${1:-prof}
+STEPS=${2:-10}
+shift 2
+mkdir -p gpurun_out/$TAG
 cd /tmp && export TMPDIR=/tmp
 cd $GRAFT_REPO_ROOT
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof1 -o run -- python bench.py --steps 10 --warmup 3 --no-graph > gpurun_out/prof1/bench.log 2>&1
-echo "prof rc=$?"
-timeout -k 10 200 python bench.py --steps 20 --warmup 5 --backend torch > gpurun_out/bench_torch.log 2>&1
-echo "torch rc=$?"
-tail -2 gpurun_out/bench_torch.log
-find gpurun_out/prof1 -name "*stats*"
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/$TAG -o run -- \
+  python bench.py --steps $STEPS --warmup 3 --no-graph "$@" > gpurun_out/$TAG/bench.log 2>&1 || exit $?
+python scripts/prof_summary.py gpurun_out/$TAG/run_kernel_stats.csv $((STEPS + 3 + 3)) gpurun_out/$TAG/summary.md > /dev/null
+tail -1 gpurun_out/$TAG/bench.log
