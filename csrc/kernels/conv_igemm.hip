@@ -391,6 +391,75 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
   }
 }
 
+// float4 variant (Nout % 4 == 0): block = 16 column quads (64 columns) x 16 row lanes, RB rows;
+// every thread keeps 2 rows x 4 columns in registers and issues its S slab loads back to back.
+__global__ __launch_bounds__(256) void splitk_reduce4_kernel(const float* __restrict__ slab, int S, int M, int Nout,
+                                                             const float* __restrict__ bias, float* __restrict__ y,
+                                                             float* __restrict__ part) {
+  __shared__ float4 red[16][16];
+  const int cq = threadIdx.x & 15;
+  const int rl = threadIdx.x >> 4;
+  const int n = blockIdx.x * 64 + cq * 4;
+  const int y0 = blockIdx.y * RB;
+  const bool nok = n < Nout;
+  const float4 bv = (bias && nok) ? ld4(bias + n) : f4zero();
+  const long long plane = (long long)M * Nout;
+  float4 v[RB / 16];
+#pragma unroll
+  for (int i = 0; i < RB / 16; ++i) {
+    const int m = y0 + rl + 16 * i;
+    float4 s = f4zero();
+    if (m < M && nok) {
+      const float* src = slab + (long long)m * Nout + n;
+      int z = 0;
+      for (; z + 3 < S; z += 4) {
+        const float4 a = ld4(src + z * plane), b = ld4(src + (z + 1) * plane);
+        const float4 c = ld4(src + (z + 2) * plane), d = ld4(src + (z + 3) * plane);
+        s.x += (a.x + b.x) + (c.x + d.x); s.y += (a.y + b.y) + (c.y + d.y);
+        s.z += (a.z + b.z) + (c.z + d.z); s.w += (a.w + b.w) + (c.w + d.w);
+      }
+      for (; z < S; ++z) {
+        const float4 a = ld4(src + z * plane);
+        s.x += a.x; s.y += a.y; s.z += a.z; s.w += a.w;
+      }
+      s.x += bv.x; s.y += bv.y; s.z += bv.z; s.w += bv.w;
+      st4(y + (long long)m * Nout + n, s);
+    }
+    v[i] = s;
+  }
+  if (!part) return;
+  const int cnt = min(RB, M - y0);
+  float4 t = f4zero();
+#pragma unroll
+  for (int i = 0; i < RB / 16; ++i)
+    if (y0 + rl + 16 * i < M) { t.x += v[i].x; t.y += v[i].y; t.z += v[i].z; t.w += v[i].w; }
+  red[rl][cq] = t;
+  __syncthreads();
+  float4 mean = f4zero();
+#pragma unroll
+  for (int k = 0; k < 16; ++k) { mean.x += red[k][cq].x; mean.y += red[k][cq].y; mean.z += red[k][cq].z; mean.w += red[k][cq].w; }
+  const float ic = 1.f / (float)cnt;
+  mean.x *= ic; mean.y *= ic; mean.z *= ic; mean.w *= ic;
+  __syncthreads();
+  t = f4zero();
+#pragma unroll
+  for (int i = 0; i < RB / 16; ++i)
+    if (y0 + rl + 16 * i < M) {
+      const float a = v[i].x - mean.x, b = v[i].y - mean.y, c = v[i].z - mean.z, d = v[i].w - mean.w;
+      t.x += a * a; t.y += b * b; t.z += c * c; t.w += d * d;
+    }
+  red[rl][cq] = t;
+  __syncthreads();
+  if (rl == 0 && nok) {
+    float4 q = f4zero();
+#pragma unroll
+    for (int k = 0; k < 16; ++k) { q.x += red[k][cq].x; q.y += red[k][cq].y; q.z += red[k][cq].z; q.w += red[k][cq].w; }
+    float* dst = part + ((long long)blockIdx.y * Nout + n) * 2;
+    dst[0] = mean.x; dst[1] = q.x; dst[2] = mean.y; dst[3] = q.y;
+    dst[4] = mean.z; dst[5] = q.z; dst[6] = mean.w; dst[7] = q.w;
+  }
+}
+
 template <int BM, int BN, int MODE, bool DGRAD>
 void launch_igemm(const ConvGemmParams& p, int ntiles, hipStream_t st) {
   hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, MODE, DGRAD>), dim3(ntiles * p.splits), dim3(256), 0, st, p);
@@ -427,7 +496,8 @@ void conv_igemm_launch(const ConvGemmParams& p, int bm, int bn, bool dgrad, hipS
 void splitk_reduce_launch(const float* slab, int S, int M, int Nout, const float* bias, float* y, float* part,
                           hipStream_t st) {
   dim3 grid((Nout + 63) / 64, (M + RB - 1) / RB);
-  hipLaunchKernelGGL(splitk_reduce_kernel, grid, dim3(256), 0, st, slab, S, M, Nout, bias, y, part);
+  if ((Nout & 3) == 0) hipLaunchKernelGGL(splitk_reduce4_kernel, grid, dim3(256), 0, st, slab, S, M, Nout, bias, y, part);
+  else hipLaunchKernelGGL(splitk_reduce_kernel, grid, dim3(256), 0, st, slab, S, M, Nout, bias, y, part);
 }
 
 }  // namespace cdp

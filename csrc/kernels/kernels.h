@@ -60,7 +60,7 @@ void splitk_reduce_launch(const float* slab, int S, int M, int Nout, const float
 int splitk_rows_per_part();
 
 // wgrad.hip
-void wgrad_launch(const WgradParams& p, hipStream_t st);
+void wgrad_launch(const WgradParams& p, int bm, int bn, hipStream_t st);
 void slab_sum_launch(const float* slab, int S, long long n, float* dst, bool accumulate, hipStream_t st);
 void slab_sum_strided_launch(const float* slab, int S, long long n_src, int src_cols, int dst_cols, float* dst,
                              bool accumulate, hipStream_t st);

@@ -17,37 +17,40 @@
 namespace cdp {
 namespace {
 
-constexpr int WBM = 128, WBN = 128, WBK = 32;
-constexpr int WLD = WBM + 4;
+constexpr int WBK = 32;
 
-template <bool FAST>
+// BM (co) x BN (k) x 32 (m) tile, 256 threads = 2x2 waves of (BM/2)x(BN/2).
+template <int BM, int BN, bool FAST>
 __global__ __launch_bounds__(256, 2) void wgrad_kernel(WgradParams p) {
-  constexpr int STAGE = WBK * WLD * 2;  // A tile + B tile
+  constexpr int LDA = BM + 4, LDB = BN + 4;
+  constexpr int STAGE = WBK * (LDA + LDB);
+  constexpr int TM = BM / 64, TN = BN / 64;
+  constexpr int CPR_A = BM / 4, RPP_A = 256 / CPR_A, NP_A = WBK / RPP_A;  // float4 per row, rows/pass, passes
+  constexpr int CPR_B = BN / 4, RPP_B = 256 / CPR_B, NP_B = WBK / RPP_B;
   __shared__ __attribute__((aligned(16))) float smem[2 * STAGE];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid >> 1, wn = wid & 1;
 
-  const int ntn = (p.Kdim + WBN - 1) / WBN;
-  const int ntm = (p.Cout + WBM - 1) / WBM;
+  const int ntn = (p.Kdim + BN - 1) / BN;
+  const int ntm = (p.Cout + BM - 1) / BM;
   const int bid = xcd_remap(blockIdx.x, gridDim.x);
   // tile (tm, tn) fastest, split slowest: blocks of one split share the dY/X row window in L2
   const int tile = bid % (ntm * ntn);
   const int split = bid / (ntm * ntn);
   const int tm_idx = tile / ntn, tn_idx = tile % ntn;
-  const int co0 = tm_idx * WBM, r0 = tn_idx * WBN;
+  const int co0 = tm_idx * BM, r0 = tn_idx * BN;
   const int mt_total = (p.M + WBK - 1) / WBK;
   const int kt_begin = (int)(((long long)split * mt_total) / p.splits);
   const int kt_end = (int)(((long long)(split + 1) * mt_total) / p.splits);
   const int PQ = p.P * p.Q;
 
-  // A (dY) tile: 32 rows x 128 cols = 1024 float4; thread -> rows tid/32 + 8i, col4 tid%32
-  // B (Xcol) tile: same geometry over k.
-  float4 ra[4], rb[4];
-  const int c4 = tid & 31;
-  // per-thread B column decode (fixed for the whole kernel): k = r0 + 4*c4 .. +3
-  const int kcol = r0 + c4 * 4;
+  float4 ra[NP_A], rb[NP_B];
+  const int ca = tid % CPR_A, cb = tid % CPR_B;
+  const int co = co0 + ca * 4;
+  // per-thread B column decode (fixed for the whole kernel): k = r0 + 4*cb .. +3
+  const int kcol = r0 + cb * 4;
   int b_kh = 0, b_kw = 0, b_c = 0;
-  bool b_kok = kcol < p.Kdim;
+  const bool b_kok = kcol < p.Kdim;
   if (FAST && b_kok) {
     const int tap = fdiv(kcol, p.fd_C);
     b_c = kcol - tap * p.C;
@@ -58,10 +61,9 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(WgradParams p) {
   auto load_tile = [&](int kt) {
     const int mb = kt * WBK;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int m = mb + (tid >> 5) + 8 * i;
+    for (int i = 0; i < NP_A; ++i) {
+      const int m = mb + tid / CPR_A + RPP_A * i;
       const bool mok = m < p.M;
-      const int co = co0 + c4 * 4;
       if (FAST) {
         ra[i] = (mok && co < p.Cout) ? ld4(p.dy + (long long)m * p.Cout + co) : f4zero();
       } else {
@@ -70,6 +72,11 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(WgradParams p) {
         for (int j = 0; j < 4; ++j) e[j] = (mok && co + j < p.Cout) ? p.dy[(long long)m * p.Cout + co + j] : 0.f;
         ra[i] = make_float4(e[0], e[1], e[2], e[3]);
       }
+    }
+#pragma unroll
+    for (int i = 0; i < NP_B; ++i) {
+      const int m = mb + tid / CPR_B + RPP_B * i;
+      const bool mok = m < p.M;
       const int mm = mok ? m : 0;
       const int n = fdiv(mm, p.fd_PQ);
       const int rem = mm - n * PQ;
@@ -102,18 +109,16 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(WgradParams p) {
   };
   auto store_tile = [&](float* st) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int row = (tid >> 5) + 8 * i;
-      st4(st + row * WLD + c4 * 4, ra[i]);
-      st4(st + WBK * WLD + row * WLD + c4 * 4, rb[i]);
-    }
+    for (int i = 0; i < NP_A; ++i) st4(st + (tid / CPR_A + RPP_A * i) * LDA + ca * 4, ra[i]);
+#pragma unroll
+    for (int i = 0; i < NP_B; ++i) st4(st + WBK * LDA + (tid / CPR_B + RPP_B * i) * LDB + cb * 4, rb[i]);
   };
 
-  f32x16 acc[2][2];
+  f32x16 acc[TM][TN];
 #pragma unroll
-  for (int a = 0; a < 2; ++a)
+  for (int a = 0; a < TM; ++a)
 #pragma unroll
-    for (int b = 0; b < 2; ++b)
+    for (int b = 0; b < TN; ++b)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
 
@@ -127,19 +132,19 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(WgradParams p) {
       const bool more = kt + 1 < kt_end;
       if (more) load_tile(kt + 1);
       const float* As = smem + cur * STAGE;
-      const float* Bs = As + WBK * WLD;
+      const float* Bs = As + WBK * LDA;
 #pragma unroll
       for (int s = 0; s < WBK / 2; ++s) {
         const int row = 2 * s + hh;
-        float af[2], bf[2];
+        float af[TM], bf[TN];
 #pragma unroll
-        for (int a = 0; a < 2; ++a) af[a] = As[row * WLD + wm * 64 + a * 32 + l32];
+        for (int a = 0; a < TM; ++a) af[a] = As[row * LDA + wm * (BM / 2) + a * 32 + l32];
 #pragma unroll
-        for (int b = 0; b < 2; ++b) bf[b] = Bs[row * WLD + wn * 64 + b * 32 + l32];
+        for (int b = 0; b < TN; ++b) bf[b] = Bs[row * LDB + wn * (BN / 2) + b * 32 + l32];
 #pragma unroll
-        for (int a = 0; a < 2; ++a)
+        for (int a = 0; a < TM; ++a)
 #pragma unroll
-          for (int b = 0; b < 2; ++b)
+          for (int b = 0; b < TN; ++b)
             acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[a], bf[b], acc[a][b], 0, 0, 0);
       }
       if (more) store_tile(smem + (cur ^ 1) * STAGE);
@@ -149,14 +154,14 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(WgradParams p) {
 
   float* out = p.out + (long long)split * p.Cout * p.Kdim;
 #pragma unroll
-  for (int a = 0; a < 2; ++a)
+  for (int a = 0; a < TM; ++a)
 #pragma unroll
-    for (int b = 0; b < 2; ++b) {
-      const int k = r0 + wn * 64 + b * 32 + l32;
+    for (int b = 0; b < TN; ++b) {
+      const int k = r0 + wn * (BN / 2) + b * 32 + l32;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const int co = co0 + wm * 64 + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
-        if (co < p.Cout && k < p.Kdim) out[(long long)co * p.Kdim + k] = acc[a][b][r];
+        const int c = co0 + wm * (BM / 2) + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
+        if (c < p.Cout && k < p.Kdim) out[(long long)c * p.Kdim + k] = acc[a][b][r];
       }
     }
 }
@@ -200,13 +205,21 @@ __global__ __launch_bounds__(256) void slab_sum_kernel(const float* __restrict__
 
 }  // namespace
 
-void wgrad_launch(const WgradParams& p, hipStream_t st) {
-  const int ntn = (p.Kdim + WBN - 1) / WBN;
-  const int ntm = (p.Cout + WBM - 1) / WBM;
+template <int BM, int BN>
+void wgrad_launch_t(const WgradParams& p, hipStream_t st) {
+  const int ntn = (p.Kdim + BN - 1) / BN;
+  const int ntm = (p.Cout + BM - 1) / BM;
   const bool fast = (p.C % 4) == 0 && (p.Cout % 4) == 0;
   dim3 grid(ntm * ntn * p.splits);
-  if (fast) hipLaunchKernelGGL(wgrad_kernel<true>, grid, dim3(256), 0, st, p);
-  else hipLaunchKernelGGL(wgrad_kernel<false>, grid, dim3(256), 0, st, p);
+  if (fast) hipLaunchKernelGGL((wgrad_kernel<BM, BN, true>), grid, dim3(256), 0, st, p);
+  else hipLaunchKernelGGL((wgrad_kernel<BM, BN, false>), grid, dim3(256), 0, st, p);
+}
+
+void wgrad_launch(const WgradParams& p, int bm, int bn, hipStream_t st) {
+  if (bm == 128 && bn == 128) wgrad_launch_t<128, 128>(p, st);
+  else if (bm == 128) wgrad_launch_t<128, 64>(p, st);
+  else if (bn == 128) wgrad_launch_t<64, 128>(p, st);
+  else wgrad_launch_t<64, 64>(p, st);
 }
 
 void slab_sum_launch(const float* slab, int S, long long n, float* dst, bool accumulate, hipStream_t st) {

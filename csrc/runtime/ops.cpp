@@ -54,8 +54,31 @@ int num_cus() {
   return cus;
 }
 
-// Tile + split-K choice for the implicit GEMM: fill >= 2 workgroups per CU (the 128x128 tile
-// runs 2 per CU: 72 KiB LDS, 160 VGPRs), keeping >= 4 K-tiles per split.
+// Workgroups each kernel keeps resident per CU (LDS-bound; VGPRs allow at least 2 waves/SIMD).
+int conv_blocks_per_cu(int bm, int bn) { return std::max(1, std::min(4, (160 * 1024) / (2 * (bm + bn) * 36 * 4))); }
+int wgrad_blocks_per_cu(int bm, int bn) { return std::max(1, std::min(4, (160 * 1024) / (2 * 32 * (bm + bn + 8) * 4))); }
+
+// Split-K factor that best fills whole waves of resident workgroups: a grid just over one wave
+// (e.g. 540 blocks on 512 slots) costs almost two waves of time, so quantisation dominates.
+int choose_splits(long long tiles, int ktiles, int slots, int min_kt) {
+  if (tiles >= slots) return 1;
+  const int smax = std::max(1, ktiles / std::max(1, min_kt));
+  int best = 1;
+  double best_eff = (double)tiles / (double)slots;
+  for (int w = 1; w <= 2; ++w) {
+    int s = (int)std::min<long long>(smax, (long long)w * slots / tiles);
+    if (s < 1) continue;
+    const long long blocks = tiles * s;
+    const long long waves = (blocks + slots - 1) / slots;
+    const double eff = (double)blocks / (double)(waves * slots);
+    if (eff > best_eff + 0.02) {
+      best = s;
+      best_eff = eff;
+    }
+  }
+  return best;
+}
+
 GemmPlan plan_gemm(long long M, int Nout, int Kdim) {
   GemmPlan g;
   g.ktiles = (Kdim + 31) / 32;
@@ -64,25 +87,24 @@ GemmPlan plan_gemm(long long M, int Nout, int Kdim) {
   long long tiles128 = ((M + 127) / 128) * ((Nout + g.bn - 1) / g.bn);
   g.bm = (tiles128 >= target || M > 4096) ? 128 : 64;
   const long long tiles = ((M + g.bm - 1) / g.bm) * ((Nout + g.bn - 1) / g.bn);
-  int s = 1;
-  if (tiles < target) {
-    s = (int)((target + tiles - 1) / tiles);
-    s = std::min(s, std::max(1, g.ktiles / 4));
-    s = std::min(s, 16);
-  }
-  g.splits = std::max(1, s);
+  const int slots = conv_blocks_per_cu(g.bm, g.bn) * num_cus();
+  g.splits = std::min(16, choose_splits(tiles, g.ktiles, slots, 4));
   return g;
 }
 
-int plan_wgrad_splits(int Cout, int Kdim, long long M) {
-  // ~2 workgroups per CU, >= 16 K-tiles (512 rows) per split: the fp32 slab traffic
-  // (splits x Cout x Kdim x 8 B) stays well under the GEMM time.
-  const long long tiles = ((Cout + 127) / 128) * (long long)((Kdim + 127) / 128);
-  const long long mt = (M + 31) / 32;
-  long long s = (2LL * num_cus() + tiles - 1) / tiles;
-  s = std::min<long long>(s, std::max<long long>(1, mt / 16));
-  s = std::min<long long>(s, 128);
-  return (int)std::max<long long>(1, s);
+struct WgradPlan {
+  int bm, bn, splits;
+};
+
+WgradPlan plan_wgrad(int Cout, int Kdim, long long M) {
+  WgradPlan w;
+  w.bm = Cout >= 128 ? 128 : 64;
+  w.bn = (Kdim % 128 == 0) ? 128 : 64;
+  const long long tiles = (long long)((Cout + w.bm - 1) / w.bm) * ((Kdim + w.bn - 1) / w.bn);
+  const int mt = (int)std::min<long long>((M + 31) / 32, 1 << 30);
+  const int slots = wgrad_blocks_per_cu(w.bm, w.bn) * num_cus();
+  w.splits = std::min(1024, choose_splits(tiles, mt, slots, 4));
+  return w;
 }
 
 template <class P>
@@ -243,15 +265,16 @@ at::Tensor conv2d_wgrad_keep(const at::Tensor& dy_, const at::Tensor& x_, std::v
   p.N = N; p.H = H; p.W = W; p.C = C; p.P = P; p.Q = Q;
   p.KH = KH; p.KW = KW; p.stride = (int)stride; p.pad = (int)pad;
   p.Cout = Co; p.Kdim = Kdim; p.M = (int)M;
-  p.splits = plan_wgrad_splits(Co, Kdim, M);
+  const WgradPlan wp = plan_wgrad(Co, Kdim, M);
+  p.splits = wp.splits;
   set_divs(p);
   if (p.splits == 1 && !accumulate && Ckeep == C) {
     p.out = dw.data_ptr<float>();
-    wgrad_launch(p, st);
+    wgrad_launch(p, wp.bm, wp.bn, st);
   } else {
     at::Tensor slab = at::empty({p.splits, Co, Kdim}, opts);
     p.out = slab.data_ptr<float>();
-    wgrad_launch(p, st);
+    wgrad_launch(p, wp.bm, wp.bn, st);
     slab_sum_strided_launch(slab.data_ptr<float>(), p.splits, (long long)Co * Kdim, C, Ckeep, dw.data_ptr<float>(),
                             accumulate, st);
   }
@@ -423,15 +446,16 @@ std::vector<at::Tensor> linear_bwd(const at::Tensor& gy_, const at::Tensor& x_, 
   p.x = x.data_ptr<float>();
   p.N = B; p.H = 1; p.W = 1; p.C = I; p.P = 1; p.Q = 1; p.KH = 1; p.KW = 1; p.stride = 1; p.pad = 0;
   p.Cout = O; p.Kdim = I; p.M = B;
-  p.splits = plan_wgrad_splits(O, I, B);
+  const WgradPlan wp = plan_wgrad(O, I, B);
+  p.splits = wp.splits;
   set_divs(p);
   if (p.splits == 1) {
     p.out = dw.data_ptr<float>();
-    wgrad_launch(p, st);
+    wgrad_launch(p, wp.bm, wp.bn, st);
   } else {
     at::Tensor slab = at::empty({p.splits, O, I}, x.options());
     p.out = slab.data_ptr<float>();
-    wgrad_launch(p, st);
+    wgrad_launch(p, wp.bm, wp.bn, st);
     slab_sum_launch(slab.data_ptr<float>(), p.splits, (long long)O * I, dw.data_ptr<float>(), false, st);
   }
   at::Tensor db;

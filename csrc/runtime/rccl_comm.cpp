@@ -199,6 +199,11 @@ std::shared_ptr<RcclWork> RcclComm::end(hipStream_t cur, bool async, std::vector
 
 void RcclComm::watchdog_loop() {
   hipSetDevice(device_);
+  // This thread only polls events. Opt it out of global-mode capture checks: otherwise a
+  // hipEventQuery here while the main thread captures a hipGraph (torch.cuda.graph uses the
+  // global mode) would invalidate that capture.
+  hipStreamCaptureMode mode = hipStreamCaptureModeRelaxed;
+  hipThreadExchangeStreamCaptureMode(&mode);
   while (!stop_.load()) {
     std::this_thread::sleep_for(std::chrono::milliseconds(20));
     std::string timed_out;

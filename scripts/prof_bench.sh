@@ -9,5 +9,5 @@ cd /tmp && export TMPDIR=/tmp
 cd $GRAFT_REPO_ROOT
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/$TAG -o run -- \
   python bench.py --steps $STEPS --warmup 3 --no-graph "$@" > gpurun_out/$TAG/bench.log 2>&1 || exit $?
-python scripts/prof_summary.py gpurun_out/$TAG/run_kernel_stats.csv $((STEPS + 3 + 3)) gpurun_out/$TAG/summary.md > /dev/null
+python scripts/prof_summary.py gpurun_out/$TAG/run_kernel_stats.csv $((STEPS + 3)) gpurun_out/$TAG/summary.md > /dev/null
 tail -1 gpurun_out/$TAG/bench.log
