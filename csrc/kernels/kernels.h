@@ -98,6 +98,10 @@ void wtrans_launch(const float* w, float* wt, int Co, int T, int Ci, hipStream_t
 void stack_mean_launch(const float* const* srcs, int k, long long n, float* dst, hipStream_t st);
 void scale_launch(float* x, long long n, float a, hipStream_t st);
 void colsum_launch(const float* x, int R, int C, float* out, bool accumulate, hipStream_t st);
+void small_linear_fwd_launch(const float* x, const float* w, const float* b, int B, int I, int O, float* y,
+                             hipStream_t st);
+void small_linear_bwd_launch(const float* dy, const float* x, const float* w, int B, int I, int O, float* dx, float* dw,
+                             float* db, hipStream_t st);
 void avgpool_fwd_launch(const float* x, int N, int HW, int C, float* y, hipStream_t st);
 void avgpool_bwd_launch(const float* gy, int N, int HW, int C, float* gx, hipStream_t st);
 void maxpool_fwd_launch(const float* x, int N, int H, int W, int C, int k, int s, int p, int Ho, int Wo, float* y,

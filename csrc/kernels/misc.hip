@@ -256,6 +256,62 @@ __global__ __launch_bounds__(256) void colsum_kernel(const float* __restrict__ x
   }
 }
 
+// ------------------------------------------------------------------ narrow Linear (classifier heads)
+// y[r][o] = x[r] . W[o] + b[o] for O <= 64 outputs: one wave per row, lanes stride over I.
+// (VGG-11's fc1 is 512 -> 10: a 128x128 MFMA tile would be >90% padding.)
+__global__ __launch_bounds__(256) void small_linear_fwd_kernel(const float* __restrict__ x, const float* __restrict__ w,
+                                                               const float* __restrict__ b, int B, int I, int O,
+                                                               float* __restrict__ y) {
+  const int lane = threadIdx.x & 63;
+  const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= B) return;
+  const float* xr = x + (long long)r * I;
+  float res = 0.f;  // lane o keeps output o
+  for (int o = 0; o < O; ++o) {
+    const float* wo = w + (long long)o * I;
+    float s = 0.f;
+    for (int i = lane; i < I; i += 64) s = fmaf(xr[i], wo[i], s);
+    s = wave_sum(s);
+    if (lane == o) res = s;
+  }
+  if (lane < O) y[(long long)r * O + lane] = res + (b ? b[lane] : 0.f);
+}
+
+// One launch for all three gradients of the narrow Linear:
+//   blocks [0, nbx)          dX[r][i]  = sum_o dy[r][o] * W[o][i]
+//   blocks [nbx, nbx + nbw)  dW[o][i]  = sum_r dy[r][o] * x[r][i]
+//   last block               db[o]     = sum_r dy[r][o]
+__global__ __launch_bounds__(256) void small_linear_bwd_kernel(const float* __restrict__ dy, const float* __restrict__ x,
+                                                               const float* __restrict__ w, int B, int I, int O,
+                                                               float* __restrict__ dx, float* __restrict__ dw,
+                                                               float* __restrict__ db, int nbx, int nbw) {
+  const int bid = blockIdx.x;
+  if (bid < nbx) {
+    const long long e = (long long)bid * 256 + threadIdx.x;
+    if (e >= (long long)B * I) return;
+    const int r = (int)(e / I), i = (int)(e % I);
+    float s = 0.f;
+    for (int o = 0; o < O; ++o) s = fmaf(dy[(long long)r * O + o], w[(long long)o * I + i], s);
+    dx[e] = s;
+  } else if (bid < nbx + nbw) {
+    const long long e = (long long)(bid - nbx) * 256 + threadIdx.x;
+    if (e >= (long long)O * I) return;
+    const int o = (int)(e / I), i = (int)(e % I);
+    float s = 0.f;
+    for (int r = 0; r < B; ++r) s = fmaf(dy[(long long)r * O + o], x[(long long)r * I + i], s);
+    dw[e] = s;
+  } else if (db) {
+    __shared__ float red[4][64];
+    const int o = threadIdx.x & 63, rl = threadIdx.x >> 6;
+    float s = 0.f;
+    if (o < O)
+      for (int r = rl; r < B; r += 4) s += dy[(long long)r * O + o];
+    red[rl][o] = s;
+    __syncthreads();
+    if (rl == 0 && o < O) db[o] = red[0][o] + red[1][o] + red[2][o] + red[3][o];
+  }
+}
+
 // global average pool over HW of NHWC -> [N][C]; and its backward
 __global__ __launch_bounds__(256) void avgpool_fwd_kernel(const float* __restrict__ x, int N, int HW, int C,
                                                           float* __restrict__ y) {
@@ -362,6 +418,17 @@ void scale_launch(float* x, long long n, float a, hipStream_t st) {
 }
 void colsum_launch(const float* x, int R, int C, float* out, bool accumulate, hipStream_t st) {
   hipLaunchKernelGGL(colsum_kernel, dim3((C + 63) / 64), dim3(256), 0, st, x, R, C, out, accumulate ? 1 : 0);
+}
+void small_linear_fwd_launch(const float* x, const float* w, const float* b, int B, int I, int O, float* y,
+                             hipStream_t st) {
+  hipLaunchKernelGGL(small_linear_fwd_kernel, dim3((B + 3) / 4), dim3(256), 0, st, x, w, b, B, I, O, y);
+}
+void small_linear_bwd_launch(const float* dy, const float* x, const float* w, int B, int I, int O, float* dx, float* dw,
+                             float* db, hipStream_t st) {
+  const int nbx = dx ? (int)(((long long)B * I + 255) / 256) : 0;
+  const int nbw = (int)(((long long)O * I + 255) / 256);
+  hipLaunchKernelGGL(small_linear_bwd_kernel, dim3(nbx + nbw + 1), dim3(256), 0, st, dy, x, w, B, I, O, dx, dw, db,
+                     nbx, nbw);
 }
 void avgpool_fwd_launch(const float* x, int N, int HW, int C, float* y, hipStream_t st) {
   hipLaunchKernelGGL(avgpool_fwd_kernel, dim3(grid_for((long long)N * C)), dim3(256), 0, st, x, N, HW, C, y);

@@ -9,10 +9,14 @@
 // counterpart on channels_last tensors.
 #include "ops.h"
 
+#include <c10/hip/HIPCachingAllocator.h>
+#include <c10/hip/HIPFunctions.h>
+#include <c10/hip/HIPGuard.h>
 #include <c10/hip/HIPStream.h>
 #include <torch/extension.h>
 
 #include <algorithm>
+#include <cstdlib>
 
 #include "../kernels/kernels.h"
 
@@ -60,20 +64,27 @@ int wgrad_blocks_per_cu(int bm, int bn) { return std::max(1, std::min(4, (160 * 
 
 // Split-K factor that best fills whole waves of resident workgroups: a grid just over one wave
 // (e.g. 540 blocks on 512 slots) costs almost two waves of time, so quantisation dominates.
-int choose_splits(long long tiles, int ktiles, int slots, int min_kt) {
+int choose_splits(long long tiles, int ktiles, int slots, int min_kt, double flops, double slab_bytes_per_split) {
   if (tiles >= slots) return 1;
   const int smax = std::max(1, ktiles / std::max(1, min_kt));
-  int best = 1;
-  double best_eff = (double)tiles / (double)slots;
-  for (int w = 1; w <= 2; ++w) {
-    int s = (int)std::min<long long>(smax, (long long)w * slots / tiles);
-    if (s < 1) continue;
+  // modelled time: MFMA work at ~120 TF/s scaled by wave-quantisation efficiency, plus the fp32
+  // split-K slab round trip (write + read) at ~4 TB/s
+  auto cost = [&](int s) {
     const long long blocks = tiles * s;
     const long long waves = (blocks + slots - 1) / slots;
     const double eff = (double)blocks / (double)(waves * slots);
-    if (eff > best_eff + 0.02) {
+    const double slab = s > 1 ? 2.0 * s * slab_bytes_per_split / 4.0e12 : 0.0;
+    return flops / (120.0e12 * eff) + slab;
+  };
+  int best = 1;
+  double best_t = cost(1);
+  for (int w = 1; w <= 4; ++w) {
+    const int s = (int)std::min<long long>(smax, (long long)w * slots / tiles);
+    if (s < 1) continue;
+    const double t = cost(s);
+    if (t < best_t * 0.98) {
       best = s;
-      best_eff = eff;
+      best_t = t;
     }
   }
   return best;
@@ -88,7 +99,7 @@ GemmPlan plan_gemm(long long M, int Nout, int Kdim) {
   g.bm = (tiles128 >= target || M > 4096) ? 128 : 64;
   const long long tiles = ((M + g.bm - 1) / g.bm) * ((Nout + g.bn - 1) / g.bn);
   const int slots = conv_blocks_per_cu(g.bm, g.bn) * num_cus();
-  g.splits = std::min(16, choose_splits(tiles, g.ktiles, slots, 4));
+  g.splits = std::min(16, choose_splits(tiles, g.ktiles, slots, 4, 2.0 * M * Nout * Kdim, 4.0 * M * Nout));
   return g;
 }
 
@@ -103,8 +114,53 @@ WgradPlan plan_wgrad(int Cout, int Kdim, long long M) {
   const long long tiles = (long long)((Cout + w.bm - 1) / w.bm) * ((Kdim + w.bn - 1) / w.bn);
   const int mt = (int)std::min<long long>((M + 31) / 32, 1 << 30);
   const int slots = wgrad_blocks_per_cu(w.bm, w.bn) * num_cus();
-  w.splits = std::min(1024, choose_splits(tiles, mt, slots, 4));
+  w.splits = std::min(1024, choose_splits(tiles, mt, slots, 4, 2.0 * M * Cout * Kdim, 4.0 * Cout * Kdim));
   return w;
+}
+
+// ---- side stream for dgrad || wgrad overlap
+bool conc_enabled() {
+  static const bool on = [] {
+    const char* e = std::getenv("CDP_BWD_OVERLAP");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
+c10::hip::HIPStream side_stream() {
+  static thread_local std::vector<c10::hip::HIPStream> streams;
+  const int dev = c10::hip::current_device();
+  while ((int)streams.size() <= dev) streams.push_back(c10::hip::getStreamFromPool(true, (c10::DeviceIndex)streams.size()));
+  return streams[dev];
+}
+
+struct EventPool {
+  std::vector<hipEvent_t> evs;
+  size_t next = 0;
+  hipEvent_t get() {
+    if (next == evs.size()) {
+      hipEvent_t e;
+      hipEventCreateWithFlags(&e, hipEventDisableTiming);
+      evs.push_back(e);
+    }
+    hipEvent_t e = evs[next];
+    next = (next + 1) % 64;  // reuse after 64 forks (re-recording an event is legal once waited on)
+    return e;
+  }
+};
+
+void fork_to(const c10::hip::HIPStream& side) {
+  static thread_local EventPool pool;
+  hipEvent_t e = pool.get();
+  hipEventRecord(e, c10::hip::getCurrentHIPStream().stream());
+  hipStreamWaitEvent(side.stream(), e, 0);
+}
+
+void join_from(const c10::hip::HIPStream& side) {
+  static thread_local EventPool pool;
+  hipEvent_t e = pool.get();
+  hipEventRecord(e, side.stream());
+  hipStreamWaitEvent(c10::hip::getCurrentHIPStream().stream(), e, 0);
 }
 
 template <class P>
@@ -380,7 +436,20 @@ std::vector<at::Tensor> conv_bn_act_bwd(const at::Tensor& gout_, const at::Tenso
   }
   // x may carry zero-padded channels (RGB stem, see conv_bn_act_fwd)
   const bool padc = x.size(1) != w.size(1);
-  at::Tensor dx;
+  // data- and weight-gradient GEMMs are independent: run the weight gradient on a side stream
+  // (fork/join by events, so it is also a parallel branch under hipGraph capture). Small layers
+  // (VGG's 4x4 / 2x2 blocks) do not fill 256 CUs alone.
+  at::Tensor dx, dw;
+  const bool overlap = need_dx && conc_enabled();
+  c10::hip::HIPStream side = overlap ? side_stream() : c10::hip::getCurrentHIPStream();
+  if (overlap) fork_to(side);
+  {
+    c10::hip::HIPStreamGuard guard(side);
+    dw = conv2d_wgrad_keep(dy, x, {w.size(0), x.size(1), w.size(2), w.size(3)}, stride, pad, dw_out, false,
+                           padc ? w.size(1) : -1);
+  }
+  if (overlap && !(dw_out.has_value() && dw_out->defined()))  // allocated on the side stream, consumed on main
+    c10::hip::HIPCachingAllocator::recordStream(dw.storage().data_ptr(), c10::hip::getCurrentHIPStream());
   if (need_dx) {
     if (padc) {
       at::Tensor dx4 = conv2d_dgrad(dy, pad_channels4(nhwc(w)), {x.size(0), x.size(1), x.size(2), x.size(3)}, stride, pad);
@@ -389,8 +458,7 @@ std::vector<at::Tensor> conv_bn_act_bwd(const at::Tensor& gout_, const at::Tenso
       dx = conv2d_dgrad(dy, w, {x.size(0), x.size(1), x.size(2), x.size(3)}, stride, pad);
     }
   }
-  at::Tensor dw = conv2d_wgrad_keep(dy, x, {w.size(0), x.size(1), w.size(2), w.size(3)}, stride, pad, dw_out, false,
-                                    padc ? w.size(1) : -1);
+  if (overlap) join_from(side);
   return {dx, dw, db, dgamma, dbeta, dres};
 }
 
@@ -403,6 +471,11 @@ at::Tensor linear_fwd(const at::Tensor& x_, const at::Tensor& w_, const c10::opt
   const int B = x.size(0), I = x.size(1), O = w.size(0);
   TORCH_CHECK(w.size(1) == I, "linear shape mismatch");
   at::Tensor y = at::empty({B, O}, x.options());
+  if (O <= 64) {
+    small_linear_fwd_launch(x.data_ptr<float>(), w.data_ptr<float>(), fptr(b), B, I, O, y.data_ptr<float>(),
+                            cur_stream());
+    return y;
+  }
   GemmPlan g = plan_gemm(B, O, I);
   ConvGemmParams p{};
   p.x = x.data_ptr<float>();
@@ -431,6 +504,16 @@ std::vector<at::Tensor> linear_bwd(const at::Tensor& gy_, const at::Tensor& x_, 
   const at::Tensor gy = gy_.contiguous(), x = x_.contiguous(), w = w_.contiguous();
   const int B = x.size(0), I = x.size(1), O = w.size(0);
   hipStream_t st = cur_stream();
+  if (O <= 64) {
+    at::Tensor dx = need_dx ? at::empty({B, I}, x.options()) : at::Tensor();
+    at::Tensor dw = (dw_out.has_value() && dw_out->defined()) ? *dw_out : at::empty({O, I}, x.options());
+    at::Tensor db;
+    if (has_bias) db = (db_out.has_value() && db_out->defined()) ? *db_out : at::empty({O}, x.options());
+    small_linear_bwd_launch(gy.data_ptr<float>(), x.data_ptr<float>(), w.data_ptr<float>(), B, I, O,
+                            need_dx ? dx.data_ptr<float>() : nullptr, dw.data_ptr<float>(),
+                            has_bias ? db.data_ptr<float>() : nullptr, st);
+    return {dx, dw, db};
+  }
   at::Tensor dx;
   if (need_dx) {
     // dx[B, I] = gy[B, O] @ W[O, I]  ->  B^T = W^T [I][O]
