@@ -38,6 +38,9 @@ def parse():
     p.add_argument("--strategy", default="ddp", choices=["ddp", "bucketed_overlap", "allreduce_blocking",
                                                           "gather_scatter"])
     p.add_argument("--no-graph", action="store_true", help="eager steps instead of one hipGraph replay per step")
+    p.add_argument("--graph", action="store_true",
+                   help="force hipGraph capture also for N > 1 (default: graph on 1 GPU, eager multi-GPU: at "
+                        "B=256/GPU the step is GPU-bound, eager and graph time within noise)")
     p.add_argument("--backend", default="native", choices=["native", "torch"],
                    help="torch = stock PyTorch-ROCm ops + torch DDP (comparison only)")
     p.add_argument("--bucket-cap-mb", type=float, default=None)
@@ -131,7 +134,8 @@ def main():
     _dbg("eager warmup done")
 
     graph = None
-    use_graph = not args.no_graph and args.strategy in ("ddp", "bucketed_overlap")
+    use_graph = (not args.no_graph and args.strategy in ("ddp", "bucketed_overlap")
+                 and (world == 1 or args.graph))
     if use_graph:
         try:
             s = torch.cuda.Stream()

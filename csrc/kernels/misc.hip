@@ -257,34 +257,49 @@ __global__ __launch_bounds__(256) void colsum_kernel(const float* __restrict__ x
 }
 
 // ------------------------------------------------------------------ narrow Linear (classifier heads)
-// y[r][o] = x[r] . W[o] + b[o] for O <= 64 outputs: one wave per row, lanes stride over I.
-// (VGG-11's fc1 is 512 -> 10: a 128x128 MFMA tile would be >90% padding.)
+// O <= 16 outputs (VGG-11's fc1 is 512 -> 10: a 128x128 MFMA tile would be >90% padding).
+constexpr int SL_MAXO = 16;
+
+// y[r][o] = x[r] . W[o] + b[o]: one wave per row; each lane keeps its slice of x in registers,
+// accumulates all O partial dot products, and the wave reduces them through LDS once.
 __global__ __launch_bounds__(256) void small_linear_fwd_kernel(const float* __restrict__ x, const float* __restrict__ w,
                                                                const float* __restrict__ b, int B, int I, int O,
                                                                float* __restrict__ y) {
-  const int lane = threadIdx.x & 63;
-  const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (r >= B) return;
-  const float* xr = x + (long long)r * I;
-  float res = 0.f;  // lane o keeps output o
-  for (int o = 0; o < O; ++o) {
-    const float* wo = w + (long long)o * I;
-    float s = 0.f;
-    for (int i = lane; i < I; i += 64) s = fmaf(xr[i], wo[i], s);
-    s = wave_sum(s);
-    if (lane == o) res = s;
+  __shared__ float red[4][SL_MAXO][65];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int r = blockIdx.x * 4 + wv;
+  float part[SL_MAXO];
+#pragma unroll
+  for (int o = 0; o < SL_MAXO; ++o) part[o] = 0.f;
+  if (r < B) {
+    const float* xr = x + (long long)r * I;
+    for (int i = lane; i < I; i += 64) {
+      const float xv = xr[i];
+#pragma unroll
+      for (int o = 0; o < SL_MAXO; ++o)
+        if (o < O) part[o] = fmaf(xv, w[(long long)o * I + i], part[o]);
+    }
   }
-  if (lane < O) y[(long long)r * O + lane] = res + (b ? b[lane] : 0.f);
+#pragma unroll
+  for (int o = 0; o < SL_MAXO; ++o) red[wv][o][lane] = part[o];
+  __syncthreads();
+  if (r < B && lane < O) {
+    float s = 0.f;
+    for (int k = 0; k < 64; ++k) s += red[wv][lane][k];
+    y[(long long)r * O + lane] = s + (b ? b[lane] : 0.f);
+  }
 }
 
-// One launch for all three gradients of the narrow Linear:
-//   blocks [0, nbx)          dX[r][i]  = sum_o dy[r][o] * W[o][i]
-//   blocks [nbx, nbx + nbw)  dW[o][i]  = sum_r dy[r][o] * x[r][i]
-//   last block               db[o]     = sum_r dy[r][o]
+// One launch for all three gradients:
+//   blocks [0, nbx)          dX[r][i] = sum_o dy[r][o] * W[o][i]       (thread per element)
+//   blocks [nbx, nbx + nbw)  dW[o][i] = sum_r dy[r][o] * x[r][i]       (16 columns x 16 row-lanes per
+//                            block; every thread accumulates all O outputs of its column)
+//   last block               db[o]    = sum_r dy[r][o]
 __global__ __launch_bounds__(256) void small_linear_bwd_kernel(const float* __restrict__ dy, const float* __restrict__ x,
                                                                const float* __restrict__ w, int B, int I, int O,
                                                                float* __restrict__ dx, float* __restrict__ dw,
                                                                float* __restrict__ db, int nbx, int nbw) {
+  __shared__ float red[16][SL_MAXO][17];
   const int bid = blockIdx.x;
   if (bid < nbx) {
     const long long e = (long long)bid * 256 + threadIdx.x;
@@ -294,21 +309,40 @@ __global__ __launch_bounds__(256) void small_linear_bwd_kernel(const float* __re
     for (int o = 0; o < O; ++o) s = fmaf(dy[(long long)r * O + o], w[(long long)o * I + i], s);
     dx[e] = s;
   } else if (bid < nbx + nbw) {
-    const long long e = (long long)(bid - nbx) * 256 + threadIdx.x;
-    if (e >= (long long)O * I) return;
-    const int o = (int)(e / I), i = (int)(e % I);
-    float s = 0.f;
-    for (int r = 0; r < B; ++r) s = fmaf(dy[(long long)r * O + o], x[(long long)r * I + i], s);
-    dw[e] = s;
+    const int col = threadIdx.x & 15, rl = threadIdx.x >> 4;
+    const int i = (bid - nbx) * 16 + col;
+    float acc[SL_MAXO];
+#pragma unroll
+    for (int o = 0; o < SL_MAXO; ++o) acc[o] = 0.f;
+    if (i < I) {
+      for (int r = rl; r < B; r += 16) {
+        const float xv = x[(long long)r * I + i];
+#pragma unroll
+        for (int o = 0; o < SL_MAXO; ++o)
+          if (o < O) acc[o] = fmaf(dy[(long long)r * O + o], xv, acc[o]);
+      }
+    }
+#pragma unroll
+    for (int o = 0; o < SL_MAXO; ++o) red[rl][o][col] = acc[o];
+    __syncthreads();
+    // 256 threads finish 16 columns x O outputs
+    const int o = threadIdx.x >> 4;
+    if (o < O && i - col + (threadIdx.x & 15) < I) {
+      const int c = threadIdx.x & 15;
+      float s = 0.f;
+#pragma unroll
+      for (int k = 0; k < 16; ++k) s += red[k][o][c];
+      dw[(long long)o * I + (bid - nbx) * 16 + c] = s;
+    }
   } else if (db) {
-    __shared__ float red[4][64];
+    __shared__ float rdb[4][64];
     const int o = threadIdx.x & 63, rl = threadIdx.x >> 6;
     float s = 0.f;
     if (o < O)
       for (int r = rl; r < B; r += 4) s += dy[(long long)r * O + o];
-    red[rl][o] = s;
+    rdb[rl][o] = s;
     __syncthreads();
-    if (rl == 0 && o < O) db[o] = red[0][o] + red[1][o] + red[2][o] + red[3][o];
+    if (rl == 0 && o < O) db[o] = rdb[0][o] + rdb[1][o] + rdb[2][o] + rdb[3][o];
   }
 }
 
@@ -426,7 +460,7 @@ void small_linear_fwd_launch(const float* x, const float* w, const float* b, int
 void small_linear_bwd_launch(const float* dy, const float* x, const float* w, int B, int I, int O, float* dx, float* dw,
                              float* db, hipStream_t st) {
   const int nbx = dx ? (int)(((long long)B * I + 255) / 256) : 0;
-  const int nbw = (int)(((long long)O * I + 255) / 256);
+  const int nbw = (I + 15) / 16;
   hipLaunchKernelGGL(small_linear_bwd_kernel, dim3(nbx + nbw + 1), dim3(256), 0, st, dy, x, w, B, I, O, dx, dw, db,
                      nbx, nbw);
 }

@@ -121,8 +121,10 @@ WgradPlan plan_wgrad(int Cout, int Kdim, long long M) {
 // ---- side stream for dgrad || wgrad overlap
 bool conc_enabled() {
   static const bool on = [] {
+    // measured on MI355X: running two full-occupancy GEMM grids concurrently is slower (VGG-11
+    // B=256: 3.0 -> 4.8 ms/step), so this is opt-in (CDP_BWD_OVERLAP=1)
     const char* e = std::getenv("CDP_BWD_OVERLAP");
-    return !(e && e[0] == '0');
+    return e && e[0] == '1';
   }();
   return on;
 }
@@ -436,9 +438,8 @@ std::vector<at::Tensor> conv_bn_act_bwd(const at::Tensor& gout_, const at::Tenso
   }
   // x may carry zero-padded channels (RGB stem, see conv_bn_act_fwd)
   const bool padc = x.size(1) != w.size(1);
-  // data- and weight-gradient GEMMs are independent: run the weight gradient on a side stream
-  // (fork/join by events, so it is also a parallel branch under hipGraph capture). Small layers
-  // (VGG's 4x4 / 2x2 blocks) do not fill 256 CUs alone.
+  // data- and weight-gradient GEMMs are independent: optionally run the weight gradient on a side
+  // stream (fork/join by events, so it is also a parallel branch under hipGraph capture).
   at::Tensor dx, dw;
   const bool overlap = need_dx && conc_enabled();
   c10::hip::HIPStream side = overlap ? side_stream() : c10::hip::getCurrentHIPStream();
@@ -471,7 +472,7 @@ at::Tensor linear_fwd(const at::Tensor& x_, const at::Tensor& w_, const c10::opt
   const int B = x.size(0), I = x.size(1), O = w.size(0);
   TORCH_CHECK(w.size(1) == I, "linear shape mismatch");
   at::Tensor y = at::empty({B, O}, x.options());
-  if (O <= 64) {
+  if (O <= 16) {
     small_linear_fwd_launch(x.data_ptr<float>(), w.data_ptr<float>(), fptr(b), B, I, O, y.data_ptr<float>(),
                             cur_stream());
     return y;
@@ -504,7 +505,7 @@ std::vector<at::Tensor> linear_bwd(const at::Tensor& gy_, const at::Tensor& x_, 
   const at::Tensor gy = gy_.contiguous(), x = x_.contiguous(), w = w_.contiguous();
   const int B = x.size(0), I = x.size(1), O = w.size(0);
   hipStream_t st = cur_stream();
-  if (O <= 64) {
+  if (O <= 16) {
     at::Tensor dx = need_dx ? at::empty({B, I}, x.options()) : at::Tensor();
     at::Tensor dw = (dw_out.has_value() && dw_out->defined()) ? *dw_out : at::empty({O, I}, x.options());
     at::Tensor db;
