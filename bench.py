@@ -66,7 +66,12 @@ def main():
 
     import cs744_distributed_data_parallel_amd as cdp
     from cs744_distributed_data_parallel_amd import distributed as dist
-    from cs744_distributed_data_parallel_amd.data import DistributedSampler, DeviceLoader, synthetic_cifar10
+    from cs744_distributed_data_parallel_amd.data import (
+        DeviceLoader,
+        DistributedSampler,
+        synthetic_cifar10,
+        synthetic_imagenet,
+    )
 
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
@@ -79,7 +84,11 @@ def main():
     global_batch = local_batch * world
     cdp.utils.seed_everything(0)
 
-    ds = synthetic_cifar10(args.dataset_size, seed=0, device=dev)
+    imagenet = args.model.startswith("resnet")
+    if imagenet:  # BASELINE.json config #5: ResNet-50, ImageNet-shaped synthetic
+        ds = synthetic_imagenet(min(args.dataset_size, 4 * local_batch * world), seed=0, device=dev)
+    else:
+        ds = synthetic_cifar10(args.dataset_size, seed=0, device=dev)
     sampler = DistributedSampler(ds, num_replicas=world, rank=rank) if world > 1 else None
     loader = DeviceLoader(ds, local_batch, sampler=sampler, shuffle=(world == 1), train=True)
 
@@ -185,7 +194,8 @@ def main():
     img_s = global_batch * args.steps / el
     if rank == 0:
         rec = {
-            "metric": METRIC,
+            "metric": METRIC if not imagenet else
+            "images/sec (whole node) ResNet-50 ImageNet-shaped synthetic, bucketed DDP (BASELINE.json config #5)",
             "value": round(img_s, 1),
             "unit": "images/sec",
             "n_gpus": world,
@@ -194,16 +204,18 @@ def main():
             "ms_per_step": round(ms, 4),
             "higher_is_better": True,
             "scaling": args.scaling,
-            "vs_baseline": round(img_s / BASELINE_IMG_S, 2),
+            "vs_baseline": None if imagenet else round(img_s / BASELINE_IMG_S, 2),
             "dtype": "fp32",
-            "data": "synthetic (random uint8 CIFAR-10-shaped 32x32x3, GPU-resident, on-GPU crop/flip/normalize); "
-                    "random-init weights",
+            "data": ("synthetic (random uint8 ImageNet-shaped 224x224x3, GPU-resident, on-GPU flip/normalize); "
+                     if imagenet else
+                     "synthetic (random uint8 CIFAR-10-shaped 32x32x3, GPU-resident, on-GPU crop/flip/normalize); ")
+                    + "random-init weights",
             "config": {
-                "model": "VGG-11" if args.model == "vgg11" else args.model,
+                "model": {"vgg11": "VGG-11", "resnet50": "ResNet-50"}.get(args.model, args.model),
                 "global_batch": global_batch,
                 "local_batch": local_batch,
                 "seq_len": None,
-                "image_shape": [3, 32, 32],
+                "image_shape": [3, 224, 224] if imagenet else [3, 32, 32],
                 "parallelism": f"dp{world}",
                 "strategy": args.strategy if world > 1 else "single",
                 "backend": args.backend,

@@ -275,9 +275,10 @@ __global__ __launch_bounds__(256) void small_linear_fwd_kernel(const float* __re
     const float* xr = x + (long long)r * I;
     for (int i = lane; i < I; i += 64) {
       const float xv = xr[i];
+      // no per-o branch: clamped rows keep every load unconditional (a runtime-predicated load per
+      // element makes hipcc wait vmcnt(0) around each one); rows >= O are never stored
 #pragma unroll
-      for (int o = 0; o < SL_MAXO; ++o)
-        if (o < O) part[o] = fmaf(xv, w[(long long)o * I + i], part[o]);
+      for (int o = 0; o < SL_MAXO; ++o) part[o] = fmaf(xv, w[(long long)min(o, O - 1) * I + i], part[o]);
     }
   }
 #pragma unroll
@@ -318,8 +319,7 @@ __global__ __launch_bounds__(256) void small_linear_bwd_kernel(const float* __re
       for (int r = rl; r < B; r += 16) {
         const float xv = x[(long long)r * I + i];
 #pragma unroll
-        for (int o = 0; o < SL_MAXO; ++o)
-          if (o < O) acc[o] = fmaf(dy[(long long)r * O + o], xv, acc[o]);
+        for (int o = 0; o < SL_MAXO; ++o) acc[o] = fmaf(dy[(long long)r * O + min(o, O - 1)], xv, acc[o]);
       }
     }
 #pragma unroll
