@@ -1,0 +1,125 @@
+// Shared epilogue of the implicit-GEMM conv kernels (fp32-MFMA and split-bf16 variants).
+//
+// The accumulator tile layout is the same for v_mfma_f32_32x32x2_f32 and
+// v_mfma_f32_32x32x16_bf16 (C/D map is dtype-independent on gfx950): lane l holds column
+// l&31 and rows (r&3) + 8*(r>>2) + 4*(l>>5) of each 32x32 tile.
+//
+// splits > 1: store the raw partial tile into its split-K slab.
+// splits == 1: add bias, store, and (when p.part) emit per-block BatchNorm partials
+// (mean_b, M2_b per column, two exact passes over the registers) so the following
+// BatchNorm never re-reads the conv output for its statistics.
+#pragma once
+#include "common.h"
+#include "kernels.h"
+
+namespace cdp {
+
+template <int BM, int BN>
+__device__ __forceinline__ void conv_epilogue(const ConvGemmParams& p, f32x16 (&acc)[BM / 64][BN / 64], float* red,
+                                              int m0, int n0, int tm_idx, int split) {
+  constexpr int TM = BM / 64, TN = BN / 64;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wid = tid >> 6;
+  const int wm = wid >> 1, wn = wid & 1;
+  const int l32 = lane & 31;
+  const int hh = lane >> 5;
+  if (p.splits > 1) {
+    float* out = p.y + (long long)split * p.M * p.Nout;
+#pragma unroll
+    for (int a = 0; a < TM; ++a)
+#pragma unroll
+      for (int b = 0; b < TN; ++b) {
+        const int n = n0 + wn * (BN / 2) + b * 32 + l32;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int m = m0 + wm * (BM / 2) + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
+          if (m < p.M && n < p.Nout) out[(long long)m * p.Nout + n] = acc[a][b][r];
+        }
+      }
+    return;
+  }
+
+  float bias_v[TN];
+#pragma unroll
+  for (int b = 0; b < TN; ++b) {
+    const int n = n0 + wn * (BN / 2) + b * 32 + l32;
+    bias_v[b] = (p.bias && n < p.Nout) ? p.bias[n] : 0.f;
+  }
+#pragma unroll
+  for (int a = 0; a < TM; ++a)
+#pragma unroll
+    for (int b = 0; b < TN; ++b) {
+      const int n = n0 + wn * (BN / 2) + b * 32 + l32;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = m0 + wm * (BM / 2) + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
+        const float v = acc[a][b][r] + bias_v[b];
+        acc[a][b][r] = v;
+        if (m < p.M && n < p.Nout) p.y[(long long)m * p.Nout + n] = v;
+      }
+    }
+  if (!p.part) return;
+
+  __syncthreads();  // `red` aliases the operand LDS
+  const int cnt = min(BM, p.M - m0);
+  float colsum[TN];
+#pragma unroll
+  for (int b = 0; b < TN; ++b) {
+    float s = 0.f;
+#pragma unroll
+    for (int a = 0; a < TM; ++a)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = m0 + wm * (BM / 2) + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
+        s += (m < p.M) ? acc[a][b][r] : 0.f;
+      }
+    s += __shfl_xor(s, 32, kWave);
+    colsum[b] = s;
+  }
+  if (hh == 0) {
+#pragma unroll
+    for (int b = 0; b < TN; ++b) red[wm * BN + wn * (BN / 2) + b * 32 + l32] = colsum[b];
+  }
+  __syncthreads();
+  float mean_b[TN];
+#pragma unroll
+  for (int b = 0; b < TN; ++b) {
+    const int c = wn * (BN / 2) + b * 32 + l32;
+    mean_b[b] = (red[c] + red[BN + c]) / (float)cnt;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int b = 0; b < TN; ++b) {
+    float s = 0.f;
+#pragma unroll
+    for (int a = 0; a < TM; ++a)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = m0 + wm * (BM / 2) + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
+        const float d = acc[a][b][r] - mean_b[b];
+        s += (m < p.M) ? d * d : 0.f;
+      }
+    s += __shfl_xor(s, 32, kWave);
+    colsum[b] = s;
+  }
+  if (hh == 0) {
+#pragma unroll
+    for (int b = 0; b < TN; ++b) red[wm * BN + wn * (BN / 2) + b * 32 + l32] = colsum[b];
+  }
+  __syncthreads();
+  if (wm == 0 && hh == 0) {
+#pragma unroll
+    for (int b = 0; b < TN; ++b) {
+      const int c = wn * (BN / 2) + b * 32 + l32;
+      const int n = n0 + c;
+      if (n < p.Nout) {
+        float* dst = p.part + ((long long)tm_idx * p.Nout + n) * 2;
+        dst[0] = mean_b[b];
+        dst[1] = red[c] + red[BN + c];
+      }
+    }
+  }
+}
+
+}  // namespace cdp

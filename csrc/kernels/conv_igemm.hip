@@ -21,6 +21,7 @@
 // reads 4 consecutive k per ds_read_b128.
 #include "common.h"
 #include "kernels.h"
+#include "conv_epilogue.h"
 
 namespace cdp {
 
@@ -237,107 +238,7 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvGemmParams p) {
     }
   }
 
-  // ---------------- epilogue ----------------
-  const int hh = lane >> 5;
-  if (p.splits > 1) {
-    float* out = p.y + (long long)split * p.M * p.Nout;
-#pragma unroll
-    for (int a = 0; a < TM; ++a)
-#pragma unroll
-      for (int b = 0; b < TN; ++b) {
-        const int n = n0 + wn * (BN / 2) + b * 32 + l32;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int m = m0 + wm * (BM / 2) + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
-          if (m < p.M && n < p.Nout) out[(long long)m * p.Nout + n] = acc[a][b][r];
-        }
-      }
-    return;
-  }
-
-  float bias_v[TN];
-#pragma unroll
-  for (int b = 0; b < TN; ++b) {
-    const int n = n0 + wn * (BN / 2) + b * 32 + l32;
-    bias_v[b] = (p.bias && n < p.Nout) ? p.bias[n] : 0.f;
-  }
-#pragma unroll
-  for (int a = 0; a < TM; ++a)
-#pragma unroll
-    for (int b = 0; b < TN; ++b) {
-      const int n = n0 + wn * (BN / 2) + b * 32 + l32;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int m = m0 + wm * (BM / 2) + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
-        const float v = acc[a][b][r] + bias_v[b];
-        acc[a][b][r] = v;
-        if (m < p.M && n < p.Nout) p.y[(long long)m * p.Nout + n] = v;
-      }
-    }
-  if (!p.part) return;
-
-  // Per-block BatchNorm partials over this tile's valid rows: mean_b and M2_b per column.
-  // Two passes over the accumulators already in registers (exact two-pass variance per block).
-  __syncthreads();  // smem reuse
-  float* red = smem;  // [2][BN]
-  const int cnt = min(BM, p.M - m0);
-  float colsum[TN];
-#pragma unroll
-  for (int b = 0; b < TN; ++b) {
-    float s = 0.f;
-#pragma unroll
-    for (int a = 0; a < TM; ++a)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int m = m0 + wm * (BM / 2) + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
-        s += (m < p.M) ? acc[a][b][r] : 0.f;
-      }
-    s += __shfl_xor(s, 32, kWave);
-    colsum[b] = s;
-  }
-  if (hh == 0) {
-#pragma unroll
-    for (int b = 0; b < TN; ++b) red[wm * BN + wn * (BN / 2) + b * 32 + l32] = colsum[b];
-  }
-  __syncthreads();
-  float mean_b[TN];
-#pragma unroll
-  for (int b = 0; b < TN; ++b) {
-    const int c = wn * (BN / 2) + b * 32 + l32;
-    mean_b[b] = (red[c] + red[BN + c]) / (float)cnt;
-  }
-  __syncthreads();
-#pragma unroll
-  for (int b = 0; b < TN; ++b) {
-    float s = 0.f;
-#pragma unroll
-    for (int a = 0; a < TM; ++a)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int m = m0 + wm * (BM / 2) + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
-        const float d = acc[a][b][r] - mean_b[b];
-        s += (m < p.M) ? d * d : 0.f;
-      }
-    s += __shfl_xor(s, 32, kWave);
-    colsum[b] = s;
-  }
-  if (hh == 0) {
-#pragma unroll
-    for (int b = 0; b < TN; ++b) red[wm * BN + wn * (BN / 2) + b * 32 + l32] = colsum[b];
-  }
-  __syncthreads();
-  if (wm == 0 && hh == 0) {
-#pragma unroll
-    for (int b = 0; b < TN; ++b) {
-      const int c = wn * (BN / 2) + b * 32 + l32;
-      const int n = n0 + c;
-      if (n < p.Nout) {
-        float* dst = p.part + ((long long)tm_idx * p.Nout + n) * 2;
-        dst[0] = mean_b[b];
-        dst[1] = red[c] + red[BN + c];
-      }
-    }
-  }
+  conv_epilogue<BM, BN>(p, acc, smem, m0, n0, tm_idx, split);
 }
 
 // Sum split-K slabs, add bias, store, and emit BatchNorm partials over RB-row groups.

@@ -1,0 +1,301 @@
+// Implicit-GEMM convolution at fp32 accuracy on the bf16 matrix cores (gfx950).
+//
+// gfx950 has no reduced-precision fp32 MFMA (no xf32) and its exact fp32-input MFMA
+// (v_mfma_f32_32x32x2_f32) runs at 1/16 of the bf16 rate. This kernel keeps fp32 numerics while
+// using v_mfma_f32_32x32x16_bf16: every fp32 operand is split into three bf16 terms,
+//     a = a0 + a1 + a2,   a0 = rn(a), a1 = rn(a - a0), a2 = rn(a - a0 - a1)
+// (each subtraction is exact, and three 8-bit significands cover fp32's 24 bits, so the split is
+// exact up to underflow), and the product is formed from the six terms of order >= 2^-16:
+//     a*b ~= a0b0 + (a0b1 + a1b0) + (a0b2 + a1b1 + a2b0)
+// accumulated in fp32 by the MFMA. The dropped terms are <= 2^-23 |ab| -- the size of one fp32
+// rounding -- so the result matches an fp32 GEMM to within the accumulation error of the fp32
+// MFMA itself (tests/test_kernels_gpu.py::test_x3_gemm_accuracy measures both against fp64).
+// Six bf16 MFMAs cost 6*32 = 192 cycles per 32x32x16 step versus 8*64 = 512 for eight fp32
+// MFMAs: 2.67x the MFMA throughput.
+//
+// Same GEMM mapping as conv_igemm.hip (forward / transposed-gather data gradient, MODE 0/1/2
+// gathers, identical epilogue). Pipeline: operands are gathered global -> registers (prefetch
+// of K-tile t+1 overlaps the MFMAs of tile t), split into three bf16 planes with
+// v_cvt_pk_bf16_f32 and stored to a single LDS stage; two barriers per K-tile. 60 KB of LDS for
+// 128x128 keeps two workgroups per CU, so one block's split/store/barrier hides under the other's
+// MFMAs. Each LDS row holds 32 bf16 + 8 pad (80 B pitch): the ds_read_b128 fragment reads of a
+// 16-lane group hit 16 distinct 16-B bank quads (5r mod 16 is a permutation), conflict free.
+#include "common.h"
+#include "kernels.h"
+#include "conv_epilogue.h"
+
+namespace cdp {
+
+namespace {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+constexpr int BK = 32;
+constexpr int LDH = BK + 8;  // bf16 per LDS row
+
+__device__ __forceinline__ void split3(const float (&v)[8], bf16x8& s0, bf16x8& s1, bf16x8& s2) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const __bf16 a = (__bf16)v[j];
+    const float r = v[j] - (float)a;
+    const __bf16 b = (__bf16)r;
+    const float r2 = r - (float)b;
+    s0[j] = a;
+    s1[j] = b;
+    s2[j] = (__bf16)r2;
+  }
+}
+
+template <int BM, int BN, int MODE, bool DGRAD>
+__global__ __launch_bounds__(256, 2) void conv_x3_kernel(ConvGemmParams p) {
+  constexpr int TM = BM / 64;
+  constexpr int TN = BN / 64;
+  constexpr int A_LD = BM / 64;  // A rows per thread (row = tid/4 + 64 i), 8 consecutive k each
+  constexpr int B_LD = BN / 64;
+  constexpr int PA = BM * LDH, PB = BN * LDH;
+  constexpr int SMEM_BYTES = 3 * (PA + PB) * 2;
+  static_assert(SMEM_BYTES >= 2 * BN * 4, "epilogue scratch");
+  __shared__ __attribute__((aligned(16))) unsigned char smem_raw[SMEM_BYTES];
+  __bf16* As = reinterpret_cast<__bf16*>(smem_raw);  // [3][BM][LDH]
+  __bf16* Bs = As + 3 * PA;                          // [3][BN][LDH]
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wid = tid >> 6;
+  const int wm = wid >> 1, wn = wid & 1;
+
+  const int ntn = (p.Nout + BN - 1) / BN;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int tn_idx = bid % ntn;
+  const int rest = bid / ntn;
+  const int split = rest % p.splits;
+  const int tm_idx = rest / p.splits;
+  const int m0 = tm_idx * BM, n0 = tn_idx * BN;
+  const int kt_begin = (int)(((long long)split * p.ktiles) / p.splits);
+  const int kt_end = (int)(((long long)(split + 1) * p.ktiles) / p.splits);
+  const int PQ = p.P * p.Q;
+
+  const int kq = (tid & 3) * 8;  // this thread's 8 consecutive k within the tile
+  const int rrow = tid >> 2;     // + 64 i
+
+  const float* a_base[A_LD];
+  int a_h[A_LD], a_w[A_LD];
+  bool a_ok[A_LD];
+#pragma unroll
+  for (int i = 0; i < A_LD; ++i) {
+    const int m = m0 + rrow + 64 * i;
+    a_ok[i] = m < p.M;
+    const int mm = a_ok[i] ? m : 0;
+    const int n = fdiv(mm, p.fd_PQ);
+    const int rem = mm - n * PQ;
+    const int pp = fdiv(rem, p.fd_Q);
+    const int qq = rem - pp * p.Q;
+    a_base[i] = p.x + (long long)n * p.H * p.W * p.C;
+    if (DGRAD) {
+      a_h[i] = pp + p.pad;
+      a_w[i] = qq + p.pad;
+    } else {
+      a_h[i] = pp * p.stride - p.pad;
+      a_w[i] = qq * p.stride - p.pad;
+    }
+  }
+
+  auto pix_ok = [&](int i, int kh, int kw, int& ih, int& iw) -> bool {
+    if (DGRAD) {
+      int oh = a_h[i] - kh, ow = a_w[i] - kw;
+      if (oh < 0 || ow < 0) return false;
+      if (p.stride != 1) {
+        if ((oh % p.stride) | (ow % p.stride)) return false;
+        oh /= p.stride;
+        ow /= p.stride;
+      }
+      ih = oh;
+      iw = ow;
+      return oh < p.H && ow < p.W;
+    } else {
+      ih = a_h[i] + kh;
+      iw = a_w[i] + kw;
+      return (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W;
+    }
+  };
+
+  float va[A_LD][8], vb[B_LD][8];
+
+  auto put4 = [](float (&d)[8], int off, float4 v) {
+    d[off] = v.x;
+    d[off + 1] = v.y;
+    d[off + 2] = v.z;
+    d[off + 3] = v.w;
+  };
+
+  auto load_tile = [&](int kt) {
+    const int r0 = kt * BK + kq;
+    if (MODE == 0) {
+      const int tap = fdiv(kt * BK, p.fd_C);
+      const int c0 = r0 - tap * p.C;
+      const int kh = fdiv(tap, p.fd_KW), kw = tap - kh * p.KW;
+#pragma unroll
+      for (int i = 0; i < A_LD; ++i) {
+        int ih, iw;
+        const bool ok = a_ok[i] && pix_ok(i, kh, kw, ih, iw);
+        const float* src = a_base[i] + ((long long)ih * p.W + iw) * p.C + c0;
+        put4(va[i], 0, ok ? ld4(src) : f4zero());
+        put4(va[i], 4, ok ? ld4(src + 4) : f4zero());
+      }
+    } else if (MODE == 1) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int r = r0 + 4 * h;
+        const bool rok = r < p.Kdim;
+        const int tap = fdiv(r, p.fd_C);
+        const int c = r - tap * p.C;
+        const int kh = fdiv(tap, p.fd_KW), kw = tap - kh * p.KW;
+#pragma unroll
+        for (int i = 0; i < A_LD; ++i) {
+          int ih, iw;
+          const bool ok = rok && a_ok[i] && pix_ok(i, kh, kw, ih, iw);
+          put4(va[i], 4 * h, ok ? ld4(a_base[i] + ((long long)ih * p.W + iw) * p.C + c) : f4zero());
+        }
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int r = r0 + j;
+        const bool rok = r < p.Kdim;
+        const int tap = fdiv(rok ? r : 0, p.fd_C);
+        const int c = r - tap * p.C;
+        const int kh = fdiv(tap, p.fd_KW), kw = tap - kh * p.KW;
+#pragma unroll
+        for (int i = 0; i < A_LD; ++i) {
+          int ih, iw;
+          const bool ok = rok && a_ok[i] && pix_ok(i, kh, kw, ih, iw);
+          va[i][j] = ok ? a_base[i][((long long)ih * p.W + iw) * p.C + c] : 0.f;
+        }
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < B_LD; ++i) {
+      const int n = n0 + rrow + 64 * i;
+      const float* src = p.w + (long long)n * p.Kdim + r0;
+      if (MODE != 2) {
+        const bool ok0 = n < p.Nout && r0 < p.Kdim;
+        const bool ok1 = n < p.Nout && r0 + 4 < p.Kdim;
+        put4(vb[i], 0, ok0 ? ld4(src) : f4zero());
+        put4(vb[i], 4, ok1 ? ld4(src + 4) : f4zero());
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) vb[i][j] = (n < p.Nout && r0 + j < p.Kdim) ? src[j] : 0.f;
+      }
+    }
+  };
+
+  auto store_tile = [&]() {
+#pragma unroll
+    for (int i = 0; i < A_LD; ++i) {
+      bf16x8 s0, s1, s2;
+      split3(va[i], s0, s1, s2);
+      __bf16* d = As + (rrow + 64 * i) * LDH + kq;
+      *reinterpret_cast<bf16x8*>(d) = s0;
+      *reinterpret_cast<bf16x8*>(d + PA) = s1;
+      *reinterpret_cast<bf16x8*>(d + 2 * PA) = s2;
+    }
+#pragma unroll
+    for (int i = 0; i < B_LD; ++i) {
+      bf16x8 s0, s1, s2;
+      split3(vb[i], s0, s1, s2);
+      __bf16* d = Bs + (rrow + 64 * i) * LDH + kq;
+      *reinterpret_cast<bf16x8*>(d) = s0;
+      *reinterpret_cast<bf16x8*>(d + PB) = s1;
+      *reinterpret_cast<bf16x8*>(d + 2 * PB) = s2;
+    }
+  };
+
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int a = 0; a < TM; ++a)
+#pragma unroll
+    for (int b = 0; b < TN; ++b)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
+
+  const int l32 = lane & 31;
+  const int koff = (lane >> 5) * 8;
+
+  if (kt_begin < kt_end) {
+    load_tile(kt_begin);
+    store_tile();
+    __syncthreads();
+    for (int kt = kt_begin; kt < kt_end; ++kt) {
+      const bool more = kt + 1 < kt_end;
+      if (more) load_tile(kt + 1);
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        bf16x8 af[TM][3], bf[TN][3];
+#pragma unroll
+        for (int a = 0; a < TM; ++a) {
+          const __bf16* src = As + (wm * (BM / 2) + a * 32 + l32) * LDH + s * 16 + koff;
+#pragma unroll
+          for (int q = 0; q < 3; ++q) af[a][q] = *reinterpret_cast<const bf16x8*>(src + q * PA);
+        }
+#pragma unroll
+        for (int b = 0; b < TN; ++b) {
+          const __bf16* src = Bs + (wn * (BN / 2) + b * 32 + l32) * LDH + s * 16 + koff;
+#pragma unroll
+          for (int q = 0; q < 3; ++q) bf[b][q] = *reinterpret_cast<const bf16x8*>(src + q * PB);
+        }
+#pragma unroll
+        for (int a = 0; a < TM; ++a)
+#pragma unroll
+          for (int b = 0; b < TN; ++b) {
+            f32x16 c = acc[a][b];
+            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[a][2], bf[b][0], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[a][1], bf[b][1], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[a][0], bf[b][2], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[a][1], bf[b][0], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[a][0], bf[b][1], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[a][0], bf[b][0], c, 0, 0, 0);
+            acc[a][b] = c;
+          }
+      }
+      __syncthreads();
+      if (more) {
+        store_tile();
+        __syncthreads();
+      }
+    }
+  }
+
+  conv_epilogue<BM, BN>(p, acc, reinterpret_cast<float*>(smem_raw), m0, n0, tm_idx, split);
+}
+
+template <int BM, int BN, int MODE, bool DGRAD>
+void launch_x3(const ConvGemmParams& p, int ntiles, hipStream_t st) {
+  hipLaunchKernelGGL((conv_x3_kernel<BM, BN, MODE, DGRAD>), dim3(ntiles * p.splits), dim3(256), 0, st, p);
+}
+
+template <int MODE, bool DGRAD>
+void dispatch_x3(const ConvGemmParams& p, int bm, int bn, hipStream_t st) {
+  const int ntm = (p.M + bm - 1) / bm, ntn = (p.Nout + bn - 1) / bn;
+  const int nt = ntm * ntn;
+  if (bm == 128 && bn == 128) launch_x3<128, 128, MODE, DGRAD>(p, nt, st);
+  else if (bm == 128 && bn == 64) launch_x3<128, 64, MODE, DGRAD>(p, nt, st);
+  else if (bm == 64 && bn == 128) launch_x3<64, 128, MODE, DGRAD>(p, nt, st);
+  else launch_x3<64, 64, MODE, DGRAD>(p, nt, st);
+}
+
+}  // namespace
+
+void conv_x3_launch(const ConvGemmParams& p, int bm, int bn, bool dgrad, hipStream_t st) {
+  if ((p.C % BK) == 0 && (p.Kdim % BK) == 0) {
+    if (dgrad) dispatch_x3<0, true>(p, bm, bn, st);
+    else dispatch_x3<0, false>(p, bm, bn, st);
+  } else if ((p.C % 4) == 0 && (p.Kdim % 4) == 0) {
+    if (dgrad) dispatch_x3<1, true>(p, bm, bn, st);
+    else dispatch_x3<1, false>(p, bm, bn, st);
+  } else {
+    if (dgrad) dispatch_x3<2, true>(p, bm, bn, st);
+    else dispatch_x3<2, false>(p, bm, bn, st);
+  }
+}
+
+}  // namespace cdp

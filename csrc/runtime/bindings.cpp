@@ -14,6 +14,8 @@ PYBIND11_MODULE(_C, m) {
   m.attr("ARCH") = "gfx950";
 
   // -------------------------------------------------------------- kernels
+  m.def("set_conv_gemm", &set_conv_gemm, py::arg("mode"), "select the conv GEMM engine: x3 (3-term bf16 split, fp32-accurate) or f32 (exact fp32 MFMA)");
+  m.def("get_conv_gemm", &get_conv_gemm);
   m.def("conv2d_fwd", &conv2d_fwd, py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("stride"), py::arg("pad"),
         py::arg("want_stats") = false);
   m.def("conv2d_dgrad", &conv2d_dgrad);

@@ -17,6 +17,7 @@
 
 #include <algorithm>
 #include <cstdlib>
+#include <string>
 
 #include "../kernels/kernels.h"
 
@@ -58,23 +59,43 @@ int num_cus() {
   return cus;
 }
 
-// Workgroups each kernel keeps resident per CU (LDS-bound; VGPRs allow at least 2 waves/SIMD).
-int conv_blocks_per_cu(int bm, int bn) { return std::max(1, std::min(4, (160 * 1024) / (2 * (bm + bn) * 36 * 4))); }
+// Conv GEMM engine: 1 = 3-term bf16 split on the bf16 MFMA (conv_x3.hip, fp32-accurate, default),
+// 0 = exact fp32-input MFMA (conv_igemm.hip). CDP_CONV_GEMM=f32 selects the latter at start-up.
+int& conv_gemm_mode() {
+  static int m = [] {
+    const char* e = std::getenv("CDP_CONV_GEMM");
+    return (e && std::string(e) == "f32") ? 0 : 1;
+  }();
+  return m;
+}
+
+void conv_launch(const ConvGemmParams& p, int bm, int bn, bool dgrad, hipStream_t st) {
+  if (conv_gemm_mode() == 1) conv_x3_launch(p, bm, bn, dgrad, st);
+  else conv_igemm_launch(p, bm, bn, dgrad, st);
+}
+
+// Workgroups each kernel keeps resident per CU (min of the LDS and VGPR limits of the build).
+int conv_blocks_per_cu(int bm, int bn) {
+  if (conv_gemm_mode() == 1) return (bm + bn) >= 256 ? 2 : (bm + bn) >= 192 ? 3 : 5;
+  return std::max(1, std::min(4, (160 * 1024) / (2 * (bm + bn) * 36 * 4)));
+}
+double conv_mfma_rate() { return conv_gemm_mode() == 1 ? 250.0e12 : 120.0e12; }
 int wgrad_blocks_per_cu(int bm, int bn) { return std::max(1, std::min(4, (160 * 1024) / (2 * 32 * (bm + bn + 8) * 4))); }
 
 // Split-K factor that best fills whole waves of resident workgroups: a grid just over one wave
 // (e.g. 540 blocks on 512 slots) costs almost two waves of time, so quantisation dominates.
-int choose_splits(long long tiles, int ktiles, int slots, int min_kt, double flops, double slab_bytes_per_split) {
+int choose_splits(long long tiles, int ktiles, int slots, int min_kt, double flops, double slab_bytes_per_split,
+                  double rate = 120.0e12) {
   if (tiles >= slots) return 1;
   const int smax = std::max(1, ktiles / std::max(1, min_kt));
-  // modelled time: MFMA work at ~120 TF/s scaled by wave-quantisation efficiency, plus the fp32
+  // modelled time: MFMA work at `rate` scaled by wave-quantisation efficiency, plus the fp32
   // split-K slab round trip (write + read) at ~4 TB/s
   auto cost = [&](int s) {
     const long long blocks = tiles * s;
     const long long waves = (blocks + slots - 1) / slots;
     const double eff = (double)blocks / (double)(waves * slots);
     const double slab = s > 1 ? 2.0 * s * slab_bytes_per_split / 4.0e12 : 0.0;
-    return flops / (120.0e12 * eff) + slab;
+    return flops / (rate * eff) + slab;
   };
   int best = 1;
   double best_t = cost(1);
@@ -99,7 +120,8 @@ GemmPlan plan_gemm(long long M, int Nout, int Kdim) {
   g.bm = (tiles128 >= target || M > 4096) ? 128 : 64;
   const long long tiles = ((M + g.bm - 1) / g.bm) * ((Nout + g.bn - 1) / g.bn);
   const int slots = conv_blocks_per_cu(g.bm, g.bn) * num_cus();
-  g.splits = std::min(16, choose_splits(tiles, g.ktiles, slots, 4, 2.0 * M * Nout * Kdim, 4.0 * M * Nout));
+  g.splits = std::min(16, choose_splits(tiles, g.ktiles, slots, 4, 2.0 * M * Nout * Kdim, 4.0 * M * Nout,
+                                        conv_mfma_rate()));
   return g;
 }
 
@@ -185,6 +207,12 @@ at::Tensor pad_channels4(const at::Tensor& t) {
 
 }  // namespace
 
+void set_conv_gemm(const std::string& mode) {
+  TORCH_CHECK(mode == "x3" || mode == "f32", "conv gemm engine must be 'x3' or 'f32', got ", mode);
+  conv_gemm_mode() = mode == "x3" ? 1 : 0;
+}
+std::string get_conv_gemm() { return conv_gemm_mode() == 1 ? "x3" : "f32"; }
+
 // ---------------------------------------------------------------- conv forward
 // Returns y (channels_last [N, Cout, P, Q]). When `part` is requested the per-tile BatchNorm
 // partials are returned in a second tensor [nparts, Cout, 2] together with rows-per-part.
@@ -225,11 +253,11 @@ std::vector<at::Tensor> conv2d_fwd(const at::Tensor& x_, const at::Tensor& w_, c
       p.part = part.data_ptr<float>();
       rpp = at::full({1}, g.bm, opts.dtype(at::kInt).device(at::kCPU));
     }
-    conv_igemm_launch(p, g.bm, g.bn, false, st);
+    conv_launch(p, g.bm, g.bn, false, st);
   } else {
     at::Tensor slab = at::empty({g.splits, M, Co}, opts);
     p.y = slab.data_ptr<float>();
-    conv_igemm_launch(p, g.bm, g.bn, false, st);
+    conv_launch(p, g.bm, g.bn, false, st);
     float* partp = nullptr;
     if (want_stats) {
       const int rb = splitk_rows_per_part();
@@ -274,11 +302,11 @@ at::Tensor conv2d_dgrad(const at::Tensor& dy_, const at::Tensor& w_, std::vector
   set_divs(p);
   if (g.splits == 1) {
     p.y = dx.data_ptr<float>();
-    conv_igemm_launch(p, g.bm, g.bn, true, st);
+    conv_launch(p, g.bm, g.bn, true, st);
   } else {
     at::Tensor slab = at::empty({g.splits, M, C}, opts);
     p.y = slab.data_ptr<float>();
-    conv_igemm_launch(p, g.bm, g.bn, true, st);
+    conv_launch(p, g.bm, g.bn, true, st);
     splitk_reduce_launch(slab.data_ptr<float>(), g.splits, (int)M, C, nullptr, dx.data_ptr<float>(), nullptr, st);
   }
   return dx;
@@ -488,11 +516,11 @@ at::Tensor linear_fwd(const at::Tensor& x_, const at::Tensor& w_, const c10::opt
   if (g.splits == 1) {
     p.y = y.data_ptr<float>();
     p.bias = fptr(b);
-    conv_igemm_launch(p, g.bm, g.bn, false, st);
+    conv_launch(p, g.bm, g.bn, false, st);
   } else {
     at::Tensor slab = at::empty({g.splits, B, O}, x.options());
     p.y = slab.data_ptr<float>();
-    conv_igemm_launch(p, g.bm, g.bn, false, st);
+    conv_launch(p, g.bm, g.bn, false, st);
     splitk_reduce_launch(slab.data_ptr<float>(), g.splits, B, O, fptr(b), y.data_ptr<float>(), nullptr, st);
   }
   return y;

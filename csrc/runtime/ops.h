@@ -6,6 +6,8 @@
 
 namespace cdp {
 
+void set_conv_gemm(const std::string& mode);
+std::string get_conv_gemm();
 std::vector<at::Tensor> conv2d_fwd(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tensor>& bias,
                                    int64_t stride, int64_t pad, bool want_stats);
 at::Tensor conv2d_dgrad(const at::Tensor& dy, const at::Tensor& w, std::vector<int64_t> in_shape, int64_t stride,

@@ -264,3 +264,35 @@ def test_stack_mean_and_scale():
     assert torch.allclose(out, torch.stack(srcs).mean(0), atol=1e-6)
     C().scale_(out, 0.5)
     assert torch.allclose(out, torch.stack(srcs).mean(0) * 0.5, atol=1e-6)
+
+
+def _rms_rel(a, b):
+    a, b = a.double().cpu(), b.double().cpu()
+    return ((a - b).norm() / b.norm().clamp_min(1e-30)).item()
+
+
+@pytest.mark.parametrize("N,Ci,H,W,Co,k,s,p", [CONV_CASES[i] for i in (0, 1, 3, 5, 7, 9)])
+def test_x3_engine_is_as_accurate_as_fp32_mfma(N, Ci, H, W, Co, k, s, p):
+    """The 3-term bf16 split engine (conv_x3.hip) must match the exact fp32-input MFMA engine's
+    error against fp64, for forward and data-gradient GEMMs."""
+    torch.manual_seed(1)
+    x = torch.randn(N, Ci, H, W, device="cuda")
+    w = torch.randn(Co, Ci, k, k, device="cuda") * (1.0 / (Ci * k * k) ** 0.5)
+    xr = x.double().cpu().requires_grad_()
+    ref = F.conv2d(xr, w.double().cpu(), None, s, p)
+    gy = torch.randn(ref.shape, device="cuda")
+    ref.backward(gy.double().cpu())
+    orig = C().get_conv_gemm()
+    errs = {}
+    try:
+        for mode in ("f32", "x3"):
+            C().set_conv_gemm(mode)
+            y = C().conv2d_fwd(cl(x), cl(w), None, s, p, False)[0]
+            dx = C().conv2d_dgrad(cl(gy), cl(w), list(x.shape), s, p)
+            errs[mode] = (_rms_rel(y, ref.detach()), _rms_rel(dx, xr.grad), rel_err(y, ref.detach()))
+    finally:
+        C().set_conv_gemm(orig)
+    print("conv errs (rms fwd, rms dgrad, max fwd)", errs)
+    for i in range(3):
+        assert errs["x3"][i] <= 2.0 * errs["f32"][i] + 1e-9, errs
+    assert errs["x3"][0] < 1e-6 and errs["x3"][1] < 1e-6, errs
