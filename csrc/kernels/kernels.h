@@ -62,7 +62,8 @@ void splitk_reduce_launch(const float* slab, int S, int M, int Nout, const float
 int splitk_rows_per_part();
 
 // wgrad.hip
-void wgrad_launch(const WgradParams& p, int bm, int bn, hipStream_t st);
+// x3: fp32-accurate 3-term bf16 split on the bf16 MFMA; otherwise the exact fp32-input MFMA
+void wgrad_launch(const WgradParams& p, int bm, int bn, bool x3, hipStream_t st);
 void slab_sum_launch(const float* slab, int S, long long n, float* dst, bool accumulate, hipStream_t st);
 void slab_sum_strided_launch(const float* slab, int S, long long n_src, int src_cols, int dst_cols, float* dst,
                              bool accumulate, hipStream_t st);

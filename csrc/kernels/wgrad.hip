@@ -166,6 +166,212 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(WgradParams p) {
     }
 }
 
+// ---------------------------------------------------------------------------------------------
+// fp32-accurate weight gradient on the bf16 MFMA (v_mfma_f32_32x32x16_bf16): both operands are
+// split into three bf16 terms and the six products of order >= 2^-16 are accumulated (see
+// conv_x3.hip for the error analysis). The MFMA needs 8 consecutive reduction (m) indices per
+// lane, so the tiles are transposed on their way into LDS: a thread gathers RPT consecutive m
+// rows x 4 columns (float4 per row, coalesced along the channels), splits them and writes, per
+// column and plane, its RPT m-values as one 8- or 4-byte LDS store into a [col][m] image (80-B
+// row pitch). Lanes of a store group differ in m first, so the stores are conflict free; the
+// fragment reads are the conflict-free ds_read_b128 pattern of conv_x3.hip.
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4_t __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+constexpr int XLD = WBK + 8;  // bf16 per LDS row
+
+template <int RPT>
+__device__ __forceinline__ void split_store_cols(const float4 (&v)[RPT], __bf16* dst, int plane) {
+  // v[r] = row m+r, 4 columns; dst -> [col 0][m] of this thread's 4 columns
+  const float* f = reinterpret_cast<const float*>(v);
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    __bf16 h0[RPT], h1[RPT], h2[RPT];
+#pragma unroll
+    for (int r = 0; r < RPT; ++r) {
+      const float x = f[4 * r + c];
+      const __bf16 a = (__bf16)x;
+      const float r1 = x - (float)a;
+      const __bf16 b = (__bf16)r1;
+      h0[r] = a;
+      h1[r] = b;
+      h2[r] = (__bf16)(r1 - (float)b);
+    }
+    __bf16* d = dst + c * XLD;
+    if constexpr (RPT == 4) {
+      *reinterpret_cast<bf16x4_t*>(d) = bf16x4_t{h0[0], h0[1], h0[2], h0[3]};
+      *reinterpret_cast<bf16x4_t*>(d + plane) = bf16x4_t{h1[0], h1[1], h1[2], h1[3]};
+      *reinterpret_cast<bf16x4_t*>(d + 2 * plane) = bf16x4_t{h2[0], h2[1], h2[2], h2[3]};
+    } else {
+      *reinterpret_cast<bf16x2_t*>(d) = bf16x2_t{h0[0], h0[1]};
+      *reinterpret_cast<bf16x2_t*>(d + plane) = bf16x2_t{h1[0], h1[1]};
+      *reinterpret_cast<bf16x2_t*>(d + 2 * plane) = bf16x2_t{h2[0], h2[1]};
+    }
+  }
+}
+
+template <int BM, int BN, bool FAST>
+__global__ __launch_bounds__(256, 2) void wgrad_x3_kernel(WgradParams p) {
+  constexpr int TM = BM / 64, TN = BN / 64;
+  constexpr int PA = BM * XLD, PB = BN * XLD;
+  constexpr int RPT_A = BM / 32, RPT_B = BN / 32;  // m rows per thread (4 for 128-wide, 2 for 64)
+  constexpr int MQ_A = WBK / RPT_A, MQ_B = WBK / RPT_B;  // m groups per tile (8 or 16)
+  __shared__ __attribute__((aligned(16))) __bf16 smem[3 * (PA + PB)];
+  __bf16* As = smem;
+  __bf16* Bs = smem + 3 * PA;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid >> 1, wn = wid & 1;
+
+  const int ntn = (p.Kdim + BN - 1) / BN;
+  const int ntm = (p.Cout + BM - 1) / BM;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int tile = bid % (ntm * ntn);
+  const int split = bid / (ntm * ntn);
+  const int tm_idx = tile / ntn, tn_idx = tile % ntn;
+  const int co0 = tm_idx * BM, r0 = tn_idx * BN;
+  const int mt_total = (p.M + WBK - 1) / WBK;
+  const int kt_begin = (int)(((long long)split * mt_total) / p.splits);
+  const int kt_end = (int)(((long long)(split + 1) * mt_total) / p.splits);
+  const int PQ = p.P * p.Q;
+
+  // A (dY^T): thread -> m group (fastest) and 4-column group
+  const int a_mq = tid % MQ_A, a_cg = tid / MQ_A;
+  const int co = co0 + a_cg * 4;
+  // B (Xcol): same shape over the k columns
+  const int b_mq = tid % MQ_B, b_cg = tid / MQ_B;
+  const int kcol = r0 + b_cg * 4;
+  int b_kh = 0, b_kw = 0, b_c = 0;
+  const bool b_kok = kcol < p.Kdim;
+  if (FAST && b_kok) {
+    const int tap = fdiv(kcol, p.fd_C);
+    b_c = kcol - tap * p.C;
+    b_kh = fdiv(tap, p.fd_KW);
+    b_kw = tap - b_kh * p.KW;
+  }
+
+  float4 ra[RPT_A], rb[RPT_B];
+  auto load_tile = [&](int kt) {
+    const int mb = kt * WBK;
+#pragma unroll
+    for (int i = 0; i < RPT_A; ++i) {
+      const int m = mb + a_mq * RPT_A + i;
+      const bool mok = m < p.M;
+      if (FAST) {
+        ra[i] = (mok && co < p.Cout) ? ld4(p.dy + (long long)m * p.Cout + co) : f4zero();
+      } else {
+        float e[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) e[j] = (mok && co + j < p.Cout) ? p.dy[(long long)m * p.Cout + co + j] : 0.f;
+        ra[i] = make_float4(e[0], e[1], e[2], e[3]);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < RPT_B; ++i) {
+      const int m = mb + b_mq * RPT_B + i;
+      const bool mok = m < p.M;
+      const int mm = mok ? m : 0;
+      const int n = fdiv(mm, p.fd_PQ);
+      const int rem = mm - n * PQ;
+      const int pp = fdiv(rem, p.fd_Q), qq = rem - pp * p.Q;
+      const int ih0 = pp * p.stride - p.pad, iw0 = qq * p.stride - p.pad;
+      const float* xb = p.x + (long long)n * p.H * p.W * p.C;
+      if (FAST) {
+        const int ih = ih0 + b_kh, iw = iw0 + b_kw;
+        const bool ok = mok && b_kok && (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W;
+        rb[i] = ok ? ld4(xb + ((long long)ih * p.W + iw) * p.C + b_c) : f4zero();
+      } else {
+        float e[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int k = kcol + j;
+          float v = 0.f;
+          if (mok && k < p.Kdim) {
+            const int tap = fdiv(k, p.fd_C);
+            const int c = k - tap * p.C;
+            const int kh = fdiv(tap, p.fd_KW), kw = tap - kh * p.KW;
+            const int ih = ih0 + kh, iw = iw0 + kw;
+            if ((unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W)
+              v = xb[((long long)ih * p.W + iw) * p.C + c];
+          }
+          e[j] = v;
+        }
+        rb[i] = make_float4(e[0], e[1], e[2], e[3]);
+      }
+    }
+  };
+  auto store_tile = [&]() {
+    split_store_cols<RPT_A>(ra, As + (a_cg * 4) * XLD + a_mq * RPT_A, PA);
+    split_store_cols<RPT_B>(rb, Bs + (b_cg * 4) * XLD + b_mq * RPT_B, PB);
+  };
+
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int a = 0; a < TM; ++a)
+#pragma unroll
+    for (int b = 0; b < TN; ++b)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
+
+  const int l32 = lane & 31, hh = lane >> 5;
+  const int koff = hh * 8;
+  if (kt_begin < kt_end) {
+    load_tile(kt_begin);
+    store_tile();
+    __syncthreads();
+    for (int kt = kt_begin; kt < kt_end; ++kt) {
+      const bool more = kt + 1 < kt_end;
+      if (more) load_tile(kt + 1);
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        bf16x8_t af[TM][3], bf[TN][3];
+#pragma unroll
+        for (int a = 0; a < TM; ++a) {
+          const __bf16* src = As + (wm * (BM / 2) + a * 32 + l32) * XLD + s * 16 + koff;
+#pragma unroll
+          for (int q = 0; q < 3; ++q) af[a][q] = *reinterpret_cast<const bf16x8_t*>(src + q * PA);
+        }
+#pragma unroll
+        for (int b = 0; b < TN; ++b) {
+          const __bf16* src = Bs + (wn * (BN / 2) + b * 32 + l32) * XLD + s * 16 + koff;
+#pragma unroll
+          for (int q = 0; q < 3; ++q) bf[b][q] = *reinterpret_cast<const bf16x8_t*>(src + q * PB);
+        }
+#pragma unroll
+        for (int a = 0; a < TM; ++a)
+#pragma unroll
+          for (int b = 0; b < TN; ++b) {
+            f32x16 c = acc[a][b];
+            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[a][2], bf[b][0], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[a][1], bf[b][1], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[a][0], bf[b][2], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[a][1], bf[b][0], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[a][0], bf[b][1], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[a][0], bf[b][0], c, 0, 0, 0);
+            acc[a][b] = c;
+          }
+      }
+      __syncthreads();
+      if (more) {
+        store_tile();
+        __syncthreads();
+      }
+    }
+  }
+
+  float* out = p.out + (long long)split * p.Cout * p.Kdim;
+#pragma unroll
+  for (int a = 0; a < TM; ++a)
+#pragma unroll
+    for (int b = 0; b < TN; ++b) {
+      const int k = r0 + wn * (BN / 2) + b * 32 + l32;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int c = co0 + wm * (BM / 2) + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
+        if (c < p.Cout && k < p.Kdim) out[(long long)c * p.Kdim + k] = acc[a][b][r];
+      }
+    }
+}
+
 // dst[r][c] = (accumulate ? dst : 0) + sum_z slab[z][r][c]  over rows x src_cols, keeping the first
 // dst_cols of each row (dst_cols < src_cols strips channel padding). Block = CB column slots x SL
 // split lanes; the SL partial sums meet in LDS, so short slabs with many splits still spread over
@@ -206,20 +412,25 @@ __global__ __launch_bounds__(256) void slab_sum_kernel(const float* __restrict__
 }  // namespace
 
 template <int BM, int BN>
-void wgrad_launch_t(const WgradParams& p, hipStream_t st) {
+void wgrad_launch_t(const WgradParams& p, bool x3, hipStream_t st) {
   const int ntn = (p.Kdim + BN - 1) / BN;
   const int ntm = (p.Cout + BM - 1) / BM;
   const bool fast = (p.C % 4) == 0 && (p.Cout % 4) == 0;
   dim3 grid(ntm * ntn * p.splits);
-  if (fast) hipLaunchKernelGGL((wgrad_kernel<BM, BN, true>), grid, dim3(256), 0, st, p);
-  else hipLaunchKernelGGL((wgrad_kernel<BM, BN, false>), grid, dim3(256), 0, st, p);
+  if (x3) {
+    if (fast) hipLaunchKernelGGL((wgrad_x3_kernel<BM, BN, true>), grid, dim3(256), 0, st, p);
+    else hipLaunchKernelGGL((wgrad_x3_kernel<BM, BN, false>), grid, dim3(256), 0, st, p);
+  } else {
+    if (fast) hipLaunchKernelGGL((wgrad_kernel<BM, BN, true>), grid, dim3(256), 0, st, p);
+    else hipLaunchKernelGGL((wgrad_kernel<BM, BN, false>), grid, dim3(256), 0, st, p);
+  }
 }
 
-void wgrad_launch(const WgradParams& p, int bm, int bn, hipStream_t st) {
-  if (bm == 128 && bn == 128) wgrad_launch_t<128, 128>(p, st);
-  else if (bm == 128) wgrad_launch_t<128, 64>(p, st);
-  else if (bn == 128) wgrad_launch_t<64, 128>(p, st);
-  else wgrad_launch_t<64, 64>(p, st);
+void wgrad_launch(const WgradParams& p, int bm, int bn, bool x3, hipStream_t st) {
+  if (bm == 128 && bn == 128) wgrad_launch_t<128, 128>(p, x3, st);
+  else if (bm == 128) wgrad_launch_t<128, 64>(p, x3, st);
+  else if (bn == 128) wgrad_launch_t<64, 128>(p, x3, st);
+  else wgrad_launch_t<64, 64>(p, x3, st);
 }
 
 void slab_sum_launch(const float* slab, int S, long long n, float* dst, bool accumulate, hipStream_t st) {

@@ -80,7 +80,10 @@ int conv_blocks_per_cu(int bm, int bn) {
   return std::max(1, std::min(4, (160 * 1024) / (2 * (bm + bn) * 36 * 4)));
 }
 double conv_mfma_rate() { return conv_gemm_mode() == 1 ? 250.0e12 : 120.0e12; }
-int wgrad_blocks_per_cu(int bm, int bn) { return std::max(1, std::min(4, (160 * 1024) / (2 * 32 * (bm + bn + 8) * 4))); }
+int wgrad_blocks_per_cu(int bm, int bn) {
+  if (conv_gemm_mode() == 1) return (bm + bn) >= 256 ? 2 : (bm + bn) >= 192 ? 3 : 5;
+  return std::max(1, std::min(4, (160 * 1024) / (2 * 32 * (bm + bn + 8) * 4)));
+}
 
 // Split-K factor that best fills whole waves of resident workgroups: a grid just over one wave
 // (e.g. 540 blocks on 512 slots) costs almost two waves of time, so quantisation dominates.
@@ -136,7 +139,8 @@ WgradPlan plan_wgrad(int Cout, int Kdim, long long M) {
   const long long tiles = (long long)((Cout + w.bm - 1) / w.bm) * ((Kdim + w.bn - 1) / w.bn);
   const int mt = (int)std::min<long long>((M + 31) / 32, 1 << 30);
   const int slots = wgrad_blocks_per_cu(w.bm, w.bn) * num_cus();
-  w.splits = std::min(1024, choose_splits(tiles, mt, slots, 4, 2.0 * M * Cout * Kdim, 4.0 * Cout * Kdim));
+  w.splits = std::min(1024, choose_splits(tiles, mt, slots, 4, 2.0 * M * Cout * Kdim, 4.0 * Cout * Kdim,
+                                          conv_mfma_rate()));
   return w;
 }
 
@@ -356,11 +360,11 @@ at::Tensor conv2d_wgrad_keep(const at::Tensor& dy_, const at::Tensor& x_, std::v
   set_divs(p);
   if (p.splits == 1 && !accumulate && Ckeep == C) {
     p.out = dw.data_ptr<float>();
-    wgrad_launch(p, wp.bm, wp.bn, st);
+    wgrad_launch(p, wp.bm, wp.bn, conv_gemm_mode() == 1, st);
   } else {
     at::Tensor slab = at::empty({p.splits, Co, Kdim}, opts);
     p.out = slab.data_ptr<float>();
-    wgrad_launch(p, wp.bm, wp.bn, st);
+    wgrad_launch(p, wp.bm, wp.bn, conv_gemm_mode() == 1, st);
     slab_sum_strided_launch(slab.data_ptr<float>(), p.splits, (long long)Co * Kdim, C, Ckeep, dw.data_ptr<float>(),
                             accumulate, st);
   }
@@ -563,11 +567,11 @@ std::vector<at::Tensor> linear_bwd(const at::Tensor& gy_, const at::Tensor& x_, 
   set_divs(p);
   if (p.splits == 1) {
     p.out = dw.data_ptr<float>();
-    wgrad_launch(p, wp.bm, wp.bn, st);
+    wgrad_launch(p, wp.bm, wp.bn, conv_gemm_mode() == 1, st);
   } else {
     at::Tensor slab = at::empty({p.splits, O, I}, x.options());
     p.out = slab.data_ptr<float>();
-    wgrad_launch(p, wp.bm, wp.bn, st);
+    wgrad_launch(p, wp.bm, wp.bn, conv_gemm_mode() == 1, st);
     slab_sum_launch(slab.data_ptr<float>(), p.splits, (long long)O * I, dw.data_ptr<float>(), false, st);
   }
   at::Tensor db;
