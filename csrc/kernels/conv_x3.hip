@@ -23,26 +23,24 @@
 #include "common.h"
 #include "kernels.h"
 #include "conv_epilogue.h"
+#include "x3_common.h"
 
 namespace cdp {
 
 namespace {
 
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-
 constexpr int BK = 32;
 constexpr int LDH = BK + 8;  // bf16 per LDS row
 
-__device__ __forceinline__ void split3(const float (&v)[8], bf16x8& s0, bf16x8& s1, bf16x8& s2) {
+// Split 8 consecutive-k fp32 values into three bf16x8 planes (as 4 packed pairs each).
+__device__ __forceinline__ void split8(const float (&v)[8], u32x4& s0, u32x4& s1, u32x4& s2) {
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const __bf16 a = (__bf16)v[j];
-    const float r = v[j] - (float)a;
-    const __bf16 b = (__bf16)r;
-    const float r2 = r - (float)b;
+  for (int j = 0; j < 4; ++j) {
+    unsigned a, b, c;
+    split_pair(v[2 * j], v[2 * j + 1], a, b, c);
     s0[j] = a;
     s1[j] = b;
-    s2[j] = (__bf16)r2;
+    s2[j] = c;
   }
 }
 
@@ -74,48 +72,62 @@ __global__ __launch_bounds__(256, 2) void conv_x3_kernel(ConvGemmParams p) {
   const int kt_begin = (int)(((long long)split * p.ktiles) / p.splits);
   const int kt_end = (int)(((long long)(split + 1) * p.ktiles) / p.splits);
   const int PQ = p.P * p.Q;
+  const int HWC = p.H * p.W * p.C;
 
   const int kq = (tid & 3) * 8;  // this thread's 8 consecutive k within the tile
   const int rrow = tid >> 2;     // + 64 i
 
-  const float* a_base[A_LD];
-  int a_h[A_LD], a_w[A_LD];
-  bool a_ok[A_LD];
+  // buffers (host guarantees < 2 GiB each): out-of-range offsets read as zero
+  const __amdgpu_buffer_rsrc_t xr = make_rsrc(p.x, (unsigned)p.N * (unsigned)HWC * 4u);
+  const __amdgpu_buffer_rsrc_t wr = make_rsrc(p.w, (unsigned)p.Nout * (unsigned)p.Kdim * 4u);
+
+  // per A row: spatial anchor and element offset of (n, anchor, kq)
+  int a_h[A_LD], a_w[A_LD], a_n[A_LD], a_off[A_LD];
 #pragma unroll
   for (int i = 0; i < A_LD; ++i) {
     const int m = m0 + rrow + 64 * i;
-    a_ok[i] = m < p.M;
-    const int mm = a_ok[i] ? m : 0;
+    const bool ok = m < p.M;
+    const int mm = ok ? m : 0;
     const int n = fdiv(mm, p.fd_PQ);
-    const int rem = mm - n * PQ;
+    const int rem = mm - mul24(n, PQ);
     const int pp = fdiv(rem, p.fd_Q);
-    const int qq = rem - pp * p.Q;
-    a_base[i] = p.x + (long long)n * p.H * p.W * p.C;
+    const int qq = rem - mul24(pp, p.Q);
     if (DGRAD) {
-      a_h[i] = pp + p.pad;
+      a_h[i] = pp + p.pad;  // oh*stride = ih + pad - kh
       a_w[i] = qq + p.pad;
     } else {
-      a_h[i] = pp * p.stride - p.pad;
-      a_w[i] = qq * p.stride - p.pad;
+      a_h[i] = mul24(pp, p.stride) - p.pad;
+      a_w[i] = mul24(qq, p.stride) - p.pad;
     }
+    if (!ok) a_h[i] = -(1 << 22);  // fails every bounds test below
+    a_n[i] = mul24(n, HWC);
+    a_off[i] = a_n[i] + mul24(mul24(a_h[i], p.W) + a_w[i], p.C) + kq;
+  }
+  // per B row: byte offset of (row, kq); rows past Nout read zeros
+  unsigned b_off[B_LD];
+#pragma unroll
+  for (int i = 0; i < B_LD; ++i) {
+    const int n = n0 + rrow + 64 * i;
+    b_off[i] = n < p.Nout ? (unsigned)(mul24(n, p.Kdim) + kq) * 4u : kOOB;
   }
 
-  auto pix_ok = [&](int i, int kh, int kw, int& ih, int& iw) -> bool {
+  // byte offset of A row i at filter tap (kh, kw), channel offset c (relative to kq); OOB if padded
+  auto a_voff = [&](int i, int kh, int kw, int c) -> unsigned {
     if (DGRAD) {
       int oh = a_h[i] - kh, ow = a_w[i] - kw;
-      if (oh < 0 || ow < 0) return false;
-      if (p.stride != 1) {
-        if ((oh % p.stride) | (ow % p.stride)) return false;
-        oh /= p.stride;
-        ow /= p.stride;
+      if (p.stride == 1) {
+        const bool ok = (unsigned)oh < (unsigned)p.H && (unsigned)ow < (unsigned)p.W;
+        return ok ? (unsigned)(a_off[i] - mul24(mul24(kh, p.W) + kw, p.C) + c) * 4u : kOOB;
       }
-      ih = oh;
-      iw = ow;
-      return oh < p.H && ow < p.W;
+      bool ok = oh >= 0 && ow >= 0 && ((oh | ow) & (p.stride - 1)) == 0;  // stride is 2 (power of two)
+      oh >>= 1;
+      ow >>= 1;
+      ok = ok && oh < p.H && ow < p.W;
+      return ok ? (unsigned)(a_n[i] + mul24(mul24(oh, p.W) + ow, p.C) + kq + c) * 4u : kOOB;
     } else {
-      ih = a_h[i] + kh;
-      iw = a_w[i] + kw;
-      return (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W;
+      const int ih = a_h[i] + kh, iw = a_w[i] + kw;
+      const bool ok = (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W;
+      return ok ? (unsigned)(a_off[i] + mul24(mul24(kh, p.W) + kw, p.C) + c) * 4u : kOOB;
     }
   };
 
@@ -129,62 +141,62 @@ __global__ __launch_bounds__(256, 2) void conv_x3_kernel(ConvGemmParams p) {
   };
 
   auto load_tile = [&](int kt) {
-    const int r0 = kt * BK + kq;
+    const int r0 = kt * BK;
     if (MODE == 0) {
-      const int tap = fdiv(kt * BK, p.fd_C);
+      // the whole K-tile lies in one filter tap (C % 32 == 0): tap decode is wave-uniform
+      const int tap = fdiv(r0, p.fd_C);
       const int c0 = r0 - tap * p.C;
       const int kh = fdiv(tap, p.fd_KW), kw = tap - kh * p.KW;
 #pragma unroll
       for (int i = 0; i < A_LD; ++i) {
-        int ih, iw;
-        const bool ok = a_ok[i] && pix_ok(i, kh, kw, ih, iw);
-        const float* src = a_base[i] + ((long long)ih * p.W + iw) * p.C + c0;
-        put4(va[i], 0, ok ? ld4(src) : f4zero());
-        put4(va[i], 4, ok ? ld4(src + 4) : f4zero());
+        const unsigned o = a_voff(i, kh, kw, c0);
+        put4(va[i], 0, bload4(xr, o));
+        put4(va[i], 4, bload4(xr, o + 16u));
       }
     } else if (MODE == 1) {
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
-        const int r = r0 + 4 * h;
-        const bool rok = r < p.Kdim;
-        const int tap = fdiv(r, p.fd_C);
-        const int c = r - tap * p.C;
-        const int kh = fdiv(tap, p.fd_KW), kw = tap - kh * p.KW;
-#pragma unroll
-        for (int i = 0; i < A_LD; ++i) {
-          int ih, iw;
-          const bool ok = rok && a_ok[i] && pix_ok(i, kh, kw, ih, iw);
-          put4(va[i], 4 * h, ok ? ld4(a_base[i] + ((long long)ih * p.W + iw) * p.C + c) : f4zero());
-        }
-      }
-    } else {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int r = r0 + j;
+        const int r = r0 + kq + 4 * h;
         const bool rok = r < p.Kdim;
         const int tap = fdiv(rok ? r : 0, p.fd_C);
         const int c = r - tap * p.C;
         const int kh = fdiv(tap, p.fd_KW), kw = tap - kh * p.KW;
 #pragma unroll
         for (int i = 0; i < A_LD; ++i) {
-          int ih, iw;
-          const bool ok = rok && a_ok[i] && pix_ok(i, kh, kw, ih, iw);
-          va[i][j] = ok ? a_base[i][((long long)ih * p.W + iw) * p.C + c] : 0.f;
+          const unsigned o = rok ? a_voff(i, kh, kw, c - kq) : kOOB;
+          put4(va[i], 4 * h, bload4(xr, o));
+        }
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int r = r0 + kq + j;
+        const bool rok = r < p.Kdim;
+        const int tap = fdiv(rok ? r : 0, p.fd_C);
+        const int c = r - tap * p.C;
+        const int kh = fdiv(tap, p.fd_KW), kw = tap - kh * p.KW;
+#pragma unroll
+        for (int i = 0; i < A_LD; ++i) {
+          const unsigned o = rok ? a_voff(i, kh, kw, c - kq) : kOOB;
+          va[i][j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xr, (int)o, 0, 0));
         }
       }
     }
 #pragma unroll
     for (int i = 0; i < B_LD; ++i) {
-      const int n = n0 + rrow + 64 * i;
-      const float* src = p.w + (long long)n * p.Kdim + r0;
-      if (MODE != 2) {
-        const bool ok0 = n < p.Nout && r0 < p.Kdim;
-        const bool ok1 = n < p.Nout && r0 + 4 < p.Kdim;
-        put4(vb[i], 0, ok0 ? ld4(src) : f4zero());
-        put4(vb[i], 4, ok1 ? ld4(src + 4) : f4zero());
+      const unsigned o = b_off[i] + (unsigned)r0 * 4u;
+      if (MODE == 0) {
+        put4(vb[i], 0, bload4(wr, o));
+        put4(vb[i], 4, bload4(wr, o + 16u));
+      } else if (MODE == 1) {
+        // Kdim % 4 == 0: a float4 is either inside the row or wholly past its end
+        put4(vb[i], 0, bload4(wr, r0 + kq < p.Kdim ? o : kOOB));
+        put4(vb[i], 4, bload4(wr, r0 + kq + 4 < p.Kdim ? o + 16u : kOOB));
       } else {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) vb[i][j] = (n < p.Nout && r0 + j < p.Kdim) ? src[j] : 0.f;
+        for (int j = 0; j < 8; ++j)
+          vb[i][j] = __uint_as_float(
+              __builtin_amdgcn_raw_buffer_load_b32(wr, (int)(r0 + kq + j < p.Kdim ? o + 4u * j : kOOB), 0, 0));
       }
     }
   };
@@ -192,21 +204,21 @@ __global__ __launch_bounds__(256, 2) void conv_x3_kernel(ConvGemmParams p) {
   auto store_tile = [&]() {
 #pragma unroll
     for (int i = 0; i < A_LD; ++i) {
-      bf16x8 s0, s1, s2;
-      split3(va[i], s0, s1, s2);
+      u32x4 s0, s1, s2;
+      split8(va[i], s0, s1, s2);
       __bf16* d = As + (rrow + 64 * i) * LDH + kq;
-      *reinterpret_cast<bf16x8*>(d) = s0;
-      *reinterpret_cast<bf16x8*>(d + PA) = s1;
-      *reinterpret_cast<bf16x8*>(d + 2 * PA) = s2;
+      *reinterpret_cast<u32x4*>(d) = s0;
+      *reinterpret_cast<u32x4*>(d + PA) = s1;
+      *reinterpret_cast<u32x4*>(d + 2 * PA) = s2;
     }
 #pragma unroll
     for (int i = 0; i < B_LD; ++i) {
-      bf16x8 s0, s1, s2;
-      split3(vb[i], s0, s1, s2);
+      u32x4 s0, s1, s2;
+      split8(vb[i], s0, s1, s2);
       __bf16* d = Bs + (rrow + 64 * i) * LDH + kq;
-      *reinterpret_cast<bf16x8*>(d) = s0;
-      *reinterpret_cast<bf16x8*>(d + PB) = s1;
-      *reinterpret_cast<bf16x8*>(d + 2 * PB) = s2;
+      *reinterpret_cast<u32x4*>(d) = s0;
+      *reinterpret_cast<u32x4*>(d + PB) = s1;
+      *reinterpret_cast<u32x4*>(d + 2 * PB) = s2;
     }
   };
 

@@ -13,6 +13,7 @@
 // conflict-free ds_read_b32.
 #include "common.h"
 #include "kernels.h"
+#include "x3_common.h"
 
 namespace cdp {
 namespace {
@@ -175,37 +176,30 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(WgradParams p) {
 // column and plane, its RPT m-values as one 8- or 4-byte LDS store into a [col][m] image (80-B
 // row pitch). Lanes of a store group differ in m first, so the stores are conflict free; the
 // fragment reads are the conflict-free ds_read_b128 pattern of conv_x3.hip.
-typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
-typedef __bf16 bf16x4_t __attribute__((ext_vector_type(4)));
-typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
 constexpr int XLD = WBK + 8;  // bf16 per LDS row
 
+// v[r] = row m+r of this thread's 4 columns; write, per column and plane, the RPT m-values
+// (packed bf16 pairs) into the [col][m] image at dst.
 template <int RPT>
 __device__ __forceinline__ void split_store_cols(const float4 (&v)[RPT], __bf16* dst, int plane) {
-  // v[r] = row m+r, 4 columns; dst -> [col 0][m] of this thread's 4 columns
-  const float* f = reinterpret_cast<const float*>(v);
+  // (component access by constant index only: a pointer walk over `v` makes the compiler
+  // promote the register array to LDS scratch)
+  auto comp = [](const float4& q, int c) { return c == 0 ? q.x : c == 1 ? q.y : c == 2 ? q.z : q.w; };
 #pragma unroll
   for (int c = 0; c < 4; ++c) {
-    __bf16 h0[RPT], h1[RPT], h2[RPT];
+    unsigned h0[RPT / 2], h1[RPT / 2], h2[RPT / 2];
 #pragma unroll
-    for (int r = 0; r < RPT; ++r) {
-      const float x = f[4 * r + c];
-      const __bf16 a = (__bf16)x;
-      const float r1 = x - (float)a;
-      const __bf16 b = (__bf16)r1;
-      h0[r] = a;
-      h1[r] = b;
-      h2[r] = (__bf16)(r1 - (float)b);
-    }
+    for (int r = 0; r < RPT / 2; ++r)
+      split_pair(comp(v[2 * r], c), comp(v[2 * r + 1], c), h0[r], h1[r], h2[r]);
     __bf16* d = dst + c * XLD;
     if constexpr (RPT == 4) {
-      *reinterpret_cast<bf16x4_t*>(d) = bf16x4_t{h0[0], h0[1], h0[2], h0[3]};
-      *reinterpret_cast<bf16x4_t*>(d + plane) = bf16x4_t{h1[0], h1[1], h1[2], h1[3]};
-      *reinterpret_cast<bf16x4_t*>(d + 2 * plane) = bf16x4_t{h2[0], h2[1], h2[2], h2[3]};
+      *reinterpret_cast<uint2*>(d) = make_uint2(h0[0], h0[1]);
+      *reinterpret_cast<uint2*>(d + plane) = make_uint2(h1[0], h1[1]);
+      *reinterpret_cast<uint2*>(d + 2 * plane) = make_uint2(h2[0], h2[1]);
     } else {
-      *reinterpret_cast<bf16x2_t*>(d) = bf16x2_t{h0[0], h0[1]};
-      *reinterpret_cast<bf16x2_t*>(d + plane) = bf16x2_t{h1[0], h1[1]};
-      *reinterpret_cast<bf16x2_t*>(d + 2 * plane) = bf16x2_t{h2[0], h2[1]};
+      *reinterpret_cast<unsigned*>(d) = h0[0];
+      *reinterpret_cast<unsigned*>(d + plane) = h1[0];
+      *reinterpret_cast<unsigned*>(d + 2 * plane) = h2[0];
     }
   }
 }
@@ -233,6 +227,7 @@ __global__ __launch_bounds__(256, 2) void wgrad_x3_kernel(WgradParams p) {
   const int kt_begin = (int)(((long long)split * mt_total) / p.splits);
   const int kt_end = (int)(((long long)(split + 1) * mt_total) / p.splits);
   const int PQ = p.P * p.Q;
+  const int HWC = p.H * p.W * p.C;
 
   // A (dY^T): thread -> m group (fastest) and 4-column group
   const int a_mq = tid % MQ_A, a_cg = tid / MQ_A;
@@ -248,22 +243,43 @@ __global__ __launch_bounds__(256, 2) void wgrad_x3_kernel(WgradParams p) {
     b_kh = fdiv(tap, p.fd_KW);
     b_kw = tap - b_kh * p.KW;
   }
+  // FAST path buffers (host keeps both < 2 GiB): dY rows are addressed relative to the tile's
+  // first row through a per-tile descriptor, so these offsets are loop invariant
+  unsigned a_off[RPT_A];
+#pragma unroll
+  for (int i = 0; i < RPT_A; ++i)
+    a_off[i] = co < p.Cout ? (unsigned)(mul24(a_mq * RPT_A + i, p.Cout) + co) * 4u : kOOB;
+  const __amdgpu_buffer_rsrc_t xr = make_rsrc(p.x, (unsigned)p.N * (unsigned)HWC * 4u);
 
   float4 ra[RPT_A], rb[RPT_B];
   auto load_tile = [&](int kt) {
     const int mb = kt * WBK;
+    if (FAST) {
+      const __amdgpu_buffer_rsrc_t dr =
+          make_rsrc(p.dy + (long long)mb * p.Cout, (unsigned)(p.M - mb) * (unsigned)p.Cout * 4u);
+#pragma unroll
+      for (int i = 0; i < RPT_A; ++i) ra[i] = bload4(dr, a_off[i]);
+#pragma unroll
+      for (int i = 0; i < RPT_B; ++i) {
+        const int m = mb + b_mq * RPT_B + i;
+        const int mm = m < p.M ? m : 0;
+        const int n = fdiv(mm, p.fd_PQ);
+        const int rem = mm - mul24(n, PQ);
+        const int pp = fdiv(rem, p.fd_Q), qq = rem - mul24(pp, p.Q);
+        const int ih = mul24(pp, p.stride) - p.pad + b_kh, iw = mul24(qq, p.stride) - p.pad + b_kw;
+        const bool ok = m < p.M && b_kok && (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W;
+        rb[i] = bload4(xr, ok ? (unsigned)(mul24(n, HWC) + mul24(mul24(ih, p.W) + iw, p.C) + b_c) * 4u : kOOB);
+      }
+      return;
+    }
 #pragma unroll
     for (int i = 0; i < RPT_A; ++i) {
       const int m = mb + a_mq * RPT_A + i;
       const bool mok = m < p.M;
-      if (FAST) {
-        ra[i] = (mok && co < p.Cout) ? ld4(p.dy + (long long)m * p.Cout + co) : f4zero();
-      } else {
-        float e[4];
+      float e[4];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) e[j] = (mok && co + j < p.Cout) ? p.dy[(long long)m * p.Cout + co + j] : 0.f;
-        ra[i] = make_float4(e[0], e[1], e[2], e[3]);
-      }
+      for (int j = 0; j < 4; ++j) e[j] = (mok && co + j < p.Cout) ? p.dy[(long long)m * p.Cout + co + j] : 0.f;
+      ra[i] = make_float4(e[0], e[1], e[2], e[3]);
     }
 #pragma unroll
     for (int i = 0; i < RPT_B; ++i) {
@@ -275,28 +291,22 @@ __global__ __launch_bounds__(256, 2) void wgrad_x3_kernel(WgradParams p) {
       const int pp = fdiv(rem, p.fd_Q), qq = rem - pp * p.Q;
       const int ih0 = pp * p.stride - p.pad, iw0 = qq * p.stride - p.pad;
       const float* xb = p.x + (long long)n * p.H * p.W * p.C;
-      if (FAST) {
-        const int ih = ih0 + b_kh, iw = iw0 + b_kw;
-        const bool ok = mok && b_kok && (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W;
-        rb[i] = ok ? ld4(xb + ((long long)ih * p.W + iw) * p.C + b_c) : f4zero();
-      } else {
-        float e[4];
+      float e[4];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int k = kcol + j;
-          float v = 0.f;
-          if (mok && k < p.Kdim) {
-            const int tap = fdiv(k, p.fd_C);
-            const int c = k - tap * p.C;
-            const int kh = fdiv(tap, p.fd_KW), kw = tap - kh * p.KW;
-            const int ih = ih0 + kh, iw = iw0 + kw;
-            if ((unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W)
-              v = xb[((long long)ih * p.W + iw) * p.C + c];
-          }
-          e[j] = v;
+      for (int j = 0; j < 4; ++j) {
+        const int k = kcol + j;
+        float v = 0.f;
+        if (mok && k < p.Kdim) {
+          const int tap = fdiv(k, p.fd_C);
+          const int c = k - tap * p.C;
+          const int kh = fdiv(tap, p.fd_KW), kw = tap - kh * p.KW;
+          const int ih = ih0 + kh, iw = iw0 + kw;
+          if ((unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W)
+            v = xb[((long long)ih * p.W + iw) * p.C + c];
         }
-        rb[i] = make_float4(e[0], e[1], e[2], e[3]);
+        e[j] = v;
       }
+      rb[i] = make_float4(e[0], e[1], e[2], e[3]);
     }
   };
   auto store_tile = [&]() {
@@ -323,18 +333,18 @@ __global__ __launch_bounds__(256, 2) void wgrad_x3_kernel(WgradParams p) {
       if (more) load_tile(kt + 1);
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
-        bf16x8_t af[TM][3], bf[TN][3];
+        bf16x8 af[TM][3], bf[TN][3];
 #pragma unroll
         for (int a = 0; a < TM; ++a) {
           const __bf16* src = As + (wm * (BM / 2) + a * 32 + l32) * XLD + s * 16 + koff;
 #pragma unroll
-          for (int q = 0; q < 3; ++q) af[a][q] = *reinterpret_cast<const bf16x8_t*>(src + q * PA);
+          for (int q = 0; q < 3; ++q) af[a][q] = *reinterpret_cast<const bf16x8*>(src + q * PA);
         }
 #pragma unroll
         for (int b = 0; b < TN; ++b) {
           const __bf16* src = Bs + (wn * (BN / 2) + b * 32 + l32) * XLD + s * 16 + koff;
 #pragma unroll
-          for (int q = 0; q < 3; ++q) bf[b][q] = *reinterpret_cast<const bf16x8_t*>(src + q * PB);
+          for (int q = 0; q < 3; ++q) bf[b][q] = *reinterpret_cast<const bf16x8*>(src + q * PB);
         }
 #pragma unroll
         for (int a = 0; a < TM; ++a)

@@ -1,0 +1,52 @@
+// Helpers of the fp32-accurate split-bf16 GEMM kernels (conv_x3.hip, wgrad.hip).
+//
+//   x = h0 + h1 + h2 exactly (barring underflow), h0 = rn_bf16(x), h1 = rn_bf16(x - h0),
+//   h2 = rn_bf16(x - h0 - h1); both subtractions are exact (Sterbenz).
+//
+// Pairs are split together so each step is one packed instruction: v_cvt_pk_bf16_f32 for the
+// rounding, a shift and a mask to widen the two bf16 back to f32, v_pk_add_f32 for the residual:
+// 9 VALU per pair of elements.
+#pragma once
+#include "common.h"
+
+namespace cdp {
+
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2_v __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ unsigned pack_bf16x2(f32x2 v) {
+  return __builtin_bit_cast(unsigned, __builtin_convertvector(v, bf16x2_v));
+}
+
+__device__ __forceinline__ f32x2 widen_bf16x2(unsigned h) {
+  return f32x2{__uint_as_float(h << 16), __uint_as_float(h & 0xffff0000u)};
+}
+
+__device__ __forceinline__ void split_pair(float x, float y, unsigned& h0, unsigned& h1, unsigned& h2) {
+  const f32x2 v{x, y};
+  h0 = pack_bf16x2(v);
+  const f32x2 r1 = v - widen_bf16x2(h0);
+  h1 = pack_bf16x2(r1);
+  const f32x2 r2 = r1 - widen_bf16x2(h1);
+  h2 = pack_bf16x2(r2);
+}
+
+// Raw buffer resource over [base, base + bytes): loads past `bytes` return 0 (hardware range
+// check), which implements the implicit-GEMM zero padding without branches or selects.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, unsigned bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
+}
+
+constexpr unsigned kOOB = 0x80000000u;  // a byte offset past every buffer (host keeps buffers < 2 GiB)
+
+__device__ __forceinline__ float4 bload4(__amdgpu_buffer_rsrc_t r, unsigned off) {
+  const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 0);
+  return make_float4(__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z), __uint_as_float(v.w));
+}
+
+// full-rate 24-bit multiplies (v_mul_u32_u24 / v_mul_i32_i24) for index math; every operand is < 2^23
+__device__ __forceinline__ int mul24(int a, int b) { return __mul24(a, b); }
+
+}  // namespace cdp

@@ -69,8 +69,23 @@ int& conv_gemm_mode() {
   return m;
 }
 
+// The x3 kernels address through 32-bit buffer offsets and 24-bit index multiplies; shapes past
+// those limits (or a strided data-gradient other than stride 2) take the exact fp32 kernels.
+constexpr long long kBuf = 1LL << 31;
+constexpr long long kIdx = 1LL << 23;
+bool x3_ok(const ConvGemmParams& p, bool dgrad) {
+  const long long hwc = (long long)p.H * p.W * p.C;
+  return (long long)p.N * hwc * 4 < kBuf && (long long)p.Nout * p.Kdim * 4 < kBuf && hwc < kIdx &&
+         (long long)p.P * p.Q < kIdx && p.Kdim < kIdx && (!dgrad || p.stride == 1 || p.stride == 2);
+}
+bool x3_ok(const WgradParams& p) {
+  const long long hwc = (long long)p.H * p.W * p.C;
+  return (long long)p.N * hwc * 4 < kBuf && (long long)p.M * p.Cout * 4 < kBuf && hwc < kIdx &&
+         (long long)p.P * p.Q < kIdx;
+}
+
 void conv_launch(const ConvGemmParams& p, int bm, int bn, bool dgrad, hipStream_t st) {
-  if (conv_gemm_mode() == 1) conv_x3_launch(p, bm, bn, dgrad, st);
+  if (conv_gemm_mode() == 1 && x3_ok(p, dgrad)) conv_x3_launch(p, bm, bn, dgrad, st);
   else conv_igemm_launch(p, bm, bn, dgrad, st);
 }
 
@@ -360,11 +375,11 @@ at::Tensor conv2d_wgrad_keep(const at::Tensor& dy_, const at::Tensor& x_, std::v
   set_divs(p);
   if (p.splits == 1 && !accumulate && Ckeep == C) {
     p.out = dw.data_ptr<float>();
-    wgrad_launch(p, wp.bm, wp.bn, conv_gemm_mode() == 1, st);
+    wgrad_launch(p, wp.bm, wp.bn, conv_gemm_mode() == 1 && x3_ok(p), st);
   } else {
     at::Tensor slab = at::empty({p.splits, Co, Kdim}, opts);
     p.out = slab.data_ptr<float>();
-    wgrad_launch(p, wp.bm, wp.bn, conv_gemm_mode() == 1, st);
+    wgrad_launch(p, wp.bm, wp.bn, conv_gemm_mode() == 1 && x3_ok(p), st);
     slab_sum_strided_launch(slab.data_ptr<float>(), p.splits, (long long)Co * Kdim, C, Ckeep, dw.data_ptr<float>(),
                             accumulate, st);
   }
@@ -567,11 +582,11 @@ std::vector<at::Tensor> linear_bwd(const at::Tensor& gy_, const at::Tensor& x_, 
   set_divs(p);
   if (p.splits == 1) {
     p.out = dw.data_ptr<float>();
-    wgrad_launch(p, wp.bm, wp.bn, conv_gemm_mode() == 1, st);
+    wgrad_launch(p, wp.bm, wp.bn, conv_gemm_mode() == 1 && x3_ok(p), st);
   } else {
     at::Tensor slab = at::empty({p.splits, O, I}, x.options());
     p.out = slab.data_ptr<float>();
-    wgrad_launch(p, wp.bm, wp.bn, conv_gemm_mode() == 1, st);
+    wgrad_launch(p, wp.bm, wp.bn, conv_gemm_mode() == 1 && x3_ok(p), st);
     slab_sum_launch(slab.data_ptr<float>(), p.splits, (long long)O * I, dw.data_ptr<float>(), false, st);
   }
   at::Tensor db;
