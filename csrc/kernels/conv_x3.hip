@@ -14,12 +14,13 @@
 // MFMAs: 2.67x the MFMA throughput.
 //
 // Same GEMM mapping as conv_igemm.hip (forward / transposed-gather data gradient, MODE 0/1/2
-// gathers, identical epilogue). Pipeline: operands are gathered global -> registers (prefetch
-// of K-tile t+1 overlaps the MFMAs of tile t), split into three bf16 planes with
-// v_cvt_pk_bf16_f32 and stored to a single LDS stage; two barriers per K-tile. 60 KB of LDS for
-// 128x128 keeps two workgroups per CU, so one block's split/store/barrier hides under the other's
-// MFMAs. Each LDS row holds 32 bf16 + 8 pad (80 B pitch): the ds_read_b128 fragment reads of a
-// 16-lane group hit 16 distinct 16-B bank quads (5r mod 16 is a permutation), conflict free.
+// gathers, identical epilogue). Pipeline (one barrier per K-tile): operands are gathered
+// global -> registers through buffer loads whose range check supplies the zero padding; two
+// register sets and two LDS stages let the split + store of tile t+1 (v_cvt_pk_bf16_f32,
+// v_pk_add_f32) interleave with the MFMAs of tile t while tile t+2 is in flight. LDS rows are
+// 64 B with XOR-swizzled 16-B chunks (chunk_pos), conflict free for the ds_write_b128 stores and
+// the ds_read_b128 fragment reads. 96 KB of LDS for 128x128 (one workgroup per CU, the MFMA
+// pipe kept busy by the in-wave interleave), 72 KB for 64x128.
 #include "common.h"
 #include "kernels.h"
 #include "conv_epilogue.h"
@@ -30,7 +31,12 @@ namespace cdp {
 namespace {
 
 constexpr int BK = 32;
-constexpr int LDH = BK + 8;  // bf16 per LDS row
+constexpr int LDH = BK;  // bf16 per LDS row (64 B, 16-B chunks XOR-swizzled, see chunk_pos)
+
+// 16-B chunk c (0..3) of LDS row r lives at chunk position c ^ ((r >> 2) & 3): the 8-lane groups
+// of the ds_write_b128 stores (two rows x four chunks) and the 16-lane groups of the ds_read_b128
+// fragment reads (16 rows, one chunk) both hit distinct banks.
+__device__ __forceinline__ int chunk_pos(int r, int c) { return c ^ ((r >> 2) & 3); }
 
 // Split 8 consecutive-k fp32 values into three bf16x8 planes (as 4 packed pairs each).
 __device__ __forceinline__ void split8(const float (&v)[8], u32x4& s0, u32x4& s1, u32x4& s2) {
@@ -51,11 +57,9 @@ __global__ __launch_bounds__(256, 2) void conv_x3_kernel(ConvGemmParams p) {
   constexpr int A_LD = BM / 64;  // A rows per thread (row = tid/4 + 64 i), 8 consecutive k each
   constexpr int B_LD = BN / 64;
   constexpr int PA = BM * LDH, PB = BN * LDH;
-  constexpr int SMEM_BYTES = 3 * (PA + PB) * 2;
-  static_assert(SMEM_BYTES >= 2 * BN * 4, "epilogue scratch");
-  __shared__ __attribute__((aligned(16))) unsigned char smem_raw[SMEM_BYTES];
-  __bf16* As = reinterpret_cast<__bf16*>(smem_raw);  // [3][BM][LDH]
-  __bf16* Bs = As + 3 * PA;                          // [3][BN][LDH]
+  constexpr int STAGE = 3 * (PA + PB);  // bf16 per stage: A planes [3][BM][LDH], B planes [3][BN][LDH]
+  static_assert(2 * STAGE * 2 >= 2 * BN * 4, "epilogue scratch");
+  __shared__ __attribute__((aligned(16))) __bf16 smem[2 * STAGE];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -131,7 +135,7 @@ __global__ __launch_bounds__(256, 2) void conv_x3_kernel(ConvGemmParams p) {
     }
   };
 
-  float va[A_LD][8], vb[B_LD][8];
+  float va0[A_LD][8], vb0[B_LD][8], va1[A_LD][8], vb1[B_LD][8];  // register ping-pong
 
   auto put4 = [](float (&d)[8], int off, float4 v) {
     d[off] = v.x;
@@ -140,7 +144,7 @@ __global__ __launch_bounds__(256, 2) void conv_x3_kernel(ConvGemmParams p) {
     d[off + 3] = v.w;
   };
 
-  auto load_tile = [&](int kt) {
+  auto load_tile = [&](int kt, float (&va)[A_LD][8], float (&vb)[B_LD][8]) {
     const int r0 = kt * BK;
     if (MODE == 0) {
       // the whole K-tile lies in one filter tap (C % 32 == 0): tap decode is wave-uniform
@@ -201,12 +205,13 @@ __global__ __launch_bounds__(256, 2) void conv_x3_kernel(ConvGemmParams p) {
     }
   };
 
-  auto store_tile = [&]() {
+  auto store_tile = [&](const float (&va)[A_LD][8], const float (&vb)[B_LD][8], __bf16* st) {
+    const int cp = chunk_pos(rrow, tid & 3) * 8;  // rrow + 64 i has the same (row >> 2) & 3
 #pragma unroll
     for (int i = 0; i < A_LD; ++i) {
       u32x4 s0, s1, s2;
       split8(va[i], s0, s1, s2);
-      __bf16* d = As + (rrow + 64 * i) * LDH + kq;
+      __bf16* d = st + (rrow + 64 * i) * LDH + cp;
       *reinterpret_cast<u32x4*>(d) = s0;
       *reinterpret_cast<u32x4*>(d + PA) = s1;
       *reinterpret_cast<u32x4*>(d + 2 * PA) = s2;
@@ -215,7 +220,7 @@ __global__ __launch_bounds__(256, 2) void conv_x3_kernel(ConvGemmParams p) {
     for (int i = 0; i < B_LD; ++i) {
       u32x4 s0, s1, s2;
       split8(vb[i], s0, s1, s2);
-      __bf16* d = Bs + (rrow + 64 * i) * LDH + kq;
+      __bf16* d = st + 3 * PA + (rrow + 64 * i) * LDH + cp;
       *reinterpret_cast<u32x4*>(d) = s0;
       *reinterpret_cast<u32x4*>(d + PB) = s1;
       *reinterpret_cast<u32x4*>(d + 2 * PB) = s2;
@@ -231,53 +236,68 @@ __global__ __launch_bounds__(256, 2) void conv_x3_kernel(ConvGemmParams p) {
       for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
 
   const int l32 = lane & 31;
-  const int koff = (lane >> 5) * 8;
+  const int hh = lane >> 5;
 
-  if (kt_begin < kt_end) {
-    load_tile(kt_begin);
-    store_tile();
-    __syncthreads();
-    for (int kt = kt_begin; kt < kt_end; ++kt) {
-      const bool more = kt + 1 < kt_end;
-      if (more) load_tile(kt + 1);
+  // MFMAs over one LDS stage (two 16-k steps of six split products per 32x32 tile)
+  auto compute = [&](const __bf16* st) {
 #pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        bf16x8 af[TM][3], bf[TN][3];
+    for (int s = 0; s < 2; ++s) {
+      bf16x8 af[TM][3], bf[TN][3];
 #pragma unroll
-        for (int a = 0; a < TM; ++a) {
-          const __bf16* src = As + (wm * (BM / 2) + a * 32 + l32) * LDH + s * 16 + koff;
+      for (int a = 0; a < TM; ++a) {
+        const int r = wm * (BM / 2) + a * 32 + l32;
+        const __bf16* src = st + r * LDH + chunk_pos(r, 2 * s + hh) * 8;
 #pragma unroll
-          for (int q = 0; q < 3; ++q) af[a][q] = *reinterpret_cast<const bf16x8*>(src + q * PA);
-        }
+        for (int q = 0; q < 3; ++q) af[a][q] = *reinterpret_cast<const bf16x8*>(src + q * PA);
+      }
+#pragma unroll
+      for (int b = 0; b < TN; ++b) {
+        const int r = wn * (BN / 2) + b * 32 + l32;
+        const __bf16* src = st + 3 * PA + r * LDH + chunk_pos(r, 2 * s + hh) * 8;
+#pragma unroll
+        for (int q = 0; q < 3; ++q) bf[b][q] = *reinterpret_cast<const bf16x8*>(src + q * PB);
+      }
+#pragma unroll
+      for (int a = 0; a < TM; ++a)
 #pragma unroll
         for (int b = 0; b < TN; ++b) {
-          const __bf16* src = Bs + (wn * (BN / 2) + b * 32 + l32) * LDH + s * 16 + koff;
-#pragma unroll
-          for (int q = 0; q < 3; ++q) bf[b][q] = *reinterpret_cast<const bf16x8*>(src + q * PB);
+          f32x16 c = acc[a][b];
+          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[a][2], bf[b][0], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[a][1], bf[b][1], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[a][0], bf[b][2], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[a][1], bf[b][0], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[a][0], bf[b][1], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[a][0], bf[b][0], c, 0, 0, 0);
+          acc[a][b] = c;
         }
-#pragma unroll
-        for (int a = 0; a < TM; ++a)
-#pragma unroll
-          for (int b = 0; b < TN; ++b) {
-            f32x16 c = acc[a][b];
-            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[a][2], bf[b][0], c, 0, 0, 0);
-            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[a][1], bf[b][1], c, 0, 0, 0);
-            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[a][0], bf[b][2], c, 0, 0, 0);
-            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[a][1], bf[b][0], c, 0, 0, 0);
-            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[a][0], bf[b][1], c, 0, 0, 0);
-            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[a][0], bf[b][0], c, 0, 0, 0);
-            acc[a][b] = c;
-          }
-      }
-      __syncthreads();
-      if (more) {
-        store_tile();
-        __syncthreads();
-      }
     }
+  };
+
+  // Software pipeline, one barrier per K-tile: while the MFMAs consume stage t&1, tile t+1
+  // (loaded into registers one iteration earlier) is split into stage (t+1)&1 and tile t+2 is
+  // being fetched into the other register set.
+  if (kt_begin < kt_end) {
+    load_tile(kt_begin, va0, vb0);
+    if (kt_begin + 1 < kt_end) load_tile(kt_begin + 1, va1, vb1);
+    store_tile(va0, vb0, smem);
+    __syncthreads();
+    int kt = kt_begin;
+    for (; kt + 1 < kt_end; kt += 2) {
+      if (kt + 2 < kt_end) load_tile(kt + 2, va0, vb0);
+      compute(smem);
+      store_tile(va1, vb1, smem + STAGE);
+      __syncthreads();
+      if (kt + 3 < kt_end) load_tile(kt + 3, va1, vb1);
+      compute(smem + STAGE);
+      // unconditional (past the last tile it stores stale registers into a stage nothing reads),
+      // so the split can interleave with the MFMAs above
+      store_tile(va0, vb0, smem);
+      __syncthreads();
+    }
+    if (kt < kt_end) compute(smem);  // odd tile count: the last tile sits in stage 0
   }
 
-  conv_epilogue<BM, BN>(p, acc, reinterpret_cast<float*>(smem_raw), m0, n0, tm_idx, split);
+  conv_epilogue<BM, BN>(p, acc, reinterpret_cast<float*>(smem), m0, n0, tm_idx, split);
 }
 
 template <int BM, int BN, int MODE, bool DGRAD>

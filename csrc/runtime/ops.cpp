@@ -91,7 +91,7 @@ void conv_launch(const ConvGemmParams& p, int bm, int bn, bool dgrad, hipStream_
 
 // Workgroups each kernel keeps resident per CU (min of the LDS and VGPR limits of the build).
 int conv_blocks_per_cu(int bm, int bn) {
-  if (conv_gemm_mode() == 1) return (bm + bn) >= 256 ? 2 : (bm + bn) >= 192 ? 3 : 5;
+  if (conv_gemm_mode() == 1) return (bm + bn) >= 256 ? 1 : (bm + bn) >= 192 ? 2 : 3;  // 2 x 3 x (bm+bn) x 64 B
   return std::max(1, std::min(4, (160 * 1024) / (2 * (bm + bn) * 36 * 4)));
 }
 double conv_mfma_rate() { return conv_gemm_mode() == 1 ? 250.0e12 : 120.0e12; }
