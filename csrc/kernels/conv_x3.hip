@@ -33,10 +33,11 @@ namespace {
 constexpr int BK = 32;
 constexpr int LDH = BK;  // bf16 per LDS row (64 B, 16-B chunks XOR-swizzled, see chunk_pos)
 
-// 16-B chunk c (0..3) of LDS row r lives at chunk position c ^ ((r >> 2) & 3): the 8-lane groups
-// of the ds_write_b128 stores (two rows x four chunks) and the 16-lane groups of the ds_read_b128
-// fragment reads (16 rows, one chunk) both hit distinct banks.
-__device__ __forceinline__ int chunk_pos(int r, int c) { return c ^ ((r >> 2) & 3); }
+// 16-B chunk c (0..3) of LDS row r lives at chunk position c ^ f((r >> 2) & 3), f(q) = -q mod 4:
+// the 8-lane groups of the ds_write_b128 stores (two rows x four chunks) and the 16-lane groups
+// of the ds_read_b128 fragment reads hit distinct banks, both for the 32x32x16 operand (16 rows,
+// one chunk) and for the 16x16x32 operand (8 rows x 2 chunks).
+__device__ __forceinline__ int chunk_pos(int r, int c) { return c ^ ((-(r >> 2)) & 3); }
 
 // Split 8 consecutive-k fp32 values into three bf16x8 planes (as 4 packed pairs each).
 __device__ __forceinline__ void split8(const float (&v)[8], u32x4& s0, u32x4& s1, u32x4& s2) {
@@ -50,7 +51,7 @@ __device__ __forceinline__ void split8(const float (&v)[8], u32x4& s0, u32x4& s1
   }
 }
 
-template <int BM, int BN, int MODE, bool DGRAD>
+template <int BM, int BN, int MODE, bool DGRAD, bool M16>
 __global__ __launch_bounds__(256, 2) void conv_x3_kernel(ConvGemmParams p) {
   constexpr int TM = BM / 64;
   constexpr int TN = BN / 64;
@@ -227,49 +228,90 @@ __global__ __launch_bounds__(256, 2) void conv_x3_kernel(ConvGemmParams p) {
     }
   };
 
-  f32x16 acc[TM][TN];
+  // accumulators: 32x32x16 tiles (TM x TN) or 16x16x32 tiles (2TM x 2TN)
+  f32x16 acc[M16 ? 1 : TM][M16 ? 1 : TN];
+  f32x4 acc16[M16 ? 2 * TM : 1][M16 ? 2 * TN : 1];
+  if constexpr (M16) {
 #pragma unroll
-  for (int a = 0; a < TM; ++a)
+    for (int a = 0; a < 2 * TM; ++a)
 #pragma unroll
-    for (int b = 0; b < TN; ++b)
+      for (int b = 0; b < 2 * TN; ++b) acc16[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+  } else {
 #pragma unroll
-      for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
+    for (int a = 0; a < TM; ++a)
+#pragma unroll
+      for (int b = 0; b < TN; ++b)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
+  }
 
   const int l32 = lane & 31;
   const int hh = lane >> 5;
 
-  // MFMAs over one LDS stage (two 16-k steps of six split products per 32x32 tile)
+  // MFMAs over one LDS stage: six split products per output tile and 32-deep K-tile, as two
+  // 32x32x16 steps or one 16x16x32 step
   auto compute = [&](const __bf16* st) {
+    if constexpr (M16) {
+      const int l16 = lane & 15, ch = lane >> 4;
+      bf16x8 bf[2 * TN][3];
 #pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      bf16x8 af[TM][3], bf[TN][3];
-#pragma unroll
-      for (int a = 0; a < TM; ++a) {
-        const int r = wm * (BM / 2) + a * 32 + l32;
-        const __bf16* src = st + r * LDH + chunk_pos(r, 2 * s + hh) * 8;
-#pragma unroll
-        for (int q = 0; q < 3; ++q) af[a][q] = *reinterpret_cast<const bf16x8*>(src + q * PA);
-      }
-#pragma unroll
-      for (int b = 0; b < TN; ++b) {
-        const int r = wn * (BN / 2) + b * 32 + l32;
-        const __bf16* src = st + 3 * PA + r * LDH + chunk_pos(r, 2 * s + hh) * 8;
+      for (int b = 0; b < 2 * TN; ++b) {
+        const int r = wn * (BN / 2) + b * 16 + l16;
+        const __bf16* src = st + 3 * PA + r * LDH + chunk_pos(r, ch) * 8;
 #pragma unroll
         for (int q = 0; q < 3; ++q) bf[b][q] = *reinterpret_cast<const bf16x8*>(src + q * PB);
       }
 #pragma unroll
-      for (int a = 0; a < TM; ++a)
+      for (int a = 0; a < 2 * TM; ++a) {
+        bf16x8 af[3];
+        const int r = wm * (BM / 2) + a * 16 + l16;
+        const __bf16* src = st + r * LDH + chunk_pos(r, ch) * 8;
+#pragma unroll
+        for (int q = 0; q < 3; ++q) af[q] = *reinterpret_cast<const bf16x8*>(src + q * PA);
+#pragma unroll
+        for (int b = 0; b < 2 * TN; ++b) {
+          f32x4 c = acc16[a][b];
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[2], bf[b][0], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[1], bf[b][1], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[0], bf[b][2], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[1], bf[b][0], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[0], bf[b][1], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[0], bf[b][0], c, 0, 0, 0);
+          acc16[a][b] = c;
+        }
+      }
+    } else {
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        bf16x8 af[TM][3], bf[TN][3];
+#pragma unroll
+        for (int a = 0; a < TM; ++a) {
+          const int r = wm * (BM / 2) + a * 32 + l32;
+          const __bf16* src = st + r * LDH + chunk_pos(r, 2 * s + hh) * 8;
+#pragma unroll
+          for (int q = 0; q < 3; ++q) af[a][q] = *reinterpret_cast<const bf16x8*>(src + q * PA);
+        }
 #pragma unroll
         for (int b = 0; b < TN; ++b) {
-          f32x16 c = acc[a][b];
-          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[a][2], bf[b][0], c, 0, 0, 0);
-          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[a][1], bf[b][1], c, 0, 0, 0);
-          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[a][0], bf[b][2], c, 0, 0, 0);
-          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[a][1], bf[b][0], c, 0, 0, 0);
-          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[a][0], bf[b][1], c, 0, 0, 0);
-          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[a][0], bf[b][0], c, 0, 0, 0);
-          acc[a][b] = c;
+          const int r = wn * (BN / 2) + b * 32 + l32;
+          const __bf16* src = st + 3 * PA + r * LDH + chunk_pos(r, 2 * s + hh) * 8;
+#pragma unroll
+          for (int q = 0; q < 3; ++q) bf[b][q] = *reinterpret_cast<const bf16x8*>(src + q * PB);
         }
+#pragma unroll
+        for (int a = 0; a < TM; ++a)
+#pragma unroll
+          for (int b = 0; b < TN; ++b) {
+            f32x16 c = acc[a][b];
+            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[a][2], bf[b][0], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[a][1], bf[b][1], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[a][0], bf[b][2], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[a][1], bf[b][0], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[a][0], bf[b][1], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[a][0], bf[b][0], c, 0, 0, 0);
+            acc[a][b] = c;
+          }
+      }
     }
   };
 
@@ -297,36 +339,38 @@ __global__ __launch_bounds__(256, 2) void conv_x3_kernel(ConvGemmParams p) {
     if (kt < kt_end) compute(smem);  // odd tile count: the last tile sits in stage 0
   }
 
-  conv_epilogue<BM, BN>(p, acc, reinterpret_cast<float*>(smem), m0, n0, tm_idx, split);
+  if constexpr (M16) conv_epilogue16<BM, BN>(p, acc16, reinterpret_cast<float*>(smem), m0, n0, tm_idx, split);
+  else conv_epilogue<BM, BN>(p, acc, reinterpret_cast<float*>(smem), m0, n0, tm_idx, split);
 }
 
 template <int BM, int BN, int MODE, bool DGRAD>
-void launch_x3(const ConvGemmParams& p, int ntiles, hipStream_t st) {
-  hipLaunchKernelGGL((conv_x3_kernel<BM, BN, MODE, DGRAD>), dim3(ntiles * p.splits), dim3(256), 0, st, p);
+void launch_x3(const ConvGemmParams& p, int ntiles, bool m16, hipStream_t st) {
+  if (m16) hipLaunchKernelGGL((conv_x3_kernel<BM, BN, MODE, DGRAD, true>), dim3(ntiles * p.splits), dim3(256), 0, st, p);
+  else hipLaunchKernelGGL((conv_x3_kernel<BM, BN, MODE, DGRAD, false>), dim3(ntiles * p.splits), dim3(256), 0, st, p);
 }
 
 template <int MODE, bool DGRAD>
-void dispatch_x3(const ConvGemmParams& p, int bm, int bn, hipStream_t st) {
+void dispatch_x3(const ConvGemmParams& p, int bm, int bn, bool m16, hipStream_t st) {
   const int ntm = (p.M + bm - 1) / bm, ntn = (p.Nout + bn - 1) / bn;
   const int nt = ntm * ntn;
-  if (bm == 128 && bn == 128) launch_x3<128, 128, MODE, DGRAD>(p, nt, st);
-  else if (bm == 128 && bn == 64) launch_x3<128, 64, MODE, DGRAD>(p, nt, st);
-  else if (bm == 64 && bn == 128) launch_x3<64, 128, MODE, DGRAD>(p, nt, st);
-  else launch_x3<64, 64, MODE, DGRAD>(p, nt, st);
+  if (bm == 128 && bn == 128) launch_x3<128, 128, MODE, DGRAD>(p, nt, m16, st);
+  else if (bm == 128 && bn == 64) launch_x3<128, 64, MODE, DGRAD>(p, nt, m16, st);
+  else if (bm == 64 && bn == 128) launch_x3<64, 128, MODE, DGRAD>(p, nt, m16, st);
+  else launch_x3<64, 64, MODE, DGRAD>(p, nt, m16, st);
 }
 
 }  // namespace
 
-void conv_x3_launch(const ConvGemmParams& p, int bm, int bn, bool dgrad, hipStream_t st) {
+void conv_x3_launch(const ConvGemmParams& p, int bm, int bn, bool dgrad, bool m16, hipStream_t st) {
   if ((p.C % BK) == 0 && (p.Kdim % BK) == 0) {
-    if (dgrad) dispatch_x3<0, true>(p, bm, bn, st);
-    else dispatch_x3<0, false>(p, bm, bn, st);
+    if (dgrad) dispatch_x3<0, true>(p, bm, bn, m16, st);
+    else dispatch_x3<0, false>(p, bm, bn, m16, st);
   } else if ((p.C % 4) == 0 && (p.Kdim % 4) == 0) {
-    if (dgrad) dispatch_x3<1, true>(p, bm, bn, st);
-    else dispatch_x3<1, false>(p, bm, bn, st);
+    if (dgrad) dispatch_x3<1, true>(p, bm, bn, m16, st);
+    else dispatch_x3<1, false>(p, bm, bn, m16, st);
   } else {
-    if (dgrad) dispatch_x3<2, true>(p, bm, bn, st);
-    else dispatch_x3<2, false>(p, bm, bn, st);
+    if (dgrad) dispatch_x3<2, true>(p, bm, bn, m16, st);
+    else dispatch_x3<2, false>(p, bm, bn, m16, st);
   }
 }
 

@@ -56,7 +56,8 @@ struct WgradParams {
 // conv_igemm.hip (exact fp32-input MFMA)
 void conv_igemm_launch(const ConvGemmParams& p, int bm, int bn, bool dgrad, hipStream_t st);
 // conv_x3.hip (fp32-accurate 3-term bf16 split on the bf16 MFMA)
-void conv_x3_launch(const ConvGemmParams& p, int bm, int bn, bool dgrad, hipStream_t st);
+// (m16: v_mfma_f32_16x16x32_bf16 tiles instead of 32x32x16)
+void conv_x3_launch(const ConvGemmParams& p, int bm, int bn, bool dgrad, bool m16, hipStream_t st);
 void splitk_reduce_launch(const float* slab, int S, int M, int Nout, const float* bias, float* y, float* part,
                           hipStream_t st);
 int splitk_rows_per_part();
