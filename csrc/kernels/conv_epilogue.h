@@ -14,10 +14,16 @@
 
 namespace cdp {
 
+// Wave grid: WM x 2 waves (WM = 4 for BM = 256, else 2), each owning (BM/WM) x (BN/2).
+template <int BM>
+constexpr int waves_m() { return BM >= 256 ? 4 : 2; }
+
 template <int BM, int BN>
-__device__ __forceinline__ void conv_epilogue(const ConvGemmParams& p, f32x16 (&acc)[BM / 64][BN / 64], float* red,
-                                              int m0, int n0, int tm_idx, int split) {
-  constexpr int TM = BM / 64, TN = BN / 64;
+__device__ __forceinline__ void conv_epilogue(const ConvGemmParams& p,
+                                              f32x16 (&acc)[BM / waves_m<BM>() / 32][BN / 64], float* red, int m0,
+                                              int n0, int tm_idx, int split) {
+  constexpr int WM = waves_m<BM>();
+  constexpr int TM = BM / WM / 32, TN = BN / 64;
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wid = tid >> 6;
@@ -33,7 +39,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvGemmParams& p, f32x16 (&
         const int n = n0 + wn * (BN / 2) + b * 32 + l32;
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const int m = m0 + wm * (BM / 2) + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
+          const int m = m0 + wm * (BM / WM) + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
           if (m < p.M && n < p.Nout) out[(long long)m * p.Nout + n] = acc[a][b][r];
         }
       }
@@ -53,7 +59,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvGemmParams& p, f32x16 (&
       const int n = n0 + wn * (BN / 2) + b * 32 + l32;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const int m = m0 + wm * (BM / 2) + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
+        const int m = m0 + wm * (BM / WM) + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
         const float v = acc[a][b][r] + bias_v[b];
         acc[a][b][r] = v;
         if (m < p.M && n < p.Nout) p.y[(long long)m * p.Nout + n] = v;
@@ -71,7 +77,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvGemmParams& p, f32x16 (&
     for (int a = 0; a < TM; ++a)
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const int m = m0 + wm * (BM / 2) + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
+        const int m = m0 + wm * (BM / WM) + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
         s += (m < p.M) ? acc[a][b][r] : 0.f;
       }
     s += __shfl_xor(s, 32, kWave);
@@ -86,7 +92,10 @@ __device__ __forceinline__ void conv_epilogue(const ConvGemmParams& p, f32x16 (&
 #pragma unroll
   for (int b = 0; b < TN; ++b) {
     const int c = wn * (BN / 2) + b * 32 + l32;
-    mean_b[b] = (red[c] + red[BN + c]) / (float)cnt;
+    float t = 0.f;
+#pragma unroll
+    for (int w = 0; w < WM; ++w) t += red[w * BN + c];
+    mean_b[b] = t / (float)cnt;
   }
   __syncthreads();
 #pragma unroll
@@ -96,7 +105,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvGemmParams& p, f32x16 (&
     for (int a = 0; a < TM; ++a)
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const int m = m0 + wm * (BM / 2) + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
+        const int m = m0 + wm * (BM / WM) + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
         const float d = acc[a][b][r] - mean_b[b];
         s += (m < p.M) ? d * d : 0.f;
       }
@@ -115,8 +124,11 @@ __device__ __forceinline__ void conv_epilogue(const ConvGemmParams& p, f32x16 (&
       const int n = n0 + c;
       if (n < p.Nout) {
         float* dst = p.part + ((long long)tm_idx * p.Nout + n) * 2;
+        float t = 0.f;
+#pragma unroll
+        for (int w = 0; w < WM; ++w) t += red[w * BN + c];
         dst[0] = mean_b[b];
-        dst[1] = red[c] + red[BN + c];
+        dst[1] = t;
       }
     }
   }
@@ -126,16 +138,18 @@ __device__ __forceinline__ void conv_epilogue(const ConvGemmParams& p, f32x16 (&
 // and rows 4*(l>>4) + r (r = 0..3) of each 16x16 tile; each wave owns (BM/2)x(BN/2) as
 // (BM/32)x(BN/32) tiles.
 template <int BM, int BN>
-__device__ __forceinline__ void conv_epilogue16(const ConvGemmParams& p, f32x4 (&acc)[BM / 32][BN / 32], float* red,
-                                                int m0, int n0, int tm_idx, int split) {
-  constexpr int TM = BM / 32, TN = BN / 32;
+__device__ __forceinline__ void conv_epilogue16(const ConvGemmParams& p,
+                                                f32x4 (&acc)[BM / waves_m<BM>() / 16][BN / 32], float* red, int m0,
+                                                int n0, int tm_idx, int split) {
+  constexpr int WM = waves_m<BM>();
+  constexpr int TM = BM / WM / 16, TN = BN / 32;
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wid = tid >> 6;
   const int wm = wid >> 1, wn = wid & 1;
   const int l16 = lane & 15;
   const int q4 = (lane >> 4) * 4;
-  auto row_of = [&](int a, int r) { return m0 + wm * (BM / 2) + a * 16 + q4 + r; };
+  auto row_of = [&](int a, int r) { return m0 + wm * (BM / WM) + a * 16 + q4 + r; };
   auto col_of = [&](int b) { return n0 + wn * (BN / 2) + b * 16 + l16; };
   if (p.splits > 1) {
     float* out = p.y + (long long)split * p.M * p.Nout;
@@ -196,7 +210,10 @@ __device__ __forceinline__ void conv_epilogue16(const ConvGemmParams& p, f32x4 (
 #pragma unroll
   for (int b = 0; b < TN; ++b) {
     const int c = wn * (BN / 2) + b * 16 + l16;
-    mean_b[b] = (red[c] + red[BN + c]) / (float)cnt;
+    float t = 0.f;
+#pragma unroll
+    for (int w = 0; w < WM; ++w) t += red[w * BN + c];
+    mean_b[b] = t / (float)cnt;
   }
   __syncthreads();
 #pragma unroll
@@ -225,8 +242,11 @@ __device__ __forceinline__ void conv_epilogue16(const ConvGemmParams& p, f32x4 (
       const int n = n0 + c;
       if (n < p.Nout) {
         float* dst = p.part + ((long long)tm_idx * p.Nout + n) * 2;
+        float t = 0.f;
+#pragma unroll
+        for (int w = 0; w < WM; ++w) t += red[w * BN + c];
         dst[0] = mean_b[b];
-        dst[1] = red[c] + red[BN + c];
+        dst[1] = t;
       }
     }
   }

@@ -21,6 +21,8 @@
 // 64 B with XOR-swizzled 16-B chunks (chunk_pos), conflict free for the ds_write_b128 stores and
 // the ds_read_b128 fragment reads. 96 KB of LDS for 128x128 (one workgroup per CU, the MFMA
 // pipe kept busy by the in-wave interleave), 72 KB for 64x128.
+#include <type_traits>
+
 #include "common.h"
 #include "kernels.h"
 #include "conv_epilogue.h"
@@ -51,12 +53,21 @@ __device__ __forceinline__ void split8(const float (&v)[8], u32x4& s0, u32x4& s1
   }
 }
 
-template <int BM, int BN, int MODE, bool DGRAD, bool M16>
-__global__ __launch_bounds__(256, 2) void conv_x3_kernel(ConvGemmParams p) {
-  constexpr int TM = BM / 64;
+// PS (pre-split): p.x / p.w hold three bf16 planes each ([3][N][H][W][C], [3][Nout][Kdim], as
+// written by split3_launch) and the tiles are copied to LDS without the split (MODE 0 only).
+// ABL (diagnostic builds only): bit 0 drops the in-loop global loads, bit 1 the in-loop LDS stores
+template <int BM, int BN, int MODE, bool DGRAD, bool M16, bool PS = false, int ABL = 0>
+__global__ __launch_bounds__(waves_m<BM>() * 128, (BM + BN >= 256) ? 1 : 2) void conv_x3_kernel(ConvGemmParams p) {
+  static_assert(!PS || MODE == 0, "pre-split operands need C % 32 == 0");
+  constexpr unsigned ES = PS ? 1u : 2u;  // log2 bytes per element of the global operands
+  constexpr int WM = waves_m<BM>();  // waves along M (2 x WM waves)
+  constexpr int NT = WM * 128;       // threads
+  constexpr int RS = NT / 4;         // rows covered by one pass of the loaders
+  constexpr int TM = BM / WM / 32;
   constexpr int TN = BN / 64;
-  constexpr int A_LD = BM / 64;  // A rows per thread (row = tid/4 + 64 i), 8 consecutive k each
-  constexpr int B_LD = BN / 64;
+  constexpr int A_LD = BM / RS;  // A rows per thread (row = tid/4 + RS i), 8 consecutive k each
+  constexpr int B_LD = BN / RS;
+  static_assert(A_LD >= 1 && B_LD >= 1, "tile too narrow for the loader");
   constexpr int PA = BM * LDH, PB = BN * LDH;
   constexpr int STAGE = 3 * (PA + PB);  // bf16 per stage: A planes [3][BM][LDH], B planes [3][BN][LDH]
   static_assert(2 * STAGE * 2 >= 2 * BN * 4, "epilogue scratch");
@@ -80,17 +91,19 @@ __global__ __launch_bounds__(256, 2) void conv_x3_kernel(ConvGemmParams p) {
   const int HWC = p.H * p.W * p.C;
 
   const int kq = (tid & 3) * 8;  // this thread's 8 consecutive k within the tile
-  const int rrow = tid >> 2;     // + 64 i
+  const int rrow = tid >> 2;     // + RS i
 
   // buffers (host guarantees < 2 GiB each): out-of-range offsets read as zero
-  const __amdgpu_buffer_rsrc_t xr = make_rsrc(p.x, (unsigned)p.N * (unsigned)HWC * 4u);
-  const __amdgpu_buffer_rsrc_t wr = make_rsrc(p.w, (unsigned)p.Nout * (unsigned)p.Kdim * 4u);
+  const unsigned xplane = ((unsigned)p.N * (unsigned)HWC) << ES;
+  const unsigned wplane = ((unsigned)p.Nout * (unsigned)p.Kdim) << ES;
+  const __amdgpu_buffer_rsrc_t xr = make_rsrc(p.x, PS ? 3u * xplane : xplane);
+  const __amdgpu_buffer_rsrc_t wr = make_rsrc(p.w, PS ? 3u * wplane : wplane);
 
   // per A row: spatial anchor and element offset of (n, anchor, kq)
   int a_h[A_LD], a_w[A_LD], a_n[A_LD], a_off[A_LD];
 #pragma unroll
   for (int i = 0; i < A_LD; ++i) {
-    const int m = m0 + rrow + 64 * i;
+    const int m = m0 + rrow + RS * i;
     const bool ok = m < p.M;
     const int mm = ok ? m : 0;
     const int n = fdiv(mm, p.fd_PQ);
@@ -112,8 +125,8 @@ __global__ __launch_bounds__(256, 2) void conv_x3_kernel(ConvGemmParams p) {
   unsigned b_off[B_LD];
 #pragma unroll
   for (int i = 0; i < B_LD; ++i) {
-    const int n = n0 + rrow + 64 * i;
-    b_off[i] = n < p.Nout ? (unsigned)(mul24(n, p.Kdim) + kq) * 4u : kOOB;
+    const int n = n0 + rrow + RS * i;
+    b_off[i] = n < p.Nout ? (unsigned)(mul24(n, p.Kdim) + kq) << ES : kOOB;
   }
 
   // byte offset of A row i at filter tap (kh, kw), channel offset c (relative to kq); OOB if padded
@@ -122,21 +135,25 @@ __global__ __launch_bounds__(256, 2) void conv_x3_kernel(ConvGemmParams p) {
       int oh = a_h[i] - kh, ow = a_w[i] - kw;
       if (p.stride == 1) {
         const bool ok = (unsigned)oh < (unsigned)p.H && (unsigned)ow < (unsigned)p.W;
-        return ok ? (unsigned)(a_off[i] - mul24(mul24(kh, p.W) + kw, p.C) + c) * 4u : kOOB;
+        return ok ? (unsigned)(a_off[i] - mul24(mul24(kh, p.W) + kw, p.C) + c) << ES : kOOB;
       }
       bool ok = oh >= 0 && ow >= 0 && ((oh | ow) & (p.stride - 1)) == 0;  // stride is 2 (power of two)
       oh >>= 1;
       ow >>= 1;
       ok = ok && oh < p.H && ow < p.W;
-      return ok ? (unsigned)(a_n[i] + mul24(mul24(oh, p.W) + ow, p.C) + kq + c) * 4u : kOOB;
+      return ok ? (unsigned)(a_n[i] + mul24(mul24(oh, p.W) + ow, p.C) + kq + c) << ES : kOOB;
     } else {
       const int ih = a_h[i] + kh, iw = a_w[i] + kw;
       const bool ok = (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W;
-      return ok ? (unsigned)(a_off[i] + mul24(mul24(kh, p.W) + kw, p.C) + c) * 4u : kOOB;
+      return ok ? (unsigned)(a_off[i] + mul24(mul24(kh, p.W) + kw, p.C) + c) << ES : kOOB;
     }
   };
 
-  float va0[A_LD][8], vb0[B_LD][8], va1[A_LD][8], vb1[B_LD][8];  // register ping-pong
+  // register ping-pong: fp32 tiles (8 k per row) or, pre-split, three bf16x8 planes per row
+  typedef std::conditional_t<PS, u32x4[A_LD][3], float[A_LD][8]> StageA;
+  typedef std::conditional_t<PS, u32x4[B_LD][3], float[B_LD][8]> StageB;
+  StageA va0, va1;
+  StageB vb0, vb1;
 
   auto put4 = [](float (&d)[8], int off, float4 v) {
     d[off] = v.x;
@@ -145,9 +162,26 @@ __global__ __launch_bounds__(256, 2) void conv_x3_kernel(ConvGemmParams p) {
     d[off + 3] = v.w;
   };
 
-  auto load_tile = [&](int kt, float (&va)[A_LD][8], float (&vb)[B_LD][8]) {
+  auto load_tile = [&](int kt, auto& va, auto& vb) {
     const int r0 = kt * BK;
-    if (MODE == 0) {
+    if constexpr (PS) {
+      const int tap = fdiv(r0, p.fd_C);
+      const int c0 = r0 - tap * p.C;
+      const int kh = fdiv(tap, p.fd_KW), kw = tap - kh * p.KW;
+#pragma unroll
+      for (int i = 0; i < A_LD; ++i) {
+        const unsigned o = a_voff(i, kh, kw, c0);
+#pragma unroll
+        for (int q = 0; q < 3; ++q) va[i][q] = __builtin_amdgcn_raw_buffer_load_b128(xr, (int)(o + q * xplane), 0, 0);
+      }
+#pragma unroll
+      for (int i = 0; i < B_LD; ++i) {
+        const unsigned o = b_off[i] + ((unsigned)r0 << ES);
+#pragma unroll
+        for (int q = 0; q < 3; ++q) vb[i][q] = __builtin_amdgcn_raw_buffer_load_b128(wr, (int)(o + q * wplane), 0, 0);
+      }
+      return;
+    } else if (MODE == 0) {
       // the whole K-tile lies in one filter tap (C % 32 == 0): tap decode is wave-uniform
       const int tap = fdiv(r0, p.fd_C);
       const int c0 = r0 - tap * p.C;
@@ -187,9 +221,10 @@ __global__ __launch_bounds__(256, 2) void conv_x3_kernel(ConvGemmParams p) {
         }
       }
     }
+    if constexpr (!PS) {
 #pragma unroll
     for (int i = 0; i < B_LD; ++i) {
-      const unsigned o = b_off[i] + (unsigned)r0 * 4u;
+      const unsigned o = b_off[i] + ((unsigned)r0 << ES);
       if (MODE == 0) {
         put4(vb[i], 0, bload4(wr, o));
         put4(vb[i], 4, bload4(wr, o + 16u));
@@ -204,15 +239,30 @@ __global__ __launch_bounds__(256, 2) void conv_x3_kernel(ConvGemmParams p) {
               __builtin_amdgcn_raw_buffer_load_b32(wr, (int)(r0 + kq + j < p.Kdim ? o + 4u * j : kOOB), 0, 0));
       }
     }
+    }
   };
 
-  auto store_tile = [&](const float (&va)[A_LD][8], const float (&vb)[B_LD][8], __bf16* st) {
-    const int cp = chunk_pos(rrow, tid & 3) * 8;  // rrow + 64 i has the same (row >> 2) & 3
+  auto store_tile = [&](const auto& va, const auto& vb, __bf16* st) {
+    const int cp = chunk_pos(rrow, tid & 3) * 8;  // rrow + RS i has the same (row >> 2) & 3
+    if constexpr (PS) {
+#pragma unroll
+      for (int i = 0; i < A_LD; ++i) {
+        __bf16* d = st + (rrow + RS * i) * LDH + cp;
+#pragma unroll
+        for (int q = 0; q < 3; ++q) *reinterpret_cast<u32x4*>(d + q * PA) = va[i][q];
+      }
+#pragma unroll
+      for (int i = 0; i < B_LD; ++i) {
+        __bf16* d = st + 3 * PA + (rrow + RS * i) * LDH + cp;
+#pragma unroll
+        for (int q = 0; q < 3; ++q) *reinterpret_cast<u32x4*>(d + q * PB) = vb[i][q];
+      }
+    } else {
 #pragma unroll
     for (int i = 0; i < A_LD; ++i) {
       u32x4 s0, s1, s2;
       split8(va[i], s0, s1, s2);
-      __bf16* d = st + (rrow + 64 * i) * LDH + cp;
+      __bf16* d = st + (rrow + RS * i) * LDH + cp;
       *reinterpret_cast<u32x4*>(d) = s0;
       *reinterpret_cast<u32x4*>(d + PA) = s1;
       *reinterpret_cast<u32x4*>(d + 2 * PA) = s2;
@@ -221,15 +271,16 @@ __global__ __launch_bounds__(256, 2) void conv_x3_kernel(ConvGemmParams p) {
     for (int i = 0; i < B_LD; ++i) {
       u32x4 s0, s1, s2;
       split8(vb[i], s0, s1, s2);
-      __bf16* d = st + 3 * PA + (rrow + 64 * i) * LDH + cp;
+      __bf16* d = st + 3 * PA + (rrow + RS * i) * LDH + cp;
       *reinterpret_cast<u32x4*>(d) = s0;
       *reinterpret_cast<u32x4*>(d + PB) = s1;
       *reinterpret_cast<u32x4*>(d + 2 * PB) = s2;
     }
+    }
   };
 
   // accumulators: 32x32x16 tiles (TM x TN) or 16x16x32 tiles (2TM x 2TN)
-  f32x16 acc[M16 ? 1 : TM][M16 ? 1 : TN];
+  f32x16 acc[TM][TN];
   f32x4 acc16[M16 ? 2 * TM : 1][M16 ? 2 * TN : 1];
   if constexpr (M16) {
 #pragma unroll
@@ -264,7 +315,7 @@ __global__ __launch_bounds__(256, 2) void conv_x3_kernel(ConvGemmParams p) {
 #pragma unroll
       for (int a = 0; a < 2 * TM; ++a) {
         bf16x8 af[3];
-        const int r = wm * (BM / 2) + a * 16 + l16;
+        const int r = wm * (BM / WM) + a * 16 + l16;
         const __bf16* src = st + r * LDH + chunk_pos(r, ch) * 8;
 #pragma unroll
         for (int q = 0; q < 3; ++q) af[q] = *reinterpret_cast<const bf16x8*>(src + q * PA);
@@ -286,7 +337,7 @@ __global__ __launch_bounds__(256, 2) void conv_x3_kernel(ConvGemmParams p) {
         bf16x8 af[TM][3], bf[TN][3];
 #pragma unroll
         for (int a = 0; a < TM; ++a) {
-          const int r = wm * (BM / 2) + a * 32 + l32;
+          const int r = wm * (BM / WM) + a * 32 + l32;
           const __bf16* src = st + r * LDH + chunk_pos(r, 2 * s + hh) * 8;
 #pragma unroll
           for (int q = 0; q < 3; ++q) af[a][q] = *reinterpret_cast<const bf16x8*>(src + q * PA);
@@ -325,15 +376,15 @@ __global__ __launch_bounds__(256, 2) void conv_x3_kernel(ConvGemmParams p) {
     __syncthreads();
     int kt = kt_begin;
     for (; kt + 1 < kt_end; kt += 2) {
-      if (kt + 2 < kt_end) load_tile(kt + 2, va0, vb0);
+      if (!(ABL & 1) && kt + 2 < kt_end) load_tile(kt + 2, va0, vb0);
       compute(smem);
-      store_tile(va1, vb1, smem + STAGE);
+      if (!(ABL & 2)) store_tile(va1, vb1, smem + STAGE);
       __syncthreads();
-      if (kt + 3 < kt_end) load_tile(kt + 3, va1, vb1);
+      if (!(ABL & 1) && kt + 3 < kt_end) load_tile(kt + 3, va1, vb1);
       compute(smem + STAGE);
       // unconditional (past the last tile it stores stale registers into a stage nothing reads),
       // so the split can interleave with the MFMAs above
-      store_tile(va0, vb0, smem);
+      if (!(ABL & 2)) store_tile(va0, vb0, smem);
       __syncthreads();
     }
     if (kt < kt_end) compute(smem);  // odd tile count: the last tile sits in stage 0
@@ -345,21 +396,57 @@ __global__ __launch_bounds__(256, 2) void conv_x3_kernel(ConvGemmParams p) {
 
 template <int BM, int BN, int MODE, bool DGRAD>
 void launch_x3(const ConvGemmParams& p, int ntiles, bool m16, hipStream_t st) {
-  if (m16) hipLaunchKernelGGL((conv_x3_kernel<BM, BN, MODE, DGRAD, true>), dim3(ntiles * p.splits), dim3(256), 0, st, p);
-  else hipLaunchKernelGGL((conv_x3_kernel<BM, BN, MODE, DGRAD, false>), dim3(ntiles * p.splits), dim3(256), 0, st, p);
+  const dim3 blk(waves_m<BM>() * 128);
+  if (m16) hipLaunchKernelGGL((conv_x3_kernel<BM, BN, MODE, DGRAD, true>), dim3(ntiles * p.splits), blk, 0, st, p);
+  else hipLaunchKernelGGL((conv_x3_kernel<BM, BN, MODE, DGRAD, false>), dim3(ntiles * p.splits), blk, 0, st, p);
 }
 
 template <int MODE, bool DGRAD>
 void dispatch_x3(const ConvGemmParams& p, int bm, int bn, bool m16, hipStream_t st) {
   const int ntm = (p.M + bm - 1) / bm, ntn = (p.Nout + bn - 1) / bn;
   const int nt = ntm * ntn;
-  if (bm == 128 && bn == 128) launch_x3<128, 128, MODE, DGRAD>(p, nt, m16, st);
+  if (bm == 256) launch_x3<256, 128, MODE, DGRAD>(p, nt, m16, st);
+  else if (bm == 128 && bn == 128) launch_x3<128, 128, MODE, DGRAD>(p, nt, m16, st);
   else if (bm == 128 && bn == 64) launch_x3<128, 64, MODE, DGRAD>(p, nt, m16, st);
   else if (bm == 64 && bn == 128) launch_x3<64, 128, MODE, DGRAD>(p, nt, m16, st);
   else launch_x3<64, 64, MODE, DGRAD>(p, nt, m16, st);
 }
 
+template <int BM, int BN, bool DGRAD>
+void launch_x3ps(const ConvGemmParams& p, int ntiles, hipStream_t st) {
+  hipLaunchKernelGGL((conv_x3_kernel<BM, BN, 0, DGRAD, false, true>), dim3(ntiles * p.splits), dim3(256), 0, st, p);
+}
+
 }  // namespace
+
+// diagnostic: 128x128 forward x3 kernel with parts of the pipeline removed (results are wrong)
+void conv_x3_ablate_launch(const ConvGemmParams& p, int abl, bool ps, hipStream_t st) {
+  const int nt = ((p.M + 127) / 128) * ((p.Nout + 127) / 128);
+  dim3 g(nt * p.splits), b(256);
+  if (ps) {
+    if (abl == 1) hipLaunchKernelGGL((conv_x3_kernel<128, 128, 0, false, false, true, 1>), g, b, 0, st, p);
+    else if (abl == 2) hipLaunchKernelGGL((conv_x3_kernel<128, 128, 0, false, false, true, 2>), g, b, 0, st, p);
+    else if (abl == 3) hipLaunchKernelGGL((conv_x3_kernel<128, 128, 0, false, false, true, 3>), g, b, 0, st, p);
+    else hipLaunchKernelGGL((conv_x3_kernel<128, 128, 0, false, false, true, 0>), g, b, 0, st, p);
+  } else {
+    if (abl == 1) hipLaunchKernelGGL((conv_x3_kernel<128, 128, 0, false, false, false, 1>), g, b, 0, st, p);
+    else if (abl == 2) hipLaunchKernelGGL((conv_x3_kernel<128, 128, 0, false, false, false, 2>), g, b, 0, st, p);
+    else if (abl == 3) hipLaunchKernelGGL((conv_x3_kernel<128, 128, 0, false, false, false, 3>), g, b, 0, st, p);
+    else hipLaunchKernelGGL((conv_x3_kernel<128, 128, 0, false, false, false, 0>), g, b, 0, st, p);
+  }
+}
+
+namespace {
+
+}  // namespace
+
+void conv_x3ps_launch(const ConvGemmParams& p, int bm, int bn, bool dgrad, hipStream_t st) {
+  const int nt = ((p.M + bm - 1) / bm) * ((p.Nout + bn - 1) / bn);
+  if (bm == 128 && bn == 128) dgrad ? launch_x3ps<128, 128, true>(p, nt, st) : launch_x3ps<128, 128, false>(p, nt, st);
+  else if (bm == 128) dgrad ? launch_x3ps<128, 64, true>(p, nt, st) : launch_x3ps<128, 64, false>(p, nt, st);
+  else if (bn == 128) dgrad ? launch_x3ps<64, 128, true>(p, nt, st) : launch_x3ps<64, 128, false>(p, nt, st);
+  else dgrad ? launch_x3ps<64, 64, true>(p, nt, st) : launch_x3ps<64, 64, false>(p, nt, st);
+}
 
 void conv_x3_launch(const ConvGemmParams& p, int bm, int bn, bool dgrad, bool m16, hipStream_t st) {
   if ((p.C % BK) == 0 && (p.Kdim % BK) == 0) {

@@ -58,6 +58,10 @@ void conv_igemm_launch(const ConvGemmParams& p, int bm, int bn, bool dgrad, hipS
 // conv_x3.hip (fp32-accurate 3-term bf16 split on the bf16 MFMA)
 // (m16: v_mfma_f32_16x16x32_bf16 tiles instead of 32x32x16)
 void conv_x3_launch(const ConvGemmParams& p, int bm, int bn, bool dgrad, bool m16, hipStream_t st);
+// pre-split operands (x, w = three bf16 planes each, from split3_launch); C % 32 == 0 only
+void conv_x3ps_launch(const ConvGemmParams& p, int bm, int bn, bool dgrad, hipStream_t st);
+void split3_launch(const float* x, long long n, void* planes, hipStream_t st);
+void conv_x3_ablate_launch(const ConvGemmParams& p, int abl, bool ps, hipStream_t st);
 void splitk_reduce_launch(const float* slab, int S, int M, int Nout, const float* bias, float* y, float* part,
                           hipStream_t st);
 int splitk_rows_per_part();

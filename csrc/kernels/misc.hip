@@ -10,6 +10,7 @@
 //   torch.mean(torch.stack(inputs), 0)  /root/reference/src/Part 2a/main.py:122
 #include "common.h"
 #include "kernels.h"
+#include "x3_common.h"
 
 namespace cdp {
 namespace {
@@ -412,6 +413,20 @@ int grid_for(long long n) {
   return (int)b;
 }
 
+
+// ------------------------------------------------------------------ split3
+// x (fp32, n elements) -> three bf16 planes [3][n] with x = h0 + h1 + h2 (x3_common.h)
+__global__ __launch_bounds__(256) void split3_kernel(const float* __restrict__ x, long long n, unsigned* __restrict__ out) {
+  const long long npair = n >> 1;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < npair; i += (long long)gridDim.x * blockDim.x) {
+    const float2 v = reinterpret_cast<const float2*>(x)[i];
+    unsigned a, b, c;
+    split_pair(v.x, v.y, a, b, c);
+    out[i] = a;
+    out[npair + i] = b;
+    out[2 * npair + i] = c;
+  }
+}
 }  // namespace
 
 void xent_fwd_launch(const float* logits, const long long* tgt, int B, int C, float* loss, long long* correct,
@@ -479,6 +494,13 @@ void maxpool_bwd_launch(const float* gy, const int* arg, int N, int H, int W, in
                         hipStream_t st) {
   hipLaunchKernelGGL(maxpool_bwd_kernel, dim3(grid_for((long long)N * Ho * Wo * C)), dim3(256), 0, st, gy, arg, N, H,
                      W, C, Ho, Wo, gx);
+}
+
+void split3_launch(const float* x, long long n, void* planes, hipStream_t st) {
+  long long b = (n / 2 + 255) / 256;
+  if (b > 4096) b = 4096;
+  if (b < 1) b = 1;
+  hipLaunchKernelGGL(split3_kernel, dim3((unsigned)b), dim3(256), 0, st, x, n, reinterpret_cast<unsigned*>(planes));
 }
 
 }  // namespace cdp

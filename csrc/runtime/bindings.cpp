@@ -16,6 +16,7 @@ PYBIND11_MODULE(_C, m) {
   // -------------------------------------------------------------- kernels
   m.def("set_conv_gemm", &set_conv_gemm, py::arg("mode"), "select the conv GEMM engine: x3 (3-term bf16 split, fp32-accurate) or f32 (exact fp32 MFMA)");
   m.def("get_conv_gemm", &get_conv_gemm);
+  m.def("bench_presplit", &bench_presplit, "experiment: in-kernel split vs pre-split bf16 planes (conv fwd GEMM)");
   m.def("conv2d_fwd", &conv2d_fwd, py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("stride"), py::arg("pad"),
         py::arg("want_stats") = false);
   m.def("conv2d_dgrad", &conv2d_dgrad);
