@@ -221,11 +221,26 @@ def main():
                 "backend": args.backend,
                 "hipgraph": graph is not None,
                 "optimizer": "SGD(lr=0.1, momentum=0.9, wd=1e-4)",
+                # conv GEMM numerics: fp32 operands/accumulation; "x3" = fp32-accurate 3-term
+                # bf16 split on the bf16 MFMA (error vs fp64 <= the exact fp32 MFMA's, see
+                # docs/PERF.md), "f32" = exact fp32-input MFMA
+                "conv_gemm": _conv_gemm_engine(args.backend),
             },
         }
         print(json.dumps(rec), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def _conv_gemm_engine(backend):
+    if backend != "native":
+        return "miopen"
+    try:
+        from cs744_distributed_data_parallel_amd import _native
+
+        return _native.lib().get_conv_gemm()
+    except Exception:  # pragma: no cover - CPU-only environments
+        return "reference"
 
 
 if __name__ == "__main__":
