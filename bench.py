@@ -58,6 +58,9 @@ def main():
 
     faulthandler.enable()
     args = parse()
+    # hang guard: a stuck collective or kernel ends the process (with every thread's traceback)
+    # instead of holding the node; generous against the ~1 min a run takes
+    faulthandler.dump_traceback_later(float(os.environ.get("CDP_BENCH_TIMEOUT_S", "1200")), exit=True)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -76,7 +79,9 @@ def main():
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("rccl" if args.backend == "native" else "nccl", rank=rank, world_size=world)
+        # collectives that stall longer than 5 minutes are aborted by the communicator's watchdog
+        dist.init_process_group("rccl" if args.backend == "native" else "nccl", rank=rank, world_size=world,
+                                comm_timeout_s=300.0)
     if args.backend == "native":
         cdp._native.lib()  # fail loudly if the HIP extension is missing
 
@@ -230,6 +235,7 @@ def main():
         print(json.dumps(rec), flush=True)
     if world > 1:
         dist.destroy_process_group()
+    faulthandler.cancel_dump_traceback_later()
 
 
 def _conv_gemm_engine(backend):

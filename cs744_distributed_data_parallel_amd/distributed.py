@@ -100,7 +100,11 @@ def init_process_group(
         if backend == "rccl" and _native.available():
             store = tdist.distributed_c10d._get_default_store()
             t = comm_timeout_s if comm_timeout_s is not None else timeout.total_seconds()
-            _S.rccl = RcclCommunicator(rank, world_size, local, store, t)
+            try:
+                _S.rccl = RcclCommunicator(rank, world_size, local, store, t)
+            except RuntimeError as e:  # e.g. an RCCL build without this topology: keep torch's RCCL PG
+                warnings.warn(f"native RCCL communicator unavailable ({e}); using the torch nccl process group")
+                _S.rccl = None
     elif backend == "gloo":
         tdist.init_process_group("gloo", init_method=init_method, rank=rank, world_size=world_size, timeout=timeout)
         _S.device = torch.device("cpu")
