@@ -62,7 +62,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvGemmParams& p,
         const int m = m0 + wm * (BM / WM) + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
         const float v = acc[a][b][r] + bias_v[b];
         acc[a][b][r] = v;
-        if (m < p.M && n < p.Nout) p.y[(long long)m * p.Nout + n] = v;
+        if (m < p.M && n < p.Nout) p.y[remap_row(p.rr, m) * p.Nout + n] = v;
       }
     }
   if (!p.part) return;
@@ -182,7 +182,7 @@ __device__ __forceinline__ void conv_epilogue16(const ConvGemmParams& p,
         const int m = row_of(a, r);
         const float v = acc[a][b][r] + bias_v[b];
         acc[a][b][r] = v;
-        if (m < p.M && n < p.Nout) p.y[(long long)m * p.Nout + n] = v;
+        if (m < p.M && n < p.Nout) p.y[remap_row(p.rr, m) * p.Nout + n] = v;
       }
     }
   if (!p.part) return;

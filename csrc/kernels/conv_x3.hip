@@ -112,7 +112,7 @@ __global__ __launch_bounds__(waves_m<BM>() * 128, (BM + BN >= 256) ? 1 : 2) void
     const int qq = rem - mul24(pp, p.Q);
     if (DGRAD) {
       a_h[i] = pp + p.pad;  // oh*stride = ih + pad - kh
-      a_w[i] = qq + p.pad;
+      a_w[i] = qq + p.pad_w;  // column pad (differs from pad in sub-pixel class launches)
     } else {
       a_h[i] = mul24(pp, p.stride) - p.pad;
       a_w[i] = mul24(qq, p.stride) - p.pad;

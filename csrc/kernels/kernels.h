@@ -31,6 +31,24 @@ __device__ __forceinline__ int fdiv(int n, const FastDiv& f) {
 }
 #endif
 
+// Output-row remap of a sub-pixel data-gradient launch: GEMM row m = (n, i, j) over a P x Q class
+// grid lands in dX row (n, 2i + ph, 2j + pw) of an H x W image.
+struct RowRemap {
+  int on, H, W, ph, pw, P, Q;
+  FastDiv fd_PQ, fd_Q;
+};
+
+#if defined(__HIPCC__)
+__device__ __forceinline__ long long remap_row(const RowRemap& r, int m) {
+  if (!r.on) return m;
+  const int n = fdiv(m, r.fd_PQ);
+  const int rem = m - n * r.P * r.Q;
+  const int i = fdiv(rem, r.fd_Q);
+  const int j = rem - i * r.Q;
+  return ((long long)n * r.H + 2 * i + r.ph) * r.W + 2 * j + r.pw;
+}
+#endif
+
 struct ConvGemmParams {
   const float* x;     // gather source, NHWC [N][H][W][C]
   const float* w;     // B^T rows [Nout][Kdim], Kdim ordered (kh, kw, c)
@@ -42,6 +60,8 @@ struct ConvGemmParams {
   int KH, KW, stride, pad;
   int Nout, M, Kdim, ktiles, splits;
   FastDiv fd_PQ, fd_Q, fd_C, fd_KW;
+  int pad_w;    // data gradient, sub-pixel class launches only: column pad (pad is the row pad)
+  RowRemap rr;  // sub-pixel class launches: scatter output rows into dX
 };
 
 struct WgradParams {
@@ -63,7 +83,7 @@ void conv_x3ps_launch(const ConvGemmParams& p, int bm, int bn, bool dgrad, hipSt
 void split3_launch(const float* x, long long n, void* planes, hipStream_t st);
 void conv_x3_ablate_launch(const ConvGemmParams& p, int abl, bool ps, hipStream_t st);
 void splitk_reduce_launch(const float* slab, int S, int M, int Nout, const float* bias, float* y, float* part,
-                          hipStream_t st);
+                          hipStream_t st, const RowRemap* rr = nullptr);
 int splitk_rows_per_part();
 
 // wgrad.hip
@@ -103,6 +123,9 @@ void augment_launch(const unsigned char* imgs, const long long* idx, long long i
                     unsigned long long seed, float* out, hipStream_t st);
 void counter_inc_launch(long long* c, hipStream_t st);
 void wtrans_launch(const float* w, float* wt, int Co, int T, int Ci, hipStream_t st);
+// sub-filter transpose: wt[ci][a][b][co] = w[co][kh0 + 2a][kw0 + 2b][ci] (a < nkh, b < nkw)
+void wtrans_sub_launch(const float* w, float* wt, int Co, int KH, int KW, int Ci, int kh0, int kw0, int nkh, int nkw,
+                       hipStream_t st);
 void stack_mean_launch(const float* const* srcs, int k, long long n, float* dst, hipStream_t st);
 void scale_launch(float* x, long long n, float a, hipStream_t st);
 void colsum_launch(const float* x, int R, int C, float* out, bool accumulate, hipStream_t st);

@@ -427,6 +427,26 @@ __global__ __launch_bounds__(256) void split3_kernel(const float* __restrict__ x
     out[2 * npair + i] = c;
   }
 }
+
+// sub-filter transpose for the sub-pixel data gradient: wt[ci][a][b][co] = w[co][kh0+2a][kw0+2b][ci]
+__global__ __launch_bounds__(256) void wtrans_sub_kernel(const float* __restrict__ w, float* __restrict__ wt, int Co,
+                                                         int KH, int KW, int Ci, int kh0, int kw0, int nkw) {
+  __shared__ float tile[32][33];
+  const int t = blockIdx.z;  // sub-tap a * nkw + b
+  const int tap_in = (kh0 + 2 * (t / nkw)) * KW + kw0 + 2 * (t % nkw);
+  const int T_in = KH * KW, T_out = gridDim.z;
+  const int co0 = blockIdx.y * 32, ci0 = blockIdx.x * 32;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+  for (int j = ty; j < 32; j += 8) {
+    const int co = co0 + j, ci = ci0 + tx;
+    tile[j][tx] = (co < Co && ci < Ci) ? w[((long long)co * T_in + tap_in) * Ci + ci] : 0.f;
+  }
+  __syncthreads();
+  for (int j = ty; j < 32; j += 8) {
+    const int ci = ci0 + j, co = co0 + tx;
+    if (ci < Ci && co < Co) wt[((long long)ci * T_out + t) * Co + co] = tile[tx][j];
+  }
+}
 }  // namespace
 
 void xent_fwd_launch(const float* logits, const long long* tgt, int B, int C, float* loss, long long* correct,
@@ -501,6 +521,12 @@ void split3_launch(const float* x, long long n, void* planes, hipStream_t st) {
   if (b > 4096) b = 4096;
   if (b < 1) b = 1;
   hipLaunchKernelGGL(split3_kernel, dim3((unsigned)b), dim3(256), 0, st, x, n, reinterpret_cast<unsigned*>(planes));
+}
+
+void wtrans_sub_launch(const float* w, float* wt, int Co, int KH, int KW, int Ci, int kh0, int kw0, int nkh, int nkw,
+                       hipStream_t st) {
+  dim3 grid((Ci + 31) / 32, (Co + 31) / 32, nkh * nkw);
+  hipLaunchKernelGGL(wtrans_sub_kernel, grid, dim3(256), 0, st, w, wt, Co, KH, KW, Ci, kh0, kw0, nkw);
 }
 
 }  // namespace cdp

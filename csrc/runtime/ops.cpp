@@ -307,6 +307,74 @@ std::vector<at::Tensor> conv2d_fwd(const at::Tensor& x_, const at::Tensor& w_, c
 }
 
 // ---------------------------------------------------------------- conv data gradient
+// Stride-2 data gradient by sub-pixel decomposition: the input pixels of parity class (ph, pw)
+// receive gradient only from the filter taps kh = kh0 + 2a, kw = kw0 + 2b, kh0 = (ph + pad) % 2,
+// through dY[(ih + pad - kh) / 2]. Each class is therefore a dense stride-1 correlation of dY with
+// a quarter-size sub-filter over a quarter of the rows: 4 GEMMs doing 1/4 of the work of the
+// masked full-resolution gather (which spends 3/4 of its MACs on taps that cannot contribute).
+// Classes without taps (e.g. the odd pixels of a 1x1 stride-2 conv) get zeros from a K-less
+// launch. Returns false when a shape is outside the x3 kernels' addressing limits.
+bool subpixel_enabled() {
+  static const bool on = [] {
+    const char* e = std::getenv("CDP_DGRAD_SUBPIXEL");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
+bool conv2d_dgrad_subpixel(const at::Tensor& dy, const at::Tensor& w, at::Tensor& dx, int pad, hipStream_t st) {
+  const int N = dx.size(0), C = dx.size(1), H = dx.size(2), W = dx.size(3);
+  const int Co = w.size(0), KH = w.size(2), KW = w.size(3);
+  const int P = dy.size(2), Q = dy.size(3);
+  if (Co % 32 != 0) return false;
+  std::vector<at::Tensor> keep;  // sub-filters / slabs stay alive until the launches are enqueued
+  for (int ph = 0; ph < 2; ++ph)
+    for (int pw = 0; pw < 2; ++pw) {
+      const int Hc = (H - ph + 1) / 2, Wc = (W - pw + 1) / 2;
+      if (Hc <= 0 || Wc <= 0) continue;
+      const int kh0 = (ph + pad) % 2, kw0 = (pw + pad) % 2;
+      const int nkh = kh0 < KH ? (KH - kh0 + 1) / 2 : 0, nkw = kw0 < KW ? (KW - kw0 + 1) / 2 : 0;
+      const long long Mc = (long long)N * Hc * Wc;
+      const int Kc = nkh * nkw * Co;
+      ConvGemmParams p{};
+      p.N = N; p.H = P; p.W = Q; p.C = Co; p.P = Hc; p.Q = Wc;
+      p.KH = std::max(nkh, 1); p.KW = std::max(nkw, 1); p.stride = 1;
+      p.pad = (ph + pad - kh0) / 2;  // oh = i + pad - a
+      p.pad_w = (pw + pad - kw0) / 2;
+      p.Nout = C; p.M = (int)Mc; p.Kdim = Kc;
+      set_divs(p);
+      p.rr = RowRemap{1, H, W, ph, pw, Hc, Wc, make_fastdiv(Hc * Wc), make_fastdiv(Wc)};
+      p.x = dy.data_ptr<float>();
+      if (!x3_ok(p, true)) return false;
+      at::Tensor wt;
+      if (Kc > 0) {
+        wt = at::empty({C, Kc}, dy.options());
+        wtrans_sub_launch(w.data_ptr<float>(), wt.data_ptr<float>(), Co, KH, KW, C, kh0, kw0, nkh, nkw, st);
+        keep.push_back(wt);
+        p.w = wt.data_ptr<float>();
+      } else {
+        p.w = w.data_ptr<float>();  // never read: no K-tiles
+      }
+      GemmPlan g = plan_gemm(Mc, C, std::max(Kc, 32));
+      p.ktiles = (Kc + 31) / 32;
+      p.splits = Kc > 0 ? g.splits : 1;
+      if (p.splits == 1) {
+        p.y = dx.data_ptr<float>();
+        conv_launch(p, g.bm, g.bn, true, st);
+      } else {
+        at::Tensor slab = at::empty({p.splits, Mc, C}, dy.options());
+        keep.push_back(slab);
+        p.y = slab.data_ptr<float>();
+        RowRemap rr = p.rr;
+        p.rr.on = 0;  // slabs are class-local; the reduction scatters
+        conv_launch(p, g.bm, g.bn, true, st);
+        splitk_reduce_launch(slab.data_ptr<float>(), p.splits, (int)Mc, C, nullptr, dx.data_ptr<float>(), nullptr,
+                             st, &rr);
+      }
+    }
+  return true;
+}
+
 // dX[N, C, H, W] from dY[N, Co, P, Q] and W[Co, C, KH, KW] (any stride / padding).
 at::Tensor conv2d_dgrad(const at::Tensor& dy_, const at::Tensor& w_, std::vector<int64_t> in_shape, int64_t stride,
                         int64_t pad) {
@@ -320,6 +388,10 @@ at::Tensor conv2d_dgrad(const at::Tensor& dy_, const at::Tensor& w_, std::vector
   TORCH_CHECK(dy.size(1) == Co && dy.size(0) == N, "dgrad shape mismatch");
   auto opts = dy.options();
   hipStream_t st = cur_stream();
+  if (stride == 2 && conv_gemm_mode() == 1 && subpixel_enabled()) {
+    at::Tensor dx = at::empty({N, C, H, W}, opts.memory_format(at::MemoryFormat::ChannelsLast));
+    if (conv2d_dgrad_subpixel(dy, w, dx, (int)pad, st)) return dx;
+  }
   // Wt[ci][tap][co] = W[co][tap][ci]
   at::Tensor wt = at::empty({C, KH * KW * Co}, opts);
   wtrans_launch(w.data_ptr<float>(), wt.data_ptr<float>(), Co, KH * KW, C, st);
@@ -331,7 +403,7 @@ at::Tensor conv2d_dgrad(const at::Tensor& dy_, const at::Tensor& w_, std::vector
   p.x = dy.data_ptr<float>();
   p.w = wt.data_ptr<float>();
   p.N = N; p.H = P; p.W = Q; p.C = Co; p.P = H; p.Q = W;
-  p.KH = KH; p.KW = KW; p.stride = (int)stride; p.pad = (int)pad;
+  p.KH = KH; p.KW = KW; p.stride = (int)stride; p.pad = (int)pad; p.pad_w = (int)pad;
   p.Nout = C; p.M = (int)M; p.Kdim = Kdim; p.ktiles = g.ktiles; p.splits = g.splits;
   set_divs(p);
   if (g.splits == 1) {
@@ -754,7 +826,7 @@ std::vector<double> bench_presplit(const at::Tensor& x_, const at::Tensor& w_, i
   GemmPlan g = plan_gemm(M, Co, Kdim);
   ConvGemmParams p{};
   p.N = N; p.H = H; p.W = W; p.C = C; p.P = P; p.Q = Q;
-  p.KH = KH; p.KW = KW; p.stride = (int)stride; p.pad = (int)pad;
+  p.KH = KH; p.KW = KW; p.stride = (int)stride; p.pad = (int)pad; p.pad_w = (int)pad;
   p.Nout = Co; p.M = (int)M; p.Kdim = Kdim; p.ktiles = g.ktiles; p.splits = 1;
   set_divs(p);
   auto opts = x.options();
