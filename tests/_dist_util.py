@@ -15,7 +15,7 @@ def free_port() -> int:
     return p
 
 
-def _entry(rank, world, port, fn, args, q):
+def _entry(rank, world, port, fn, args, q, init_kwargs=None):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     os.environ["RANK"] = str(rank)
@@ -27,7 +27,7 @@ def _entry(rank, world, port, fn, args, q):
     try:
         from cs744_distributed_data_parallel_amd import distributed as dist
 
-        dist.init_process_group("gloo", rank=rank, world_size=world)
+        dist.init_process_group("gloo", rank=rank, world_size=world, **(init_kwargs or {}))
         try:
             out = fn(rank, world, *args)
         finally:
@@ -37,11 +37,11 @@ def _entry(rank, world, port, fn, args, q):
         q.put((rank, "err", traceback.format_exc()))
 
 
-def run_ranks(fn, world=2, args=(), timeout=240):
+def run_ranks(fn, world=2, args=(), timeout=240, init_kwargs=None):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = free_port()
-    procs = [ctx.Process(target=_entry, args=(r, world, port, fn, args, q)) for r in range(world)]
+    procs = [ctx.Process(target=_entry, args=(r, world, port, fn, args, q, init_kwargs)) for r in range(world)]
     for p in procs:
         p.start()
     results = {}

@@ -225,3 +225,28 @@ def test_bucket_rebuild_in_ready_order():
     assert rebuilt
     assert sum(before) == sum(after)
     assert res[0][1] == res[1][1]  # identical plan on all ranks
+
+
+def _dead_peer(rank, world):
+    import time
+
+    from cs744_distributed_data_parallel_amd import distributed as dist
+
+    if rank == 1:
+        time.sleep(6)  # never enters the collective within the group timeout
+        return ("slept", 0.0)
+    t0 = time.time()
+    try:
+        dist.all_reduce(torch.ones(4))
+    except Exception:  # failure detection: the collective times out instead of hanging
+        return ("raised", time.time() - t0)
+    return ("completed", time.time() - t0)
+
+
+def test_dead_peer_is_detected_by_timeout():
+    import datetime
+
+    res = run_ranks(_dead_peer, 2, init_kwargs={"timeout": datetime.timedelta(seconds=2)}, timeout=120)
+    status, dt = res[0]
+    assert status == "raised", res
+    assert dt < 6.0, res
