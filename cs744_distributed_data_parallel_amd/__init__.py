@@ -16,7 +16,7 @@ Typical use (mirrors the reference API)::
     loss = cdp.ops.CrossEntropyLoss()(model(x), y); loss.backward(); opt.step()
 """
 from . import _native, data, distributed, models, ops, optim, parallel, utils
-from .models import VGG11, VGG13, VGG16, VGG19, get_model, resnet50
+from .models import VGG11, VGG13, VGG16, VGG19, ResNet, get_model, resnet18, resnet34, resnet50, resnet101, resnet152
 from .ops import CrossEntropyLoss
 from .optim import SGD
 from .parallel import DDP, DistributedDataParallel
@@ -25,7 +25,8 @@ __version__ = "0.1.0"
 
 __all__ = [
     "_native", "data", "distributed", "models", "ops", "optim", "parallel", "utils",
-    "VGG11", "VGG13", "VGG16", "VGG19", "get_model", "resnet50", "CrossEntropyLoss", "SGD",
+    "VGG11", "VGG13", "VGG16", "VGG19", "get_model", "ResNet", "resnet18", "resnet34", "resnet50", "resnet101",
+    "resnet152", "CrossEntropyLoss", "SGD",
     "DDP", "DistributedDataParallel", "native_available",
 ]
 

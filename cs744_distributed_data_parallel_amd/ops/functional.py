@@ -17,6 +17,7 @@ import torch.nn.functional as F
 from .. import _native
 
 __all__ = [
+    "GradSink",
     "conv_bn_act",
     "linear",
     "cross_entropy",
@@ -45,15 +46,33 @@ def _bn_momentum(bn) -> float:
 
 
 # --------------------------------------------------------------------------- conv + BN + act
+class GradSink:
+    """Hands a residual-branch gradient from a block's last fused op to its first one.
+
+    In a ResNet identity block the block input x feeds both conv1 and the residual add of conv3,
+    so autograd would sum two full-size gradients with a separate add kernel. With a sink, conv3's
+    backward parks the residual gradient here instead of returning it, and conv1's data-gradient
+    GEMM accumulates onto it in its epilogue (writing the sum in place). conv1's backward always
+    runs after conv3's: it needs conv2's output gradient, which needs conv3's.
+    """
+
+    __slots__ = ("grad",)
+
+    def __init__(self):
+        self.grad = None
+
+
 class _ConvBNAct(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, b, gamma, beta, rm, rv, nbt, momentum, eps, training, stride, pad, pool, relu, residual):
+    def forward(ctx, x, w, b, gamma, beta, rm, rv, nbt, momentum, eps, training, stride, pad, pool, relu, residual,
+                res_sink=None, dx_sink=None):
         C = _native.lib()
         out, y, stats, xsave = C.conv_bn_act_fwd(
             x, w, b, gamma, beta, rm, rv, nbt, momentum, eps, training, stride, pad, pool, relu, residual
         )
         ctx.cfg = (stride, pad, pool, relu, training, b is not None, residual is not None)
         ctx.params = (w, b, gamma, beta)
+        ctx.sinks = (res_sink, dx_sink)
         zout = out if residual is not None else None
         ctx.save_for_backward(xsave, w, y, stats, zout)  # xsave: x, or x zero-padded to 4k channels
         return out
@@ -62,13 +81,19 @@ class _ConvBNAct(torch.autograd.Function):
     def backward(ctx, gout):
         x, w, y, stats, zout = ctx.saved_tensors
         stride, pad, pool, relu, training, has_bias, has_res = ctx.cfg
+        res_sink, dx_sink = ctx.sinks
         C = _native.lib()
         wp, bp, gp, betap = ctx.params
         nig = ctx.needs_input_grad
+        addend = None
+        if dx_sink is not None and nig[0]:
+            addend, dx_sink.grad = dx_sink.grad, None
         dx, dw, db, dgamma, dbeta, dres = C.conv_bn_act_bwd(
             gout, x, w, y, stats, stride, pad, pool, relu, nig[0], has_bias, zout, training,
-            _slot(wp, nig[1]), _slot(bp, nig[2] and has_bias), _slot(gp, nig[3]), _slot(betap, nig[4]),
+            _slot(wp, nig[1]), _slot(bp, nig[2] and has_bias), _slot(gp, nig[3]), _slot(betap, nig[4]), addend,
         )
+        if has_res and res_sink is not None:
+            res_sink.grad, dres = dres, None
         return (
             dx if ctx.needs_input_grad[0] else None,
             dw,
@@ -77,14 +102,17 @@ class _ConvBNAct(torch.autograd.Function):
             dbeta if ctx.needs_input_grad[4] else None,
             None, None, None, None, None, None, None, None, None, None,
             dres if has_res else None,
+            None, None,
         )
 
 
-def conv_bn_act(x, conv, bn, relu: bool = True, pool: bool = False, residual=None):
+def conv_bn_act(x, conv, bn, relu: bool = True, pool: bool = False, residual=None, res_sink=None, dx_sink=None):
     """``[maxpool2x2](act(bn(conv(x)) [+ residual]))`` for an ``nn.Conv2d`` / ``nn.BatchNorm2d`` pair.
 
     ``pool`` is the reference's ``MaxPool2d(kernel_size=2, stride=2)``; ``relu`` its
     ``ReLU(inplace=True)``; ``residual`` (ResNet) is added after BN and before the activation.
+    ``res_sink`` / ``dx_sink`` (:class:`GradSink`, GPU path only) route the residual gradient of an
+    identity block into the data-gradient GEMM of the block's first conv instead of an autograd add.
     """
     stride = conv.stride[0]
     pad = conv.padding[0]
@@ -108,6 +136,8 @@ def conv_bn_act(x, conv, bn, relu: bool = True, pool: bool = False, residual=Non
             pool,
             relu,
             residual,
+            res_sink,
+            dx_sink,
         )
     y = F.conv2d(x, conv.weight, conv.bias, conv.stride, conv.padding)
     y = bn(y)
@@ -186,17 +216,18 @@ class _MaxPool(torch.autograd.Function):
         y, arg = _native.lib().maxpool2d_fwd(x, k, s, p)
         ctx.save_for_backward(arg)
         ctx.in_shape = list(x.shape)
+        ctx.ksp = (k, s, p)
         return y
 
     @staticmethod
     def backward(ctx, gy):
         (arg,) = ctx.saved_tensors
-        return _native.lib().maxpool2d_bwd(gy, arg, ctx.in_shape), None, None, None
+        return _native.lib().maxpool2d_bwd(gy, arg, ctx.in_shape, *ctx.ksp), None, None, None
 
 
 def max_pool2d(x, kernel_size, stride=None, padding=0):
     stride = kernel_size if stride is None else stride
-    if use_native(x):
+    if use_native(x) and x.shape[1] % 4 == 0:
         return _MaxPool.apply(x, int(kernel_size), int(stride), int(padding))
     return F.max_pool2d(x, kernel_size, stride, padding)
 

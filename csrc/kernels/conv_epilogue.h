@@ -60,9 +60,13 @@ __device__ __forceinline__ void conv_epilogue(const ConvGemmParams& p,
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int m = m0 + wm * (BM / WM) + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
-        const float v = acc[a][b][r] + bias_v[b];
+        float v = acc[a][b][r] + bias_v[b];
+        if (m < p.M && n < p.Nout) {
+          const long long o = remap_row(p.rr, m) * p.Nout + n;
+          if (p.addend) v += p.addend[o];
+          p.y[o] = v;
+        }
         acc[a][b][r] = v;
-        if (m < p.M && n < p.Nout) p.y[remap_row(p.rr, m) * p.Nout + n] = v;
       }
     }
   if (!p.part) return;
@@ -180,9 +184,13 @@ __device__ __forceinline__ void conv_epilogue16(const ConvGemmParams& p,
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int m = row_of(a, r);
-        const float v = acc[a][b][r] + bias_v[b];
+        float v = acc[a][b][r] + bias_v[b];
+        if (m < p.M && n < p.Nout) {
+          const long long o = remap_row(p.rr, m) * p.Nout + n;
+          if (p.addend) v += p.addend[o];
+          p.y[o] = v;
+        }
         acc[a][b][r] = v;
-        if (m < p.M && n < p.Nout) p.y[remap_row(p.rr, m) * p.Nout + n] = v;
       }
     }
   if (!p.part) return;

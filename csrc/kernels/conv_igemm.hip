@@ -245,8 +245,9 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvGemmParams p) {
 // Thread = one output column of a 64-column strip; 4 row lanes x RB/4 rows.
 constexpr int RB = 32;
 __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restrict__ slab, int S, int M, int Nout,
-                                                            const float* __restrict__ bias, float* __restrict__ y,
-                                                            float* __restrict__ part, RowRemap rr) {
+                                                            const float* __restrict__ bias, float* y,
+                                                            float* __restrict__ part, RowRemap rr,
+                                                            const float* addend) {
   __shared__ float red[4][64];
   const int col = threadIdx.x & 63;
   const int rl = threadIdx.x >> 6;
@@ -264,7 +265,9 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
       const float* src = slab + (long long)m * Nout + n;
       for (int z = 0; z < S; ++z) s += src[z * plane];
       s += bv;
-      y[remap_row(rr, m) * Nout + n] = s;
+      const long long o = remap_row(rr, m) * Nout + n;
+      if (addend) s += addend[o];
+      y[o] = s;
     }
     v[i] = s;
   }
@@ -295,8 +298,9 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
 // float4 variant (Nout % 4 == 0): block = 16 column quads (64 columns) x 16 row lanes, RB rows;
 // every thread keeps 2 rows x 4 columns in registers and issues its S slab loads back to back.
 __global__ __launch_bounds__(256) void splitk_reduce4_kernel(const float* __restrict__ slab, int S, int M, int Nout,
-                                                             const float* __restrict__ bias, float* __restrict__ y,
-                                                             float* __restrict__ part, RowRemap rr) {
+                                                             const float* __restrict__ bias, float* y,
+                                                             float* __restrict__ part, RowRemap rr,
+                                                            const float* addend) {
   __shared__ float4 red[16][16];
   const int cq = threadIdx.x & 15;
   const int rl = threadIdx.x >> 4;
@@ -324,7 +328,12 @@ __global__ __launch_bounds__(256) void splitk_reduce4_kernel(const float* __rest
         s.x += a.x; s.y += a.y; s.z += a.z; s.w += a.w;
       }
       s.x += bv.x; s.y += bv.y; s.z += bv.z; s.w += bv.w;
-      st4(y + remap_row(rr, m) * Nout + n, s);
+      const long long o = remap_row(rr, m) * Nout + n;
+      if (addend) {
+        const float4 ad = ld4(addend + o);
+        s.x += ad.x; s.y += ad.y; s.z += ad.z; s.w += ad.w;
+      }
+      st4(y + o, s);
     }
     v[i] = s;
   }
@@ -395,12 +404,12 @@ void conv_igemm_launch(const ConvGemmParams& p, int bm, int bn, bool dgrad, hipS
 }
 
 void splitk_reduce_launch(const float* slab, int S, int M, int Nout, const float* bias, float* y, float* part,
-                          hipStream_t st, const RowRemap* rr) {
+                          hipStream_t st, const RowRemap* rr, const float* addend) {
   dim3 grid((Nout + 63) / 64, (M + RB - 1) / RB);
   const RowRemap r = rr ? *rr : RowRemap{};
   if ((Nout & 3) == 0)
-    hipLaunchKernelGGL(splitk_reduce4_kernel, grid, dim3(256), 0, st, slab, S, M, Nout, bias, y, part, r);
-  else hipLaunchKernelGGL(splitk_reduce_kernel, grid, dim3(256), 0, st, slab, S, M, Nout, bias, y, part, r);
+    hipLaunchKernelGGL(splitk_reduce4_kernel, grid, dim3(256), 0, st, slab, S, M, Nout, bias, y, part, r, addend);
+  else hipLaunchKernelGGL(splitk_reduce_kernel, grid, dim3(256), 0, st, slab, S, M, Nout, bias, y, part, r, addend);
 }
 
 }  // namespace cdp

@@ -62,6 +62,7 @@ struct ConvGemmParams {
   FastDiv fd_PQ, fd_Q, fd_C, fd_KW;
   int pad_w;    // data gradient, sub-pixel class launches only: column pad (pad is the row pad)
   RowRemap rr;  // sub-pixel class launches: scatter output rows into dX
+  const float* addend;  // optional: y += addend (same layout as y; may alias y)
 };
 
 struct WgradParams {
@@ -83,7 +84,7 @@ void conv_x3ps_launch(const ConvGemmParams& p, int bm, int bn, bool dgrad, hipSt
 void split3_launch(const float* x, long long n, void* planes, hipStream_t st);
 void conv_x3_ablate_launch(const ConvGemmParams& p, int abl, bool ps, hipStream_t st);
 void splitk_reduce_launch(const float* slab, int S, int M, int Nout, const float* bias, float* y, float* part,
-                          hipStream_t st, const RowRemap* rr = nullptr);
+                          hipStream_t st, const RowRemap* rr = nullptr, const float* addend = nullptr);
 int splitk_rows_per_part();
 
 // wgrad.hip
@@ -135,9 +136,10 @@ void small_linear_bwd_launch(const float* dy, const float* x, const float* w, in
                              float* db, hipStream_t st);
 void avgpool_fwd_launch(const float* x, int N, int HW, int C, float* y, hipStream_t st);
 void avgpool_bwd_launch(const float* gy, int N, int HW, int C, float* gx, hipStream_t st);
+// NHWC, C % 4 == 0; arg = window-local argmax tap (uint8, k*k <= 255)
 void maxpool_fwd_launch(const float* x, int N, int H, int W, int C, int k, int s, int p, int Ho, int Wo, float* y,
-                        int* arg, hipStream_t st);
-void maxpool_bwd_launch(const float* gy, const int* arg, int N, int H, int W, int C, int Ho, int Wo, float* gx,
-                        hipStream_t st);
+                        unsigned char* arg, hipStream_t st);
+void maxpool_bwd_launch(const float* gy, const unsigned char* arg, int N, int H, int W, int C, int k, int s, int p,
+                        int Ho, int Wo, float* gx, hipStream_t st);
 
 }  // namespace cdp

@@ -371,38 +371,77 @@ __global__ __launch_bounds__(256) void avgpool_bwd_kernel(const float* __restric
 }
 
 // MaxPool2d(k, s, p) forward on NHWC with int32 argmax (flat h*W+w), and backward (scatter-add).
+// Max-pool on NHWC, float4 along C. The argmax is kept as the window-local tap index (uint8,
+// first max wins in (dh, dw) scan order like ATen), a quarter of an int32 index map.
 __global__ __launch_bounds__(256) void maxpool_fwd_kernel(const float* __restrict__ x, int N, int H, int W, int C,
                                                           int k, int s, int pd, int Ho, int Wo, float* __restrict__ y,
-                                                          int* __restrict__ arg) {
-  const long long total = (long long)N * Ho * Wo * C;
+                                                          unsigned char* __restrict__ arg) {
+  const int C4 = C >> 2;
+  const long long total = (long long)N * Ho * Wo * C4;
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long long)gridDim.x * blockDim.x) {
-    const int c = (int)(i % C);
-    long long t = i / C;
-    const int wo = (int)(t % Wo);
-    t /= Wo;
+    const int c4 = (int)(i % C4);
+    const long long pix = i / C4;
+    const int wo = (int)(pix % Wo);
+    const long long t = pix / Wo;
     const int ho = (int)(t % Ho);
     const int n = (int)(t / Ho);
-    float mx = -INFINITY;
-    int am = -1;
-    for (int dh = 0; dh < k; ++dh)
+    float m[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+    int am[4] = {-1, -1, -1, -1};
+    const float* base = x + (long long)n * H * W * C + 4 * c4;
+    for (int dh = 0; dh < k; ++dh) {
+      const int h = ho * s - pd + dh;
+      if ((unsigned)h >= (unsigned)H) continue;
       for (int dw = 0; dw < k; ++dw) {
-        const int h = ho * s - pd + dh, w = wo * s - pd + dw;
-        if ((unsigned)h >= (unsigned)H || (unsigned)w >= (unsigned)W) continue;
-        const float v = x[(((long long)n * H + h) * W + w) * C + c];
-        if (v > mx || am < 0) { mx = v; am = h * W + w; }
+        const int w = wo * s - pd + dw;
+        if ((unsigned)w >= (unsigned)W) continue;
+        const float4 v = ld4(base + ((long long)h * W + w) * C);
+        const float vv[4] = {v.x, v.y, v.z, v.w};
+        const int tap = dh * k + dw;
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          if (vv[e] > m[e] || am[e] < 0) {
+            m[e] = vv[e];
+            am[e] = tap;
+          }
       }
-    y[i] = mx;
-    arg[i] = am;
+    }
+    st4(y + pix * C + 4 * c4, make_float4(m[0], m[1], m[2], m[3]));
+    *reinterpret_cast<uchar4*>(arg + pix * C + 4 * c4) =
+        make_uchar4((unsigned char)am[0], (unsigned char)am[1], (unsigned char)am[2], (unsigned char)am[3]);
   }
 }
-__global__ __launch_bounds__(256) void maxpool_bwd_kernel(const float* __restrict__ gy, const int* __restrict__ arg,
-                                                          int N, int H, int W, int C, int Ho, int Wo,
+
+// Gather form of the backward (no atomics, no zero fill): every input element sums the gradients
+// of the windows that cover it and whose argmax tap is this element.
+__global__ __launch_bounds__(256) void maxpool_bwd_kernel(const float* __restrict__ gy,
+                                                          const unsigned char* __restrict__ arg, int N, int H, int W,
+                                                          int C, int k, int s, int pd, int Ho, int Wo,
                                                           float* __restrict__ gx) {
-  const long long total = (long long)N * Ho * Wo * C;
+  const int C4 = C >> 2;
+  const long long total = (long long)N * H * W * C4;
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long long)gridDim.x * blockDim.x) {
-    const int c = (int)(i % C);
-    const long long n = i / ((long long)Ho * Wo * C);
-    atomicAdd(gx + ((n * H * W) + arg[i]) * C + c, gy[i]);
+    const int c4 = (int)(i % C4);
+    const long long pix = i / C4;
+    const int w = (int)(pix % W);
+    const long long t = pix / W;
+    const int h = (int)(t % H);
+    const int n = (int)(t / H);
+    // windows ho with ho*s - pd <= h <= ho*s - pd + k - 1
+    const int ho0 = max(0, (h + pd - k + s) / s), ho1 = min(Ho - 1, (h + pd) / s);
+    const int wo0 = max(0, (w + pd - k + s) / s), wo1 = min(Wo - 1, (w + pd) / s);
+    float g[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int ho = ho0; ho <= ho1; ++ho)
+      for (int wo = wo0; wo <= wo1; ++wo) {
+        const int tap = (h - (ho * s - pd)) * k + (w - (wo * s - pd));
+        const long long o = (((long long)n * Ho + ho) * Wo + wo) * C + 4 * c4;
+        const uchar4 a = *reinterpret_cast<const uchar4*>(arg + o);
+        const float4 v = ld4(gy + o);
+        if (a.x == tap) g[0] += v.x;
+        if (a.y == tap) g[1] += v.y;
+        if (a.z == tap) g[2] += v.z;
+        if (a.w == tap) g[3] += v.w;
+      }
+    st4(gx + pix * C + 4 * c4, make_float4(g[0], g[1], g[2], g[3]));
   }
 }
 
@@ -506,14 +545,14 @@ void avgpool_bwd_launch(const float* gy, int N, int HW, int C, float* gx, hipStr
   hipLaunchKernelGGL(avgpool_bwd_kernel, dim3(grid_for((long long)N * HW * C)), dim3(256), 0, st, gy, N, HW, C, gx);
 }
 void maxpool_fwd_launch(const float* x, int N, int H, int W, int C, int k, int s, int p, int Ho, int Wo, float* y,
-                        int* arg, hipStream_t st) {
-  hipLaunchKernelGGL(maxpool_fwd_kernel, dim3(grid_for((long long)N * Ho * Wo * C)), dim3(256), 0, st, x, N, H, W, C,
-                     k, s, p, Ho, Wo, y, arg);
+                        unsigned char* arg, hipStream_t st) {
+  hipLaunchKernelGGL(maxpool_fwd_kernel, dim3(grid_for((long long)N * Ho * Wo * (C / 4))), dim3(256), 0, st, x, N,
+                     H, W, C, k, s, p, Ho, Wo, y, arg);
 }
-void maxpool_bwd_launch(const float* gy, const int* arg, int N, int H, int W, int C, int Ho, int Wo, float* gx,
-                        hipStream_t st) {
-  hipLaunchKernelGGL(maxpool_bwd_kernel, dim3(grid_for((long long)N * Ho * Wo * C)), dim3(256), 0, st, gy, arg, N, H,
-                     W, C, Ho, Wo, gx);
+void maxpool_bwd_launch(const float* gy, const unsigned char* arg, int N, int H, int W, int C, int k, int s, int p,
+                        int Ho, int Wo, float* gx, hipStream_t st) {
+  hipLaunchKernelGGL(maxpool_bwd_kernel, dim3(grid_for((long long)N * H * W * (C / 4))), dim3(256), 0, st, gy, arg,
+                     N, H, W, C, k, s, p, Ho, Wo, gx);
 }
 
 void split3_launch(const float* x, long long n, void* planes, hipStream_t st) {

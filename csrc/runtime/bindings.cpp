@@ -19,14 +19,16 @@ PYBIND11_MODULE(_C, m) {
   m.def("bench_presplit", &bench_presplit, "experiment: in-kernel split vs pre-split bf16 planes (conv fwd GEMM)");
   m.def("conv2d_fwd", &conv2d_fwd, py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("stride"), py::arg("pad"),
         py::arg("want_stats") = false);
-  m.def("conv2d_dgrad", &conv2d_dgrad);
+  m.def("conv2d_dgrad", &conv2d_dgrad, py::arg("dy"), py::arg("w"), py::arg("in_shape"), py::arg("stride"),
+        py::arg("pad"), py::arg("addend") = py::none());
   m.def("conv2d_wgrad", &conv2d_wgrad, py::arg("dy"), py::arg("x"), py::arg("w_shape"), py::arg("stride"),
         py::arg("pad"), py::arg("out") = py::none(), py::arg("accumulate") = false);
   m.def("conv_bn_act_fwd", &conv_bn_act_fwd);
   m.def("conv_bn_act_bwd", &conv_bn_act_bwd, py::arg("gout"), py::arg("x"), py::arg("w"), py::arg("y"),
         py::arg("stats"), py::arg("stride"), py::arg("pad"), py::arg("pool"), py::arg("relu"), py::arg("need_dx"),
         py::arg("has_bias"), py::arg("zout") = py::none(), py::arg("training") = true, py::arg("dw_out") = py::none(),
-        py::arg("db_out") = py::none(), py::arg("dgamma_out") = py::none(), py::arg("dbeta_out") = py::none());
+        py::arg("db_out") = py::none(), py::arg("dgamma_out") = py::none(), py::arg("dbeta_out") = py::none(),
+        py::arg("dx_addend") = py::none());
   m.def("linear_fwd", &linear_fwd);
   m.def("linear_bwd", &linear_bwd, py::arg("gy"), py::arg("x"), py::arg("w"), py::arg("need_dx"),
         py::arg("has_bias"), py::arg("dw_out") = py::none(), py::arg("db_out") = py::none());

@@ -322,7 +322,8 @@ bool subpixel_enabled() {
   return on;
 }
 
-bool conv2d_dgrad_subpixel(const at::Tensor& dy, const at::Tensor& w, at::Tensor& dx, int pad, hipStream_t st) {
+bool conv2d_dgrad_subpixel(const at::Tensor& dy, const at::Tensor& w, at::Tensor& dx, int pad, hipStream_t st,
+                           const float* addend) {
   const int N = dx.size(0), C = dx.size(1), H = dx.size(2), W = dx.size(3);
   const int Co = w.size(0), KH = w.size(2), KW = w.size(3);
   const int P = dy.size(2), Q = dy.size(3);
@@ -360,6 +361,7 @@ bool conv2d_dgrad_subpixel(const at::Tensor& dy, const at::Tensor& w, at::Tensor
       p.splits = Kc > 0 ? g.splits : 1;
       if (p.splits == 1) {
         p.y = dx.data_ptr<float>();
+        p.addend = addend;
         conv_launch(p, g.bm, g.bn, true, st);
       } else {
         at::Tensor slab = at::empty({p.splits, Mc, C}, dy.options());
@@ -369,7 +371,7 @@ bool conv2d_dgrad_subpixel(const at::Tensor& dy, const at::Tensor& w, at::Tensor
         p.rr.on = 0;  // slabs are class-local; the reduction scatters
         conv_launch(p, g.bm, g.bn, true, st);
         splitk_reduce_launch(slab.data_ptr<float>(), p.splits, (int)Mc, C, nullptr, dx.data_ptr<float>(), nullptr,
-                             st, &rr);
+                             st, &rr, addend);
       }
     }
   return true;
@@ -377,7 +379,7 @@ bool conv2d_dgrad_subpixel(const at::Tensor& dy, const at::Tensor& w, at::Tensor
 
 // dX[N, C, H, W] from dY[N, Co, P, Q] and W[Co, C, KH, KW] (any stride / padding).
 at::Tensor conv2d_dgrad(const at::Tensor& dy_, const at::Tensor& w_, std::vector<int64_t> in_shape, int64_t stride,
-                        int64_t pad) {
+                        int64_t pad, const c10::optional<at::Tensor>& addend) {
   check_f32_cuda(dy_, "grad_output");
   check_f32_cuda(w_, "weight");
   const at::Tensor dy = nhwc(dy_);
@@ -388,14 +390,21 @@ at::Tensor conv2d_dgrad(const at::Tensor& dy_, const at::Tensor& w_, std::vector
   TORCH_CHECK(dy.size(1) == Co && dy.size(0) == N, "dgrad shape mismatch");
   auto opts = dy.options();
   hipStream_t st = cur_stream();
+  // dx = dgrad (+ addend, accumulated in the GEMM epilogue and written over the addend in place)
+  const bool has_add = addend.has_value() && addend->defined();
+  if (has_add)
+    TORCH_CHECK(addend->scalar_type() == at::kFloat && addend->is_contiguous(at::MemoryFormat::ChannelsLast) &&
+                    addend->size(0) == N && addend->size(1) == C && addend->size(2) == H && addend->size(3) == W,
+                "dgrad addend must be a channels_last fp32 tensor of the input's shape");
+  const float* addp = has_add ? addend->data_ptr<float>() : nullptr;
   if (stride == 2 && conv_gemm_mode() == 1 && subpixel_enabled()) {
-    at::Tensor dx = at::empty({N, C, H, W}, opts.memory_format(at::MemoryFormat::ChannelsLast));
-    if (conv2d_dgrad_subpixel(dy, w, dx, (int)pad, st)) return dx;
+    at::Tensor dx = has_add ? *addend : at::empty({N, C, H, W}, opts.memory_format(at::MemoryFormat::ChannelsLast));
+    if (conv2d_dgrad_subpixel(dy, w, dx, (int)pad, st, addp)) return dx;
   }
   // Wt[ci][tap][co] = W[co][tap][ci]
   at::Tensor wt = at::empty({C, KH * KW * Co}, opts);
   wtrans_launch(w.data_ptr<float>(), wt.data_ptr<float>(), Co, KH * KW, C, st);
-  at::Tensor dx = at::empty({N, C, H, W}, opts.memory_format(at::MemoryFormat::ChannelsLast));
+  at::Tensor dx = has_add ? *addend : at::empty({N, C, H, W}, opts.memory_format(at::MemoryFormat::ChannelsLast));
   const long long M = (long long)N * H * W;
   const int Kdim = KH * KW * Co;
   GemmPlan g = plan_gemm(M, C, Kdim);
@@ -408,12 +417,14 @@ at::Tensor conv2d_dgrad(const at::Tensor& dy_, const at::Tensor& w_, std::vector
   set_divs(p);
   if (g.splits == 1) {
     p.y = dx.data_ptr<float>();
+    p.addend = addp;
     conv_launch(p, g.bm, g.bn, true, st);
   } else {
     at::Tensor slab = at::empty({g.splits, M, C}, opts);
     p.y = slab.data_ptr<float>();
     conv_launch(p, g.bm, g.bn, true, st);
-    splitk_reduce_launch(slab.data_ptr<float>(), g.splits, (int)M, C, nullptr, dx.data_ptr<float>(), nullptr, st);
+    splitk_reduce_launch(slab.data_ptr<float>(), g.splits, (int)M, C, nullptr, dx.data_ptr<float>(), nullptr, st,
+                         nullptr, addp);
   }
   return dx;
 }
@@ -533,7 +544,8 @@ std::vector<at::Tensor> conv_bn_act_bwd(const at::Tensor& gout_, const at::Tenso
                                         const c10::optional<at::Tensor>& dw_out,
                                         const c10::optional<at::Tensor>& db_out,
                                         const c10::optional<at::Tensor>& dgamma_out,
-                                        const c10::optional<at::Tensor>& dbeta_out) {
+                                        const c10::optional<at::Tensor>& dbeta_out,
+                                        const c10::optional<at::Tensor>& dx_addend) {
   check_f32_cuda(gout_, "grad_output");
   const at::Tensor gout = nhwc(gout_);
   const int N = y.size(0), C = y.size(1), H = y.size(2), W = y.size(3);
@@ -587,10 +599,13 @@ std::vector<at::Tensor> conv_bn_act_bwd(const at::Tensor& gout_, const at::Tenso
     c10::hip::HIPCachingAllocator::recordStream(dw.storage().data_ptr(), c10::hip::getCurrentHIPStream());
   if (need_dx) {
     if (padc) {
-      at::Tensor dx4 = conv2d_dgrad(dy, pad_channels4(nhwc(w)), {x.size(0), x.size(1), x.size(2), x.size(3)}, stride, pad);
+      at::Tensor dx4 = conv2d_dgrad(dy, pad_channels4(nhwc(w)), {x.size(0), x.size(1), x.size(2), x.size(3)}, stride,
+                                    pad, c10::nullopt);
       dx = dx4.narrow(1, 0, w.size(1)).contiguous(at::MemoryFormat::ChannelsLast);
+      if (dx_addend.has_value() && dx_addend->defined()) dx.add_(*dx_addend);
     } else {
-      dx = conv2d_dgrad(dy, w, {x.size(0), x.size(1), x.size(2), x.size(3)}, stride, pad);
+      // residual-branch gradient (dx_addend) is accumulated by the data-gradient GEMM's epilogue
+      dx = conv2d_dgrad(dy, w, {x.size(0), x.size(1), x.size(2), x.size(3)}, stride, pad, dx_addend);
     }
   }
   if (overlap) join_from(side);
@@ -774,22 +789,24 @@ void scale_(at::Tensor x, double a) {
 std::vector<at::Tensor> maxpool2d_fwd(const at::Tensor& x_, int64_t k, int64_t s, int64_t p) {
   const at::Tensor x = nhwc(x_);
   const int N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
+  TORCH_CHECK(C % 4 == 0 && k * k <= 255, "maxpool2d: needs C % 4 == 0 and k*k <= 255");
   const int Ho = (H + 2 * p - k) / s + 1, Wo = (W + 2 * p - k) / s + 1;
   at::Tensor y = at::empty({N, C, Ho, Wo}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
-  at::Tensor arg = at::empty({N, C, Ho, Wo}, x.options().dtype(at::kInt).memory_format(at::MemoryFormat::ChannelsLast));
-  maxpool_fwd_launch(x.data_ptr<float>(), N, H, W, C, k, s, p, Ho, Wo, y.data_ptr<float>(), arg.data_ptr<int>(),
+  at::Tensor arg = at::empty({N, C, Ho, Wo}, x.options().dtype(at::kByte).memory_format(at::MemoryFormat::ChannelsLast));
+  maxpool_fwd_launch(x.data_ptr<float>(), N, H, W, C, k, s, p, Ho, Wo, y.data_ptr<float>(), arg.data_ptr<uint8_t>(),
                      cur_stream());
   return {y, arg};
 }
 
-at::Tensor maxpool2d_bwd(const at::Tensor& gy_, const at::Tensor& arg, std::vector<int64_t> in_shape) {
+at::Tensor maxpool2d_bwd(const at::Tensor& gy_, const at::Tensor& arg, std::vector<int64_t> in_shape, int64_t k,
+                         int64_t s, int64_t p) {
   const at::Tensor gy = nhwc(gy_);
   const int N = in_shape[0], C = in_shape[1], H = in_shape[2], W = in_shape[3];
-  // at::zeros ignores TensorOptions::memory_format -> allocate channels_last explicitly, then clear
+  TORCH_CHECK(arg.scalar_type() == at::kByte && arg.is_contiguous(at::MemoryFormat::ChannelsLast),
+              "maxpool2d_bwd: arg must be the uint8 channels_last map of maxpool2d_fwd");
   at::Tensor gx = at::empty({N, C, H, W}, gy.options().memory_format(at::MemoryFormat::ChannelsLast));
-  gx.zero_();
-  maxpool_bwd_launch(gy.data_ptr<float>(), arg.data_ptr<int>(), N, H, W, C, gy.size(2), gy.size(3),
-                     gx.data_ptr<float>(), cur_stream());
+  maxpool_bwd_launch(gy.data_ptr<float>(), arg.data_ptr<uint8_t>(), N, H, W, C, (int)k, (int)s, (int)p, gy.size(2),
+                     gy.size(3), gx.data_ptr<float>(), cur_stream());
   return gx;
 }
 

@@ -13,7 +13,7 @@ std::string get_conv_gemm();
 std::vector<at::Tensor> conv2d_fwd(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tensor>& bias,
                                    int64_t stride, int64_t pad, bool want_stats);
 at::Tensor conv2d_dgrad(const at::Tensor& dy, const at::Tensor& w, std::vector<int64_t> in_shape, int64_t stride,
-                        int64_t pad);
+                        int64_t pad, const c10::optional<at::Tensor>& addend);
 at::Tensor conv2d_wgrad(const at::Tensor& dy, const at::Tensor& x, std::vector<int64_t> w_shape, int64_t stride,
                         int64_t pad, const c10::optional<at::Tensor>& out, bool accumulate);
 at::Tensor conv2d_wgrad_keep(const at::Tensor& dy, const at::Tensor& x, std::vector<int64_t> w_shape, int64_t stride,
@@ -32,7 +32,8 @@ std::vector<at::Tensor> conv_bn_act_bwd(const at::Tensor& gout, const at::Tensor
                                         const c10::optional<at::Tensor>& dw_out,
                                         const c10::optional<at::Tensor>& db_out,
                                         const c10::optional<at::Tensor>& dgamma_out,
-                                        const c10::optional<at::Tensor>& dbeta_out);
+                                        const c10::optional<at::Tensor>& dbeta_out,
+                                        const c10::optional<at::Tensor>& dx_addend);
 at::Tensor linear_fwd(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tensor>& b);
 std::vector<at::Tensor> linear_bwd(const at::Tensor& gy, const at::Tensor& x, const at::Tensor& w, bool need_dx,
                                    bool has_bias, const c10::optional<at::Tensor>& dw_out,
@@ -49,7 +50,8 @@ void counter_inc(at::Tensor c);
 void stack_mean(const std::vector<at::Tensor>& srcs, at::Tensor dst);
 void scale_(at::Tensor x, double a);
 std::vector<at::Tensor> maxpool2d_fwd(const at::Tensor& x, int64_t k, int64_t s, int64_t p);
-at::Tensor maxpool2d_bwd(const at::Tensor& gy, const at::Tensor& arg, std::vector<int64_t> in_shape);
+at::Tensor maxpool2d_bwd(const at::Tensor& gy, const at::Tensor& arg, std::vector<int64_t> in_shape, int64_t k,
+                         int64_t s, int64_t p);
 at::Tensor avgpool_fwd(const at::Tensor& x);
 at::Tensor avgpool_bwd(const at::Tensor& gy, std::vector<int64_t> in_shape);
 

@@ -250,6 +250,16 @@ def test_pooling_ops():
     y.backward(g)
     ref.backward(g.double().cpu())
     assert rel_err(xn.grad, xr.grad) < 1e-6
+    # ties (all-zero windows after a ReLU): the first max in scan order takes the gradient, as in ATen
+    xt = torch.randn(2, 32, 16, 16, device="cuda").clamp_min(0.5) - 0.5
+    xtn = cl(xt).requires_grad_()
+    yt = CF.max_pool2d(xtn, 3, 2, 1)
+    xtr = xt.double().cpu().requires_grad_()
+    reft = F.max_pool2d(xtr, 3, 2, 1)
+    gt = torch.randn_like(yt)
+    yt.backward(gt)
+    reft.backward(gt.double().cpu())
+    assert rel_err(yt, reft) < 1e-6 and rel_err(xtn.grad, xtr.grad) < 1e-6
     x2 = cl(torch.randn(4, 128, 7, 7, device="cuda")).requires_grad_()
     p = CF.global_avg_pool(x2)
     x2r = x2.detach().double().cpu().requires_grad_()

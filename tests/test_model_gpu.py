@@ -104,6 +104,23 @@ def test_resnet50_forward_backward_small(monkeypatch):
     assert e_nat < max(3 * e_t32, 1e-4), (e_nat, e_t32)
 
 
+def test_resnet18_basic_blocks_gradients():
+    """BasicBlock identity shortcuts (residual gradient summed inside conv1's dgrad epilogue)."""
+    import cs744_distributed_data_parallel_amd as cdp
+
+    torch.manual_seed(1)
+    ref = cdp.resnet18(num_classes=10, channels_last=False).double()
+    model = cdp.resnet18(num_classes=10).cuda()
+    model.load_state_dict({k: v.float().cuda() for k, v in ref.state_dict().items()})
+    x = torch.randn(2, 3, 64, 64)
+    y = torch.randint(0, 10, (2,))
+    cdp.CrossEntropyLoss()(model(x.cuda()), y.cuda()).backward()
+    torch.nn.functional.cross_entropy(ref(x.double()), y).backward()
+    for (n, p), pr in zip(model.named_parameters(), ref.parameters()):
+        err = ((p.grad.double().cpu() - pr.grad).norm() / pr.grad.norm().clamp_min(1e-30)).item()
+        assert err < 1e-4, (n, err)
+
+
 def test_graph_capture_training_step():
     """A whole training step (augment, fwd, bwd, SGD) captured in a hipGraph replays correctly."""
     import cs744_distributed_data_parallel_amd as cdp
