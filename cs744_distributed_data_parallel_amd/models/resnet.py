@@ -34,10 +34,12 @@ class BasicBlock(nn.Module):
 
     def forward(self, x):
         if CF.use_native(x):
-            sink = CF.GradSink() if self.downsample is None and x.requires_grad else None
+            sink = CF.GradSink.make(x)
             out = CF.conv_bn_act(x, self.conv1, self.bn1, relu=True, dx_sink=sink)
-            idt = x if self.downsample is None else CF.conv_bn_act(x, self.downsample[0], self.downsample[1], relu=False)
-            return CF.conv_bn_act(out, self.conv2, self.bn2, relu=True, residual=idt, res_sink=sink)
+            if self.downsample is None:
+                return CF.conv_bn_act(out, self.conv2, self.bn2, relu=True, residual=x, res_sink=sink)
+            idt = CF.conv_bn_act(x, self.downsample[0], self.downsample[1], relu=False, dx_sink=sink)
+            return CF.conv_bn_act(out, self.conv2, self.bn2, relu=True, residual=idt)
         idt = x if self.downsample is None else self.downsample(x)
         out = self.relu(self.bn1(self.conv1(x)))
         out = self.bn2(self.conv2(out))
@@ -62,12 +64,15 @@ class Bottleneck(nn.Module):
 
     def forward(self, x):
         if CF.use_native(x):
-            # identity blocks: the residual gradient is summed inside conv1's data-gradient GEMM
-            sink = CF.GradSink() if self.downsample is None and x.requires_grad else None
+            # x's two gradients (conv1 + residual, or conv1 + downsample) are summed inside a
+            # data-gradient GEMM epilogue instead of an autograd add (GradSink)
+            sink = CF.GradSink.make(x)
             out = CF.conv_bn_act(x, self.conv1, self.bn1, relu=True, dx_sink=sink)
             out = CF.conv_bn_act(out, self.conv2, self.bn2, relu=True)
-            idt = x if self.downsample is None else CF.conv_bn_act(x, self.downsample[0], self.downsample[1], relu=False)
-            return CF.conv_bn_act(out, self.conv3, self.bn3, relu=True, residual=idt, res_sink=sink)
+            if self.downsample is None:
+                return CF.conv_bn_act(out, self.conv3, self.bn3, relu=True, residual=x, res_sink=sink)
+            idt = CF.conv_bn_act(x, self.downsample[0], self.downsample[1], relu=False, dx_sink=sink)
+            return CF.conv_bn_act(out, self.conv3, self.bn3, relu=True, residual=idt)
         idt = x if self.downsample is None else self.downsample(x)
         out = self.relu(self.bn1(self.conv1(x)))
         out = self.relu(self.bn2(self.conv2(out)))

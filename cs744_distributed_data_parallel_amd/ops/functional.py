@@ -47,19 +47,29 @@ def _bn_momentum(bn) -> float:
 
 # --------------------------------------------------------------------------- conv + BN + act
 class GradSink:
-    """Hands a residual-branch gradient from a block's last fused op to its first one.
+    """Sums the two gradients of a tensor consumed by two fused ops without an autograd add.
 
-    In a ResNet identity block the block input x feeds both conv1 and the residual add of conv3,
-    so autograd would sum two full-size gradients with a separate add kernel. With a sink, conv3's
-    backward parks the residual gradient here instead of returning it, and conv1's data-gradient
-    GEMM accumulates onto it in its epilogue (writing the sum in place). conv1's backward always
-    runs after conv3's: it needs conv2's output gradient, which needs conv3's.
+    A ResNet block input x feeds conv1 and either the residual add of the last conv (identity
+    block) or the downsample conv, so autograd would sum two full-size gradients with a separate
+    add kernel. Both consumers share a sink: whichever backward runs first parks its gradient here
+    and returns None for x; the second one accumulates the parked gradient into its own result --
+    inside its data-gradient GEMM's epilogue when it is a conv -- and returns the sum. The result
+    does not depend on the order in which autograd runs the two.
     """
 
     __slots__ = ("grad",)
 
     def __init__(self):
         self.grad = None
+
+    @staticmethod
+    def make(x):
+        """A sink for ``x`` (None when x needs no gradient or CDP_GRAD_SINK=0)."""
+        import os
+
+        if not x.requires_grad or os.environ.get("CDP_GRAD_SINK", "1") == "0":
+            return None
+        return GradSink()
 
 
 class _ConvBNAct(torch.autograd.Function):
@@ -85,17 +95,26 @@ class _ConvBNAct(torch.autograd.Function):
         C = _native.lib()
         wp, bp, gp, betap = ctx.params
         nig = ctx.needs_input_grad
-        addend = None
+        addend, park_dx = None, False
         if dx_sink is not None and nig[0]:
-            addend, dx_sink.grad = dx_sink.grad, None
+            if dx_sink.grad is None:
+                park_dx = True
+            else:
+                addend, dx_sink.grad = dx_sink.grad, None
         dx, dw, db, dgamma, dbeta, dres = C.conv_bn_act_bwd(
             gout, x, w, y, stats, stride, pad, pool, relu, nig[0], has_bias, zout, training,
             _slot(wp, nig[1]), _slot(bp, nig[2] and has_bias), _slot(gp, nig[3]), _slot(betap, nig[4]), addend,
         )
-        if has_res and res_sink is not None:
-            res_sink.grad, dres = dres, None
+        if park_dx:
+            dx_sink.grad, dx = dx, None
+        if has_res and res_sink is not None and nig[15]:
+            if res_sink.grad is None:
+                res_sink.grad, dres = dres, None
+            else:
+                dres = dres.add_(res_sink.grad)
+                res_sink.grad = None
         return (
-            dx if ctx.needs_input_grad[0] else None,
+            dx if ctx.needs_input_grad[0] else None,  # None also when parked in dx_sink
             dw,
             db if has_bias else None,
             dgamma if ctx.needs_input_grad[3] else None,

@@ -46,6 +46,22 @@ __device__ __forceinline__ void conv_epilogue(const ConvGemmParams& p,
     return;
   }
 
+  if (p.addend) {  // y += addend (may alias y): every load is issued before any store
+#pragma unroll
+    for (int a = 0; a < TM; ++a)
+#pragma unroll
+      for (int b = 0; b < TN; ++b) {
+        const int n = n0 + wn * (BN / 2) + b * 32 + l32;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int m = m0 + wm * (BM / WM) + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
+          // branch-free (clamped address + select) so all loads issue before the first wait
+          const bool ok = m < p.M && n < p.Nout;
+          const float av = p.addend[ok ? remap_row(p.rr, m) * p.Nout + n : 0];
+          acc[a][b][r] += ok ? av : 0.f;
+        }
+      }
+  }
   float bias_v[TN];
 #pragma unroll
   for (int b = 0; b < TN; ++b) {
@@ -60,13 +76,9 @@ __device__ __forceinline__ void conv_epilogue(const ConvGemmParams& p,
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int m = m0 + wm * (BM / WM) + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
-        float v = acc[a][b][r] + bias_v[b];
-        if (m < p.M && n < p.Nout) {
-          const long long o = remap_row(p.rr, m) * p.Nout + n;
-          if (p.addend) v += p.addend[o];
-          p.y[o] = v;
-        }
+        const float v = acc[a][b][r] + bias_v[b];
         acc[a][b][r] = v;
+        if (m < p.M && n < p.Nout) p.y[remap_row(p.rr, m) * p.Nout + n] = v;
       }
     }
   if (!p.part) return;
@@ -170,6 +182,22 @@ __device__ __forceinline__ void conv_epilogue16(const ConvGemmParams& p,
       }
     return;
   }
+  if (p.addend) {  // y += addend (may alias y): every load is issued before any store
+#pragma unroll
+    for (int a = 0; a < TM; ++a)
+#pragma unroll
+      for (int b = 0; b < TN; ++b) {
+        const int n = col_of(b);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int m = row_of(a, r);
+          // branch-free (clamped address + select) so all loads issue before the first wait
+          const bool ok = m < p.M && n < p.Nout;
+          const float av = p.addend[ok ? remap_row(p.rr, m) * p.Nout + n : 0];
+          acc[a][b][r] += ok ? av : 0.f;
+        }
+      }
+  }
   float bias_v[TN];
 #pragma unroll
   for (int b = 0; b < TN; ++b) {
@@ -184,13 +212,9 @@ __device__ __forceinline__ void conv_epilogue16(const ConvGemmParams& p,
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int m = row_of(a, r);
-        float v = acc[a][b][r] + bias_v[b];
-        if (m < p.M && n < p.Nout) {
-          const long long o = remap_row(p.rr, m) * p.Nout + n;
-          if (p.addend) v += p.addend[o];
-          p.y[o] = v;
-        }
+        const float v = acc[a][b][r] + bias_v[b];
         acc[a][b][r] = v;
+        if (m < p.M && n < p.Nout) p.y[remap_row(p.rr, m) * p.Nout + n] = v;
       }
     }
   if (!p.part) return;
