@@ -9,6 +9,8 @@
 // (mean_b, M2_b per column, two exact passes over the registers) so the following
 // BatchNorm never re-reads the conv output for its statistics.
 #pragma once
+#include <type_traits>
+
 #include "common.h"
 #include "kernels.h"
 
@@ -30,19 +32,25 @@ __device__ __forceinline__ void conv_epilogue(const ConvGemmParams& p,
   const int wm = wid >> 1, wn = wid & 1;
   const int l32 = lane & 31;
   const int hh = lane >> 5;
+  // whole tile in bounds (the common case): unpredicated stores, no per-element exec branches
+  const bool full = m0 + BM <= p.M && n0 + BN <= p.Nout;
   if (p.splits > 1) {
     float* out = p.y + (long long)split * p.M * p.Nout;
+    auto slab_store = [&](auto pred) {
 #pragma unroll
-    for (int a = 0; a < TM; ++a)
+      for (int a = 0; a < TM; ++a)
 #pragma unroll
-      for (int b = 0; b < TN; ++b) {
-        const int n = n0 + wn * (BN / 2) + b * 32 + l32;
+        for (int b = 0; b < TN; ++b) {
+          const int n = n0 + wn * (BN / 2) + b * 32 + l32;
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int m = m0 + wm * (BM / WM) + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
-          if (m < p.M && n < p.Nout) out[(long long)m * p.Nout + n] = acc[a][b][r];
+          for (int r = 0; r < 16; ++r) {
+            const int m = m0 + wm * (BM / WM) + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
+            if (!decltype(pred)::value || (m < p.M && n < p.Nout)) out[(long long)m * p.Nout + n] = acc[a][b][r];
+          }
         }
-      }
+    };
+    if (full) slab_store(std::false_type{});
+    else slab_store(std::true_type{});
     return;
   }
 
@@ -68,19 +76,23 @@ __device__ __forceinline__ void conv_epilogue(const ConvGemmParams& p,
     const int n = n0 + wn * (BN / 2) + b * 32 + l32;
     bias_v[b] = (p.bias && n < p.Nout) ? p.bias[n] : 0.f;
   }
+  auto out_store = [&](auto pred) {
 #pragma unroll
-  for (int a = 0; a < TM; ++a)
+    for (int a = 0; a < TM; ++a)
 #pragma unroll
-    for (int b = 0; b < TN; ++b) {
-      const int n = n0 + wn * (BN / 2) + b * 32 + l32;
+      for (int b = 0; b < TN; ++b) {
+        const int n = n0 + wn * (BN / 2) + b * 32 + l32;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int m = m0 + wm * (BM / WM) + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
-        const float v = acc[a][b][r] + bias_v[b];
-        acc[a][b][r] = v;
-        if (m < p.M && n < p.Nout) p.y[remap_row(p.rr, m) * p.Nout + n] = v;
+        for (int r = 0; r < 16; ++r) {
+          const int m = m0 + wm * (BM / WM) + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
+          const float v = acc[a][b][r] + bias_v[b];
+          acc[a][b][r] = v;
+          if (!decltype(pred)::value || (m < p.M && n < p.Nout)) p.y[remap_row(p.rr, m) * p.Nout + n] = v;
+        }
       }
-    }
+  };
+  if (full) out_store(std::false_type{});
+  else out_store(std::true_type{});
   if (!p.part) return;
 
   __syncthreads();  // `red` aliases the operand LDS
@@ -167,19 +179,24 @@ __device__ __forceinline__ void conv_epilogue16(const ConvGemmParams& p,
   const int q4 = (lane >> 4) * 4;
   auto row_of = [&](int a, int r) { return m0 + wm * (BM / WM) + a * 16 + q4 + r; };
   auto col_of = [&](int b) { return n0 + wn * (BN / 2) + b * 16 + l16; };
+  const bool full = m0 + BM <= p.M && n0 + BN <= p.Nout;
   if (p.splits > 1) {
     float* out = p.y + (long long)split * p.M * p.Nout;
+    auto slab_store = [&](auto pred) {
 #pragma unroll
-    for (int a = 0; a < TM; ++a)
+      for (int a = 0; a < TM; ++a)
 #pragma unroll
-      for (int b = 0; b < TN; ++b) {
-        const int n = col_of(b);
+        for (int b = 0; b < TN; ++b) {
+          const int n = col_of(b);
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int m = row_of(a, r);
-          if (m < p.M && n < p.Nout) out[(long long)m * p.Nout + n] = acc[a][b][r];
+          for (int r = 0; r < 4; ++r) {
+            const int m = row_of(a, r);
+            if (!decltype(pred)::value || (m < p.M && n < p.Nout)) out[(long long)m * p.Nout + n] = acc[a][b][r];
+          }
         }
-      }
+    };
+    if (full) slab_store(std::false_type{});
+    else slab_store(std::true_type{});
     return;
   }
   if (p.addend) {  // y += addend (may alias y): every load is issued before any store
@@ -204,19 +221,23 @@ __device__ __forceinline__ void conv_epilogue16(const ConvGemmParams& p,
     const int n = col_of(b);
     bias_v[b] = (p.bias && n < p.Nout) ? p.bias[n] : 0.f;
   }
+  auto out_store = [&](auto pred) {
 #pragma unroll
-  for (int a = 0; a < TM; ++a)
+    for (int a = 0; a < TM; ++a)
 #pragma unroll
-    for (int b = 0; b < TN; ++b) {
-      const int n = col_of(b);
+      for (int b = 0; b < TN; ++b) {
+        const int n = col_of(b);
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int m = row_of(a, r);
-        const float v = acc[a][b][r] + bias_v[b];
-        acc[a][b][r] = v;
-        if (m < p.M && n < p.Nout) p.y[remap_row(p.rr, m) * p.Nout + n] = v;
+        for (int r = 0; r < 4; ++r) {
+          const int m = row_of(a, r);
+          const float v = acc[a][b][r] + bias_v[b];
+          acc[a][b][r] = v;
+          if (!decltype(pred)::value || (m < p.M && n < p.Nout)) p.y[remap_row(p.rr, m) * p.Nout + n] = v;
+        }
       }
-    }
+  };
+  if (full) out_store(std::false_type{});
+  else out_store(std::true_type{});
   if (!p.part) return;
 
   __syncthreads();  // `red` aliases the operand LDS

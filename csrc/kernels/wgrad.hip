@@ -11,6 +11,8 @@
 // m-major ([m][co] and [m][k]) exactly as they sit in memory, so no transpose is needed: an MFMA
 // operand lane (i, h) reads row m = 2s + h, column i -- 32 consecutive floats per half-wave,
 // conflict-free ds_read_b32.
+#include <type_traits>
+
 #include "common.h"
 #include "kernels.h"
 #include "x3_common.h"
@@ -154,17 +156,22 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(WgradParams p) {
   }
 
   float* out = p.out + (long long)split * p.Cout * p.Kdim;
+  const bool full = co0 + BM <= p.Cout && r0 + BN <= p.Kdim;
+  auto store = [&](auto pred) {  // unpredicated stores for in-bounds tiles
 #pragma unroll
-  for (int a = 0; a < TM; ++a)
+    for (int a = 0; a < TM; ++a)
 #pragma unroll
-    for (int b = 0; b < TN; ++b) {
-      const int k = r0 + wn * (BN / 2) + b * 32 + l32;
+      for (int b = 0; b < TN; ++b) {
+        const int k = r0 + wn * (BN / 2) + b * 32 + l32;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int c = co0 + wm * (BM / 2) + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
-        if (c < p.Cout && k < p.Kdim) out[(long long)c * p.Kdim + k] = acc[a][b][r];
+        for (int r = 0; r < 16; ++r) {
+          const int c = co0 + wm * (BM / 2) + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
+          if (!decltype(pred)::value || (c < p.Cout && k < p.Kdim)) out[(long long)c * p.Kdim + k] = acc[a][b][r];
+        }
       }
-    }
+  };
+  if (full) store(std::false_type{});
+  else store(std::true_type{});
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -369,17 +376,22 @@ __global__ __launch_bounds__(256, 2) void wgrad_x3_kernel(WgradParams p) {
   }
 
   float* out = p.out + (long long)split * p.Cout * p.Kdim;
+  const bool full = co0 + BM <= p.Cout && r0 + BN <= p.Kdim;
+  auto store = [&](auto pred) {  // unpredicated stores for in-bounds tiles
 #pragma unroll
-  for (int a = 0; a < TM; ++a)
+    for (int a = 0; a < TM; ++a)
 #pragma unroll
-    for (int b = 0; b < TN; ++b) {
-      const int k = r0 + wn * (BN / 2) + b * 32 + l32;
+      for (int b = 0; b < TN; ++b) {
+        const int k = r0 + wn * (BN / 2) + b * 32 + l32;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int c = co0 + wm * (BM / 2) + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
-        if (c < p.Cout && k < p.Kdim) out[(long long)c * p.Kdim + k] = acc[a][b][r];
+        for (int r = 0; r < 16; ++r) {
+          const int c = co0 + wm * (BM / 2) + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
+          if (!decltype(pred)::value || (c < p.Cout && k < p.Kdim)) out[(long long)c * p.Kdim + k] = acc[a][b][r];
+        }
       }
-    }
+  };
+  if (full) store(std::false_type{});
+  else store(std::true_type{});
 }
 
 // dst[r][c] = (accumulate ? dst : 0) + sum_z slab[z][r][c]  over rows x src_cols, keeping the first
