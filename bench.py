@@ -43,6 +43,10 @@ def parse():
                         "B=256/GPU the step is GPU-bound, eager and graph time within noise)")
     p.add_argument("--backend", default="native", choices=["native", "torch"],
                    help="torch = stock PyTorch-ROCm ops + torch DDP (comparison only)")
+    p.add_argument("--precision", default="fp32", choices=["fp32", "bf16"],
+                   help="fp32 (default, the reference's precision; conv GEMMs fp32-accurate via the 3-term "
+                        "bf16 split) or bf16 (conv GEMM operands rounded to bf16, fp32 accumulation: "
+                        "the non-parity fast mode)")
     p.add_argument("--bucket-cap-mb", type=float, default=None)
     p.add_argument("--dataset-size", type=int, default=50000)
     return p.parse_args()
@@ -84,6 +88,8 @@ def main():
                                 comm_timeout_s=300.0)
     if args.backend == "native":
         cdp._native.lib()  # fail loudly if the HIP extension is missing
+        if args.precision == "bf16":
+            cdp._native.lib().set_conv_gemm("bf16")
 
     local_batch = args.local_batch if args.scaling == "weak" else max(1, 256 // world)
     global_batch = local_batch * world
@@ -210,7 +216,7 @@ def main():
             "higher_is_better": True,
             "scaling": args.scaling,
             "vs_baseline": None if imagenet else round(img_s / BASELINE_IMG_S, 2),
-            "dtype": "fp32",
+            "dtype": "fp32" if args.precision == "fp32" else "bf16",
             "data": ("synthetic (random uint8 ImageNet-shaped 224x224x3, GPU-resident, on-GPU flip/normalize); "
                      if imagenet else
                      "synthetic (random uint8 CIFAR-10-shaped 32x32x3, GPU-resident, on-GPU crop/flip/normalize); ")

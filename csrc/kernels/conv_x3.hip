@@ -56,9 +56,20 @@ __device__ __forceinline__ void split8(const float (&v)[8], u32x4& s0, u32x4& s1
 // PS (pre-split): p.x / p.w hold three bf16 planes each ([3][N][H][W][C], [3][Nout][Kdim], as
 // written by split3_launch) and the tiles are copied to LDS without the split (MODE 0 only).
 // ABL (diagnostic builds only): bit 0 drops the in-loop global loads, bit 1 the in-loop LDS stores
-template <int BM, int BN, int MODE, bool DGRAD, bool M16, bool PS = false, int ABL = 0>
+// NP = bf16 planes per operand: 3 = fp32-accurate split (six products), 1 = plain bf16 operands
+// with fp32 accumulation (one product; the non-parity fast mode, CDP_CONV_GEMM=bf16).
+// 8 consecutive-k fp32 values rounded to bf16 (one plane)
+__device__ __forceinline__ u32x4 pack8(const float (&v)[8]) {
+  u32x4 r;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) r[j] = pack_bf16x2(f32x2{v[2 * j], v[2 * j + 1]});
+  return r;
+}
+
+template <int BM, int BN, int MODE, bool DGRAD, bool M16, bool PS = false, int ABL = 0, int NP = 3>
 __global__ __launch_bounds__(waves_m<BM>() * 128, (BM + BN >= 256) ? 1 : 2) void conv_x3_kernel(ConvGemmParams p) {
   static_assert(!PS || MODE == 0, "pre-split operands need C % 32 == 0");
+  static_assert(NP == 3 || (NP == 1 && !PS), "planes");
   constexpr unsigned ES = PS ? 1u : 2u;  // log2 bytes per element of the global operands
   constexpr int WM = waves_m<BM>();  // waves along M (2 x WM waves)
   constexpr int NT = WM * 128;       // threads
@@ -69,7 +80,7 @@ __global__ __launch_bounds__(waves_m<BM>() * 128, (BM + BN >= 256) ? 1 : 2) void
   constexpr int B_LD = BN / RS;
   static_assert(A_LD >= 1 && B_LD >= 1, "tile too narrow for the loader");
   constexpr int PA = BM * LDH, PB = BN * LDH;
-  constexpr int STAGE = 3 * (PA + PB);  // bf16 per stage: A planes [3][BM][LDH], B planes [3][BN][LDH]
+  constexpr int STAGE = NP * (PA + PB);  // bf16 per stage: A planes [NP][BM][LDH], B planes [NP][BN][LDH]
   static_assert(2 * STAGE * 2 >= 2 * BN * 4, "epilogue scratch");
   __shared__ __attribute__((aligned(16))) __bf16 smem[2 * STAGE];
 
@@ -253,28 +264,36 @@ __global__ __launch_bounds__(waves_m<BM>() * 128, (BM + BN >= 256) ? 1 : 2) void
       }
 #pragma unroll
       for (int i = 0; i < B_LD; ++i) {
-        __bf16* d = st + 3 * PA + (rrow + RS * i) * LDH + cp;
+        __bf16* d = st + NP * PA + (rrow + RS * i) * LDH + cp;
 #pragma unroll
         for (int q = 0; q < 3; ++q) *reinterpret_cast<u32x4*>(d + q * PB) = vb[i][q];
       }
     } else {
 #pragma unroll
     for (int i = 0; i < A_LD; ++i) {
-      u32x4 s0, s1, s2;
-      split8(va[i], s0, s1, s2);
       __bf16* d = st + (rrow + RS * i) * LDH + cp;
-      *reinterpret_cast<u32x4*>(d) = s0;
-      *reinterpret_cast<u32x4*>(d + PA) = s1;
-      *reinterpret_cast<u32x4*>(d + 2 * PA) = s2;
+      if constexpr (NP == 1) {
+        *reinterpret_cast<u32x4*>(d) = pack8(va[i]);
+      } else {
+        u32x4 s0, s1, s2;
+        split8(va[i], s0, s1, s2);
+        *reinterpret_cast<u32x4*>(d) = s0;
+        *reinterpret_cast<u32x4*>(d + PA) = s1;
+        *reinterpret_cast<u32x4*>(d + 2 * PA) = s2;
+      }
     }
 #pragma unroll
     for (int i = 0; i < B_LD; ++i) {
-      u32x4 s0, s1, s2;
-      split8(vb[i], s0, s1, s2);
-      __bf16* d = st + 3 * PA + (rrow + RS * i) * LDH + cp;
-      *reinterpret_cast<u32x4*>(d) = s0;
-      *reinterpret_cast<u32x4*>(d + PB) = s1;
-      *reinterpret_cast<u32x4*>(d + 2 * PB) = s2;
+      __bf16* d = st + NP * PA + (rrow + RS * i) * LDH + cp;
+      if constexpr (NP == 1) {
+        *reinterpret_cast<u32x4*>(d) = pack8(vb[i]);
+      } else {
+        u32x4 s0, s1, s2;
+        split8(vb[i], s0, s1, s2);
+        *reinterpret_cast<u32x4*>(d) = s0;
+        *reinterpret_cast<u32x4*>(d + PB) = s1;
+        *reinterpret_cast<u32x4*>(d + 2 * PB) = s2;
+      }
     }
     }
   };
@@ -308,9 +327,9 @@ __global__ __launch_bounds__(waves_m<BM>() * 128, (BM + BN >= 256) ? 1 : 2) void
 #pragma unroll
       for (int b = 0; b < 2 * TN; ++b) {
         const int r = wn * (BN / 2) + b * 16 + l16;
-        const __bf16* src = st + 3 * PA + r * LDH + chunk_pos(r, ch) * 8;
+        const __bf16* src = st + NP * PA + r * LDH + chunk_pos(r, ch) * 8;
 #pragma unroll
-        for (int q = 0; q < 3; ++q) bf[b][q] = *reinterpret_cast<const bf16x8*>(src + q * PB);
+        for (int q = 0; q < NP; ++q) bf[b][q] = *reinterpret_cast<const bf16x8*>(src + q * PB);
       }
 #pragma unroll
       for (int a = 0; a < 2 * TM; ++a) {
@@ -318,10 +337,14 @@ __global__ __launch_bounds__(waves_m<BM>() * 128, (BM + BN >= 256) ? 1 : 2) void
         const int r = wm * (BM / WM) + a * 16 + l16;
         const __bf16* src = st + r * LDH + chunk_pos(r, ch) * 8;
 #pragma unroll
-        for (int q = 0; q < 3; ++q) af[q] = *reinterpret_cast<const bf16x8*>(src + q * PA);
+        for (int q = 0; q < NP; ++q) af[q] = *reinterpret_cast<const bf16x8*>(src + q * PA);
 #pragma unroll
         for (int b = 0; b < 2 * TN; ++b) {
           f32x4 c = acc16[a][b];
+          if constexpr (NP == 1) {
+            acc16[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[0], bf[b][0], c, 0, 0, 0);
+            continue;
+          }
           c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[2], bf[b][0], c, 0, 0, 0);
           c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[1], bf[b][1], c, 0, 0, 0);
           c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[0], bf[b][2], c, 0, 0, 0);
@@ -340,20 +363,24 @@ __global__ __launch_bounds__(waves_m<BM>() * 128, (BM + BN >= 256) ? 1 : 2) void
           const int r = wm * (BM / WM) + a * 32 + l32;
           const __bf16* src = st + r * LDH + chunk_pos(r, 2 * s + hh) * 8;
 #pragma unroll
-          for (int q = 0; q < 3; ++q) af[a][q] = *reinterpret_cast<const bf16x8*>(src + q * PA);
+          for (int q = 0; q < NP; ++q) af[a][q] = *reinterpret_cast<const bf16x8*>(src + q * PA);
         }
 #pragma unroll
         for (int b = 0; b < TN; ++b) {
           const int r = wn * (BN / 2) + b * 32 + l32;
-          const __bf16* src = st + 3 * PA + r * LDH + chunk_pos(r, 2 * s + hh) * 8;
+          const __bf16* src = st + NP * PA + r * LDH + chunk_pos(r, 2 * s + hh) * 8;
 #pragma unroll
-          for (int q = 0; q < 3; ++q) bf[b][q] = *reinterpret_cast<const bf16x8*>(src + q * PB);
+          for (int q = 0; q < NP; ++q) bf[b][q] = *reinterpret_cast<const bf16x8*>(src + q * PB);
         }
 #pragma unroll
         for (int a = 0; a < TM; ++a)
 #pragma unroll
           for (int b = 0; b < TN; ++b) {
             f32x16 c = acc[a][b];
+            if constexpr (NP == 1) {
+              acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[a][0], bf[b][0], c, 0, 0, 0);
+              continue;
+            }
             c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[a][2], bf[b][0], c, 0, 0, 0);
             c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[a][1], bf[b][1], c, 0, 0, 0);
             c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[a][0], bf[b][2], c, 0, 0, 0);
@@ -395,21 +422,22 @@ __global__ __launch_bounds__(waves_m<BM>() * 128, (BM + BN >= 256) ? 1 : 2) void
 }
 
 template <int BM, int BN, int MODE, bool DGRAD>
-void launch_x3(const ConvGemmParams& p, int ntiles, bool m16, hipStream_t st) {
-  const dim3 blk(waves_m<BM>() * 128);
-  if (m16) hipLaunchKernelGGL((conv_x3_kernel<BM, BN, MODE, DGRAD, true>), dim3(ntiles * p.splits), blk, 0, st, p);
-  else hipLaunchKernelGGL((conv_x3_kernel<BM, BN, MODE, DGRAD, false>), dim3(ntiles * p.splits), blk, 0, st, p);
+void launch_x3(const ConvGemmParams& p, int ntiles, bool m16, bool bf16, hipStream_t st) {
+  const dim3 blk(waves_m<BM>() * 128), grd(ntiles * p.splits);
+  if (bf16) hipLaunchKernelGGL((conv_x3_kernel<BM, BN, MODE, DGRAD, false, false, 0, 1>), grd, blk, 0, st, p);
+  else if (m16) hipLaunchKernelGGL((conv_x3_kernel<BM, BN, MODE, DGRAD, true>), grd, blk, 0, st, p);
+  else hipLaunchKernelGGL((conv_x3_kernel<BM, BN, MODE, DGRAD, false>), grd, blk, 0, st, p);
 }
 
 template <int MODE, bool DGRAD>
-void dispatch_x3(const ConvGemmParams& p, int bm, int bn, bool m16, hipStream_t st) {
+void dispatch_x3(const ConvGemmParams& p, int bm, int bn, bool m16, bool bf16, hipStream_t st) {
   const int ntm = (p.M + bm - 1) / bm, ntn = (p.Nout + bn - 1) / bn;
   const int nt = ntm * ntn;
-  if (bm == 256) launch_x3<256, 128, MODE, DGRAD>(p, nt, m16, st);
-  else if (bm == 128 && bn == 128) launch_x3<128, 128, MODE, DGRAD>(p, nt, m16, st);
-  else if (bm == 128 && bn == 64) launch_x3<128, 64, MODE, DGRAD>(p, nt, m16, st);
-  else if (bm == 64 && bn == 128) launch_x3<64, 128, MODE, DGRAD>(p, nt, m16, st);
-  else launch_x3<64, 64, MODE, DGRAD>(p, nt, m16, st);
+  if (bm == 256) launch_x3<256, 128, MODE, DGRAD>(p, nt, m16, bf16, st);
+  else if (bm == 128 && bn == 128) launch_x3<128, 128, MODE, DGRAD>(p, nt, m16, bf16, st);
+  else if (bm == 128 && bn == 64) launch_x3<128, 64, MODE, DGRAD>(p, nt, m16, bf16, st);
+  else if (bm == 64 && bn == 128) launch_x3<64, 128, MODE, DGRAD>(p, nt, m16, bf16, st);
+  else launch_x3<64, 64, MODE, DGRAD>(p, nt, m16, bf16, st);
 }
 
 template <int BM, int BN, bool DGRAD>
@@ -448,16 +476,16 @@ void conv_x3ps_launch(const ConvGemmParams& p, int bm, int bn, bool dgrad, hipSt
   else dgrad ? launch_x3ps<64, 64, true>(p, nt, st) : launch_x3ps<64, 64, false>(p, nt, st);
 }
 
-void conv_x3_launch(const ConvGemmParams& p, int bm, int bn, bool dgrad, bool m16, hipStream_t st) {
+void conv_x3_launch(const ConvGemmParams& p, int bm, int bn, bool dgrad, bool m16, hipStream_t st, bool bf16) {
   if ((p.C % BK) == 0 && (p.Kdim % BK) == 0) {
-    if (dgrad) dispatch_x3<0, true>(p, bm, bn, m16, st);
-    else dispatch_x3<0, false>(p, bm, bn, m16, st);
+    if (dgrad) dispatch_x3<0, true>(p, bm, bn, m16, bf16, st);
+    else dispatch_x3<0, false>(p, bm, bn, m16, bf16, st);
   } else if ((p.C % 4) == 0 && (p.Kdim % 4) == 0) {
-    if (dgrad) dispatch_x3<1, true>(p, bm, bn, m16, st);
-    else dispatch_x3<1, false>(p, bm, bn, m16, st);
+    if (dgrad) dispatch_x3<1, true>(p, bm, bn, m16, bf16, st);
+    else dispatch_x3<1, false>(p, bm, bn, m16, bf16, st);
   } else {
-    if (dgrad) dispatch_x3<2, true>(p, bm, bn, m16, st);
-    else dispatch_x3<2, false>(p, bm, bn, m16, st);
+    if (dgrad) dispatch_x3<2, true>(p, bm, bn, m16, bf16, st);
+    else dispatch_x3<2, false>(p, bm, bn, m16, bf16, st);
   }
 }
 

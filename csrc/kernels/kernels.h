@@ -78,7 +78,9 @@ struct WgradParams {
 void conv_igemm_launch(const ConvGemmParams& p, int bm, int bn, bool dgrad, hipStream_t st);
 // conv_x3.hip (fp32-accurate 3-term bf16 split on the bf16 MFMA)
 // (m16: v_mfma_f32_16x16x32_bf16 tiles instead of 32x32x16)
-void conv_x3_launch(const ConvGemmParams& p, int bm, int bn, bool dgrad, bool m16, hipStream_t st);
+// (bf16: operands rounded to bf16, one product per MAC -- the non-parity fast mode)
+void conv_x3_launch(const ConvGemmParams& p, int bm, int bn, bool dgrad, bool m16, hipStream_t st,
+                    bool bf16 = false);
 // pre-split operands (x, w = three bf16 planes each, from split3_launch); C % 32 == 0 only
 void conv_x3ps_launch(const ConvGemmParams& p, int bm, int bn, bool dgrad, hipStream_t st);
 void split3_launch(const float* x, long long n, void* planes, hipStream_t st);
@@ -89,7 +91,7 @@ int splitk_rows_per_part();
 
 // wgrad.hip
 // x3: fp32-accurate 3-term bf16 split on the bf16 MFMA; otherwise the exact fp32-input MFMA
-void wgrad_launch(const WgradParams& p, int bm, int bn, bool x3, hipStream_t st);
+void wgrad_launch(const WgradParams& p, int bm, int bn, bool x3, hipStream_t st, bool bf16 = false);
 void slab_sum_launch(const float* slab, int S, long long n, float* dst, bool accumulate, hipStream_t st);
 void slab_sum_strided_launch(const float* slab, int S, long long n_src, int src_cols, int dst_cols, float* dst,
                              bool accumulate, hipStream_t st);

@@ -187,7 +187,7 @@ constexpr int XLD = WBK + 8;  // bf16 per LDS row
 
 // v[r] = row m+r of this thread's 4 columns; write, per column and plane, the RPT m-values
 // (packed bf16 pairs) into the [col][m] image at dst.
-template <int RPT>
+template <int RPT, int NP>
 __device__ __forceinline__ void split_store_cols(const float4 (&v)[RPT], __bf16* dst, int plane) {
   // (component access by constant index only: a pointer walk over `v` makes the compiler
   // promote the register array to LDS scratch)
@@ -196,10 +196,15 @@ __device__ __forceinline__ void split_store_cols(const float4 (&v)[RPT], __bf16*
   for (int c = 0; c < 4; ++c) {
     unsigned h0[RPT / 2], h1[RPT / 2], h2[RPT / 2];
 #pragma unroll
-    for (int r = 0; r < RPT / 2; ++r)
-      split_pair(comp(v[2 * r], c), comp(v[2 * r + 1], c), h0[r], h1[r], h2[r]);
+    for (int r = 0; r < RPT / 2; ++r) {
+      if constexpr (NP == 1) h0[r] = pack_bf16x2(f32x2{comp(v[2 * r], c), comp(v[2 * r + 1], c)});
+      else split_pair(comp(v[2 * r], c), comp(v[2 * r + 1], c), h0[r], h1[r], h2[r]);
+    }
     __bf16* d = dst + c * XLD;
-    if constexpr (RPT == 4) {
+    if constexpr (NP == 1) {
+      if constexpr (RPT == 4) *reinterpret_cast<uint2*>(d) = make_uint2(h0[0], h0[1]);
+      else *reinterpret_cast<unsigned*>(d) = h0[0];
+    } else if constexpr (RPT == 4) {
       *reinterpret_cast<uint2*>(d) = make_uint2(h0[0], h0[1]);
       *reinterpret_cast<uint2*>(d + plane) = make_uint2(h1[0], h1[1]);
       *reinterpret_cast<uint2*>(d + 2 * plane) = make_uint2(h2[0], h2[1]);
@@ -211,15 +216,15 @@ __device__ __forceinline__ void split_store_cols(const float4 (&v)[RPT], __bf16*
   }
 }
 
-template <int BM, int BN, bool FAST>
+template <int BM, int BN, bool FAST, int NP = 3>  // NP = 1: plain bf16 operands (non-parity mode)
 __global__ __launch_bounds__(256, 2) void wgrad_x3_kernel(WgradParams p) {
   constexpr int TM = BM / 64, TN = BN / 64;
   constexpr int PA = BM * XLD, PB = BN * XLD;
   constexpr int RPT_A = BM / 32, RPT_B = BN / 32;  // m rows per thread (4 for 128-wide, 2 for 64)
   constexpr int MQ_A = WBK / RPT_A, MQ_B = WBK / RPT_B;  // m groups per tile (8 or 16)
-  __shared__ __attribute__((aligned(16))) __bf16 smem[3 * (PA + PB)];
+  __shared__ __attribute__((aligned(16))) __bf16 smem[NP * (PA + PB)];
   __bf16* As = smem;
-  __bf16* Bs = smem + 3 * PA;
+  __bf16* Bs = smem + NP * PA;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid >> 1, wn = wid & 1;
 
@@ -317,8 +322,8 @@ __global__ __launch_bounds__(256, 2) void wgrad_x3_kernel(WgradParams p) {
     }
   };
   auto store_tile = [&]() {
-    split_store_cols<RPT_A>(ra, As + (a_cg * 4) * XLD + a_mq * RPT_A, PA);
-    split_store_cols<RPT_B>(rb, Bs + (b_cg * 4) * XLD + b_mq * RPT_B, PB);
+    split_store_cols<RPT_A, NP>(ra, As + (a_cg * 4) * XLD + a_mq * RPT_A, PA);
+    split_store_cols<RPT_B, NP>(rb, Bs + (b_cg * 4) * XLD + b_mq * RPT_B, PB);
   };
 
   f32x16 acc[TM][TN];
@@ -345,19 +350,23 @@ __global__ __launch_bounds__(256, 2) void wgrad_x3_kernel(WgradParams p) {
         for (int a = 0; a < TM; ++a) {
           const __bf16* src = As + (wm * (BM / 2) + a * 32 + l32) * XLD + s * 16 + koff;
 #pragma unroll
-          for (int q = 0; q < 3; ++q) af[a][q] = *reinterpret_cast<const bf16x8*>(src + q * PA);
+          for (int q = 0; q < NP; ++q) af[a][q] = *reinterpret_cast<const bf16x8*>(src + q * PA);
         }
 #pragma unroll
         for (int b = 0; b < TN; ++b) {
           const __bf16* src = Bs + (wn * (BN / 2) + b * 32 + l32) * XLD + s * 16 + koff;
 #pragma unroll
-          for (int q = 0; q < 3; ++q) bf[b][q] = *reinterpret_cast<const bf16x8*>(src + q * PB);
+          for (int q = 0; q < NP; ++q) bf[b][q] = *reinterpret_cast<const bf16x8*>(src + q * PB);
         }
 #pragma unroll
         for (int a = 0; a < TM; ++a)
 #pragma unroll
           for (int b = 0; b < TN; ++b) {
             f32x16 c = acc[a][b];
+            if constexpr (NP == 1) {
+              acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[a][0], bf[b][0], c, 0, 0, 0);
+              continue;
+            }
             c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[a][2], bf[b][0], c, 0, 0, 0);
             c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[a][1], bf[b][1], c, 0, 0, 0);
             c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[a][0], bf[b][2], c, 0, 0, 0);
@@ -434,13 +443,16 @@ __global__ __launch_bounds__(256) void slab_sum_kernel(const float* __restrict__
 }  // namespace
 
 template <int BM, int BN>
-void wgrad_launch_t(const WgradParams& p, bool x3, hipStream_t st) {
+void wgrad_launch_t(const WgradParams& p, bool x3, hipStream_t st, bool bf16) {
   const int ntn = (p.Kdim + BN - 1) / BN;
   const int ntm = (p.Cout + BM - 1) / BM;
   const bool fast = (p.C % 4) == 0 && (p.Cout % 4) == 0;
   dim3 grid(ntm * ntn * p.splits);
   if (x3) {
-    if (fast) hipLaunchKernelGGL((wgrad_x3_kernel<BM, BN, true>), grid, dim3(256), 0, st, p);
+    if (bf16) {
+      if (fast) hipLaunchKernelGGL((wgrad_x3_kernel<BM, BN, true, 1>), grid, dim3(256), 0, st, p);
+      else hipLaunchKernelGGL((wgrad_x3_kernel<BM, BN, false, 1>), grid, dim3(256), 0, st, p);
+    } else if (fast) hipLaunchKernelGGL((wgrad_x3_kernel<BM, BN, true>), grid, dim3(256), 0, st, p);
     else hipLaunchKernelGGL((wgrad_x3_kernel<BM, BN, false>), grid, dim3(256), 0, st, p);
   } else {
     if (fast) hipLaunchKernelGGL((wgrad_kernel<BM, BN, true>), grid, dim3(256), 0, st, p);
@@ -448,11 +460,11 @@ void wgrad_launch_t(const WgradParams& p, bool x3, hipStream_t st) {
   }
 }
 
-void wgrad_launch(const WgradParams& p, int bm, int bn, bool x3, hipStream_t st) {
-  if (bm == 128 && bn == 128) wgrad_launch_t<128, 128>(p, x3, st);
-  else if (bm == 128) wgrad_launch_t<128, 64>(p, x3, st);
-  else if (bn == 128) wgrad_launch_t<64, 128>(p, x3, st);
-  else wgrad_launch_t<64, 64>(p, x3, st);
+void wgrad_launch(const WgradParams& p, int bm, int bn, bool x3, hipStream_t st, bool bf16) {
+  if (bm == 128 && bn == 128) wgrad_launch_t<128, 128>(p, x3, st, bf16);
+  else if (bm == 128) wgrad_launch_t<128, 64>(p, x3, st, bf16);
+  else if (bn == 128) wgrad_launch_t<64, 128>(p, x3, st, bf16);
+  else wgrad_launch_t<64, 64>(p, x3, st, bf16);
 }
 
 void slab_sum_launch(const float* slab, int S, long long n, float* dst, bool accumulate, hipStream_t st) {

@@ -60,14 +60,19 @@ int num_cus() {
 }
 
 // Conv GEMM engine: 1 = 3-term bf16 split on the bf16 MFMA (conv_x3.hip, fp32-accurate, default),
-// 0 = exact fp32-input MFMA (conv_igemm.hip). CDP_CONV_GEMM=f32 selects the latter at start-up.
+// 0 = exact fp32-input MFMA (conv_igemm.hip), 2 = plain bf16 operands with fp32 accumulation
+// (same kernels, one product per MAC: the fast non-parity mode). CDP_CONV_GEMM=f32|bf16 selects
+// at start-up; set_conv_gemm at run time.
 int& conv_gemm_mode() {
   static int m = [] {
     const char* e = std::getenv("CDP_CONV_GEMM");
-    return (e && std::string(e) == "f32") ? 0 : 1;
+    if (e && std::string(e) == "f32") return 0;
+    if (e && std::string(e) == "bf16") return 2;
+    return 1;
   }();
   return m;
 }
+bool x3_family() { return conv_gemm_mode() != 0; }
 
 // The x3 kernels address through 32-bit buffer offsets and 24-bit index multiplies; shapes past
 // those limits (or a strided data-gradient other than stride 2) take the exact fp32 kernels.
@@ -89,18 +94,18 @@ void conv_launch(const ConvGemmParams& p, int bm, int bn, bool dgrad, hipStream_
     const char* e = std::getenv("CDP_MFMA16");
     return e && e[0] == '1';  // measured: 16x16x32 tiles ran ~2% slower on VGG-11
   }();
-  if (conv_gemm_mode() == 1 && x3_ok(p, dgrad)) conv_x3_launch(p, bm, bn, dgrad, m16, st);
+  if (x3_family() && x3_ok(p, dgrad)) conv_x3_launch(p, bm, bn, dgrad, m16, st, conv_gemm_mode() == 2);
   else conv_igemm_launch(p, bm, bn, dgrad, st);
 }
 
 // Workgroups each kernel keeps resident per CU (min of the LDS and VGPR limits of the build).
 int conv_blocks_per_cu(int bm, int bn) {
-  if (conv_gemm_mode() == 1) return (bm + bn) >= 256 ? 1 : (bm + bn) >= 192 ? 2 : 3;  // 2 x 3 x (bm+bn) x 64 B
+  if (x3_family()) return (bm + bn) >= 256 ? 1 : (bm + bn) >= 192 ? 2 : 3;  // 2 x 3 x (bm+bn) x 64 B
   return std::max(1, std::min(4, (160 * 1024) / (2 * (bm + bn) * 36 * 4)));
 }
-double conv_mfma_rate() { return conv_gemm_mode() == 1 ? 250.0e12 : 120.0e12; }
+double conv_mfma_rate() { return conv_gemm_mode() == 1 ? 250.0e12 : conv_gemm_mode() == 2 ? 800.0e12 : 120.0e12; }
 int wgrad_blocks_per_cu(int bm, int bn) {
-  if (conv_gemm_mode() == 1) return (bm + bn) >= 256 ? 2 : (bm + bn) >= 192 ? 3 : 5;
+  if (x3_family()) return (bm + bn) >= 256 ? 2 : (bm + bn) >= 192 ? 3 : 5;
   return std::max(1, std::min(4, (160 * 1024) / (2 * 32 * (bm + bn + 8) * 4)));
 }
 
@@ -143,13 +148,13 @@ GemmPlan plan_gemm(long long M, int Nout, int Kdim) {
   // x3 engine: 8-wave 256x128 tiles (two waves per SIMD next to the software pipeline); measured
   // on VGG-11 B=256 they beat 128x128 / 64x128 on every layer, split-K making up the grid
   // (127.5k vs 124.5k img/s with 256 only for M >= 8192)
-  if (conv_gemm_mode() == 1 && g.bn == 128) g.bm = 256;
+  if (x3_family() && g.bn == 128) g.bm = 256;
   static const int force_bm = [] {
     const char* e = std::getenv("CDP_TILE_BM");
     return e ? std::atoi(e) : 0;
   }();
   if (force_bm == 64 || force_bm == 128) g.bm = force_bm;
-  if (force_bm == 256 && g.bn == 128 && conv_gemm_mode() == 1) g.bm = 256;
+  if (force_bm == 256 && g.bn == 128 && x3_family()) g.bm = 256;
   if (force_bm == 128 && g.bm == 256) g.bm = 128;
   const long long tiles = ((M + g.bm - 1) / g.bm) * ((Nout + g.bn - 1) / g.bn);
   const int slots = conv_blocks_per_cu(g.bm, g.bn) * num_cus();
@@ -242,10 +247,14 @@ at::Tensor pad_channels4(const at::Tensor& t) {
 }  // namespace
 
 void set_conv_gemm(const std::string& mode) {
-  TORCH_CHECK(mode == "x3" || mode == "f32", "conv gemm engine must be 'x3' or 'f32', got ", mode);
-  conv_gemm_mode() = mode == "x3" ? 1 : 0;
+  TORCH_CHECK(mode == "x3" || mode == "f32" || mode == "bf16", "conv gemm engine must be 'x3', 'f32' or 'bf16', got ",
+              mode);
+  conv_gemm_mode() = mode == "x3" ? 1 : mode == "bf16" ? 2 : 0;
 }
-std::string get_conv_gemm() { return conv_gemm_mode() == 1 ? "x3" : "f32"; }
+std::string get_conv_gemm() {
+  const int m = conv_gemm_mode();
+  return m == 1 ? "x3" : m == 2 ? "bf16" : "f32";
+}
 
 // ---------------------------------------------------------------- conv forward
 // Returns y (channels_last [N, Cout, P, Q]). When `part` is requested the per-tile BatchNorm
@@ -397,7 +406,7 @@ at::Tensor conv2d_dgrad(const at::Tensor& dy_, const at::Tensor& w_, std::vector
                     addend->size(0) == N && addend->size(1) == C && addend->size(2) == H && addend->size(3) == W,
                 "dgrad addend must be a channels_last fp32 tensor of the input's shape");
   const float* addp = has_add ? addend->data_ptr<float>() : nullptr;
-  if (stride == 2 && conv_gemm_mode() == 1 && subpixel_enabled()) {
+  if (stride == 2 && x3_family() && subpixel_enabled()) {
     at::Tensor dx = has_add ? *addend : at::empty({N, C, H, W}, opts.memory_format(at::MemoryFormat::ChannelsLast));
     if (conv2d_dgrad_subpixel(dy, w, dx, (int)pad, st, addp)) return dx;
   }
@@ -473,11 +482,11 @@ at::Tensor conv2d_wgrad_keep(const at::Tensor& dy_, const at::Tensor& x_, std::v
   set_divs(p);
   if (p.splits == 1 && !accumulate && Ckeep == C) {
     p.out = dw.data_ptr<float>();
-    wgrad_launch(p, wp.bm, wp.bn, conv_gemm_mode() == 1 && x3_ok(p), st);
+    wgrad_launch(p, wp.bm, wp.bn, x3_family() && x3_ok(p), st, conv_gemm_mode() == 2);
   } else {
     at::Tensor slab = at::empty({p.splits, Co, Kdim}, opts);
     p.out = slab.data_ptr<float>();
-    wgrad_launch(p, wp.bm, wp.bn, conv_gemm_mode() == 1 && x3_ok(p), st);
+    wgrad_launch(p, wp.bm, wp.bn, x3_family() && x3_ok(p), st, conv_gemm_mode() == 2);
     slab_sum_strided_launch(slab.data_ptr<float>(), p.splits, (long long)Co * Kdim, C, Ckeep, dw.data_ptr<float>(),
                             accumulate, st);
   }
@@ -684,11 +693,11 @@ std::vector<at::Tensor> linear_bwd(const at::Tensor& gy_, const at::Tensor& x_, 
   set_divs(p);
   if (p.splits == 1) {
     p.out = dw.data_ptr<float>();
-    wgrad_launch(p, wp.bm, wp.bn, conv_gemm_mode() == 1 && x3_ok(p), st);
+    wgrad_launch(p, wp.bm, wp.bn, x3_family() && x3_ok(p), st, conv_gemm_mode() == 2);
   } else {
     at::Tensor slab = at::empty({p.splits, O, I}, x.options());
     p.out = slab.data_ptr<float>();
-    wgrad_launch(p, wp.bm, wp.bn, conv_gemm_mode() == 1 && x3_ok(p), st);
+    wgrad_launch(p, wp.bm, wp.bn, x3_family() && x3_ok(p), st, conv_gemm_mode() == 2);
     slab_sum_launch(slab.data_ptr<float>(), p.splits, (long long)O * I, dw.data_ptr<float>(), false, st);
   }
   at::Tensor db;

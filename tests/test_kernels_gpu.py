@@ -309,3 +309,27 @@ def test_x3_engine_is_as_accurate_as_fp32_mfma(N, Ci, H, W, Co, k, s, p):
     for i in range(4):
         assert errs["x3"][i] <= 2.0 * errs["f32"][i] + 1e-9, errs
     assert max(errs["x3"][0], errs["x3"][1], errs["x3"][3]) < 1e-6, errs
+
+
+def test_bf16_engine_runs_at_bf16_accuracy():
+    """CDP_CONV_GEMM=bf16 (non-parity fast mode): one bf16 product per MAC, fp32 accumulation."""
+    torch.manual_seed(2)
+    N, Ci, H, W, Co = 4, 128, 8, 8, 256
+    x = torch.randn(N, Ci, H, W, device="cuda")
+    w = torch.randn(Co, Ci, 3, 3, device="cuda") * (1.0 / (Ci * 9) ** 0.5)
+    ref = F.conv2d(x.double().cpu(), w.double().cpu(), None, 1, 1)
+    orig = C().get_conv_gemm()
+    try:
+        C().set_conv_gemm("bf16")
+        assert C().get_conv_gemm() == "bf16"
+        y = C().conv2d_fwd(cl(x), cl(w), None, 1, 1, False)[0]
+        gy = torch.randn_like(y)
+        dw = C().conv2d_wgrad(cl(gy), cl(x), list(w.shape), 1, 1)
+    finally:
+        C().set_conv_gemm(orig)
+    e = _rms_rel(y, ref)
+    assert 1e-5 < e < 1e-2, e  # bf16-level, clearly not fp32-level
+    xr = x.double().cpu()
+    wr = w.double().cpu().requires_grad_()
+    F.conv2d(xr, wr, None, 1, 1).backward(gy.double().cpu())
+    assert _rms_rel(dw, wr.grad) < 1e-2
