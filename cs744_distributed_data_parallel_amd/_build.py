@@ -23,7 +23,7 @@ EXT_SUFFIX = sysconfig.get_config_var("EXT_SUFFIX") or ".so"
 OUTPUT = os.path.join(PKG_DIR, "_C" + EXT_SUFFIX)
 
 KERNELS = ["conv_igemm.hip", "conv_x3.hip", "wgrad.hip", "bn.hip", "misc.hip"]
-RUNTIME = ["ops.cpp", "rccl_comm.cpp", "reducer.cpp", "bindings.cpp"]
+RUNTIME = ["ops.cpp", "rccl_comm.cpp", "reducer.cpp", "torch_ops.cpp", "bindings.cpp"]
 
 
 def _torch_paths():

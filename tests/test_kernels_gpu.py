@@ -333,3 +333,33 @@ def test_bf16_engine_runs_at_bf16_accuracy():
     wr = w.double().cpu().requires_grad_()
     F.conv2d(xr, wr, None, 1, 1).backward(gy.double().cpu())
     assert _rms_rel(dw, wr.grad) < 1e-2
+
+
+def test_torch_custom_ops_with_autograd():
+    """torch.ops.cdp.* (TORCH_LIBRARY registration) dispatch to the gfx950 kernels; conv2d and
+    linear carry C++ autograd formulas."""
+    C()  # loads the extension, which registers the ops
+    torch.manual_seed(3)
+    x = cl(torch.randn(4, 64, 8, 8, device="cuda")).requires_grad_()
+    w = cl(torch.randn(128, 64, 3, 3, device="cuda") * 0.05).requires_grad_()
+    b = torch.randn(128, device="cuda", requires_grad=True)
+    y = torch.ops.cdp.conv2d(x, w, b, 1, 1)
+    gy = torch.randn_like(y)
+    y.backward(gy)
+    xr, wr, br = (t.detach().double().cpu().requires_grad_() for t in (x, w, b))
+    yr = F.conv2d(xr, wr, br, 1, 1)
+    yr.backward(gy.double().cpu())
+    assert rel_err(y, yr) < 2e-5
+    for g, gr in ((x.grad, xr.grad), (w.grad, wr.grad), (b.grad, br.grad)):
+        assert rel_err(g, gr) < 2e-5
+    xl = torch.randn(16, 512, device="cuda", requires_grad=True)
+    wl = (torch.randn(10, 512, device="cuda") * 0.05).requires_grad_()
+    yl = torch.ops.cdp.linear(xl, wl, None)
+    yl.sum().backward()
+    assert rel_err(yl, xl.detach().double().cpu() @ wl.detach().double().cpu().t()) < 2e-5
+    assert rel_err(xl.grad, wl.detach().double().cpu().sum(0).expand(16, 512)) < 2e-5
+    logits = torch.randn(32, 10, device="cuda")
+    tgt = torch.randint(0, 10, (32,), device="cuda")
+    assert abs(torch.ops.cdp.cross_entropy(logits, tgt).item() - F.cross_entropy(logits, tgt).item()) < 1e-5
+    yp, arg = torch.ops.cdp.max_pool2d(cl(torch.randn(2, 32, 8, 8, device="cuda")), 2, 2, 0)
+    assert yp.shape == (2, 32, 4, 4) and arg.dtype == torch.uint8
