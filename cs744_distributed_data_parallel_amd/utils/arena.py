@@ -215,7 +215,9 @@ def arena_for(params: Sequence[torch.nn.Parameter], create: bool = True) -> Flat
 class BufferArena:
     """Flat arena for module buffers (BN running stats) so they broadcast as ONE collective.
 
-    Floating buffers share one fp32 storage; integer buffers (``num_batches_tracked``) another.
+    Every buffer, whatever its dtype (fp32 running stats, int64 ``num_batches_tracked``), is a
+    typed view into one byte storage; DDP's per-forward buffer sync is then a single ``uint8``
+    broadcast instead of one per dtype (each collective costs a launch-latency round at N>1).
     """
 
     def __init__(self, buffers: Sequence[torch.Tensor]):
@@ -224,9 +226,17 @@ class BufferArena:
         by_dtype = {}
         for b in self.buffers:
             by_dtype.setdefault(b.dtype, []).append(b)
+        layout, nbytes = [], 0
         for dt, bufs in by_dtype.items():
+            es = torch.empty((), dtype=dt).element_size()
+            nbytes = (nbytes + 15) // 16 * 16  # 16-B aligned groups
             total = sum(b.numel() for b in bufs)
-            flat = torch.empty(total, device=bufs[0].device, dtype=dt)
+            layout.append((dt, bufs, nbytes, total))
+            nbytes += total * es
+        self.bytes = torch.empty(max(nbytes, 1), device=self.buffers[0].device, dtype=torch.uint8)
+        for dt, bufs, start, total in layout:
+            es = torch.empty((), dtype=dt).element_size()
+            flat = self.bytes[start : start + total * es].view(dt)
             off = 0
             for b in bufs:
                 n = b.numel()
@@ -237,4 +247,5 @@ class BufferArena:
             self.groups[dt] = flat
 
     def flats(self) -> List[torch.Tensor]:
-        return list(self.groups.values())
+        """The storages to broadcast: one byte tensor covering every buffer."""
+        return [self.bytes]

@@ -139,7 +139,15 @@ def _buffers_broadcast(rank, world):
     w0 = m[0].weight.detach().clone().numpy()
     rm0 = m[1].running_mean.clone().numpy()
     net(torch.randn(2, 3, 8, 8))
-    return w0, rm0, net.state_dict().keys().__iter__().__next__()
+    # per-forward sync: rank 1 drifts its fp32 and int64 buffers, the next forward restores
+    # rank 0's (both dtypes travel in one byte broadcast, see utils/arena.py BufferArena)
+    with torch.no_grad():
+        if rank == 1:
+            m[1].running_var.fill_(7.0)
+            m[1].num_batches_tracked.fill_(100)
+    net(torch.randn(2, 3, 8, 8, generator=torch.Generator().manual_seed(0)))  # same batch on both
+    extra = (m[1].running_var.clone().numpy(), int(m[1].num_batches_tracked))
+    return w0, rm0, net.state_dict().keys().__iter__().__next__(), extra
 
 
 def _rebuild_ready_order(rank, world):
@@ -217,6 +225,8 @@ def test_ddp_broadcasts_rank0_state():
     np.testing.assert_allclose(res[0][0], res[1][0])
     np.testing.assert_allclose(res[1][1], 0.0)  # rank 1's running_mean replaced by rank 0's
     assert res[0][2].startswith("module.")
+    np.testing.assert_allclose(res[0][3][0], res[1][3][0])
+    assert res[0][3][1] == res[1][3][1] == 2
 
 
 def test_bucket_rebuild_in_ready_order():
