@@ -163,13 +163,16 @@ __device__ __forceinline__ void pool_relu_grad(float z0, float z1, float z2, flo
 
 #define F4GET(v, j) ((j) == 0 ? (v).x : (j) == 1 ? (v).y : (j) == 2 ? (v).z : (v).w)
 
-// Per (block, channel) partial sums of dz and dz*xhat, where dz is the gradient at the BN output.
+// Per (block, channel) partial sums of dz and dz*xhat, where dz is the gradient at the BN output,
+// and (PS == 3) of xhat itself, from which chan_finalize derives the conv-bias gradient
+// sum(dy) = -scale * sum(xhat) * sum(dz*xhat) / M without a second pass over dy.
 // Block = 256 threads; for C4 <= 256 threads split as ppb pixel lanes x C4 channel quads.
+template <int PS>
 __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const float* __restrict__ y, const float* __restrict__ gout,
                                                             const float* __restrict__ stats, float* __restrict__ part,
                                                             int N, int H, int W, int C, int pool, int relu,
                                                             const float* __restrict__ zout) {
-  __shared__ float4 red1[256], red2[256];
+  __shared__ float4 red1[256], red2[256], red3[PS == 3 ? 256 : 1];
   const int C4 = C >> 2;
   const int tid = threadIdx.x;
   const int cq_per_thread = (C4 + 255) / 256;  // 1 or 2
@@ -186,7 +189,7 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const float* __restr
   const long long npix = (long long)N * Ho * Wo;  // output (pooled) pixels
   for (int j = 0; j < cq_per_thread; ++j) {
     const int cq = cq0 + j * 256;
-    float4 a1 = f4zero(), a2 = f4zero();
+    float4 a1 = f4zero(), a2 = f4zero(), a3 = f4zero();
     if (active && cq < C4) {
       const float4 sc = ld4(scale + 4 * cq), sh = ld4(shift + 4 * cq);
       const float4 mu = ld4(mean + 4 * cq), is = ld4(invstd + 4 * cq);
@@ -199,10 +202,10 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const float* __restr
           for (int e = 0; e < 4; ++e) {
             const float dz = (!relu || F4GET(z, e) > 0.f) ? F4GET(g, e) : 0.f;
             const float xh = (F4GET(yv, e) - F4GET(mu, e)) * F4GET(is, e);
-            if (e == 0) { a1.x += dz; a2.x += dz * xh; }
-            if (e == 1) { a1.y += dz; a2.y += dz * xh; }
-            if (e == 2) { a1.z += dz; a2.z += dz * xh; }
-            if (e == 3) { a1.w += dz; a2.w += dz * xh; }
+            if (e == 0) { a1.x += dz; a2.x += dz * xh; a3.x += xh; }
+            if (e == 1) { a1.y += dz; a2.y += dz * xh; a3.y += xh; }
+            if (e == 2) { a1.z += dz; a2.z += dz * xh; a3.z += xh; }
+            if (e == 3) { a1.w += dz; a2.w += dz * xh; a3.w += xh; }
           }
         } else {
           const int wo = (int)(px % Wo);
@@ -221,63 +224,90 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const float* __restr
                            d3);
             const float m = F4GET(mu, e), s = F4GET(is, e);
             const float sdz = d0 + d1 + d2 + d3;
-            const float sdx = d0 * ((F4GET(y0, e) - m) * s) + d1 * ((F4GET(y1, e) - m) * s) +
-                              d2 * ((F4GET(y2, e) - m) * s) + d3 * ((F4GET(y3, e) - m) * s);
-            if (e == 0) { a1.x += sdz; a2.x += sdx; }
-            if (e == 1) { a1.y += sdz; a2.y += sdx; }
-            if (e == 2) { a1.z += sdz; a2.z += sdx; }
-            if (e == 3) { a1.w += sdz; a2.w += sdx; }
+            const float x0 = (F4GET(y0, e) - m) * s, x1 = (F4GET(y1, e) - m) * s, x2 = (F4GET(y2, e) - m) * s,
+                        x3 = (F4GET(y3, e) - m) * s;
+            const float sdx = d0 * x0 + d1 * x1 + d2 * x2 + d3 * x3;
+            const float sx = (x0 + x1) + (x2 + x3);
+            if (e == 0) { a1.x += sdz; a2.x += sdx; a3.x += sx; }
+            if (e == 1) { a1.y += sdz; a2.y += sdx; a3.y += sx; }
+            if (e == 2) { a1.z += sdz; a2.z += sdx; a3.z += sx; }
+            if (e == 3) { a1.w += sdz; a2.w += sdx; a3.w += sx; }
           }
         }
       }
     }
     red1[tid] = a1;
     red2[tid] = a2;
+    if constexpr (PS == 3) red3[tid] = a3;
     __syncthreads();
     if (pl == 0 && cq < C4) {
-      float4 s1 = a1, s2 = a2;
+      float4 s1 = a1, s2 = a2, s3 = a3;
       for (int k = 1; k < ppb; ++k) {
         const float4 b1 = red1[k * lanes_c + cq0], b2 = red2[k * lanes_c + cq0];
         s1.x += b1.x; s1.y += b1.y; s1.z += b1.z; s1.w += b1.w;
         s2.x += b2.x; s2.y += b2.y; s2.z += b2.z; s2.w += b2.w;
+        if constexpr (PS == 3) {
+          const float4 b3 = red3[k * lanes_c + cq0];
+          s3.x += b3.x; s3.y += b3.y; s3.z += b3.z; s3.w += b3.w;
+        }
       }
-      float* dst = part + ((long long)blockIdx.x * C + 4 * cq) * 2;
-      dst[0] = s1.x; dst[1] = s2.x; dst[2] = s1.y; dst[3] = s2.y;
-      dst[4] = s1.z; dst[5] = s2.z; dst[6] = s1.w; dst[7] = s2.w;
+      float* dst = part + ((long long)blockIdx.x * C + 4 * cq) * PS;
+      dst[0] = s1.x; dst[1] = s2.x;
+      dst[PS] = s1.y; dst[PS + 1] = s2.y;
+      dst[2 * PS] = s1.z; dst[2 * PS + 1] = s2.z;
+      dst[3 * PS] = s1.w; dst[3 * PS + 1] = s2.w;
+      if constexpr (PS == 3) {
+        dst[2] = s3.x; dst[5] = s3.y; dst[8] = s3.z; dst[11] = s3.w;
+      }
     }
     __syncthreads();
   }
 }
 
-// Sum per-block partial pairs: out[c] = sum_b part[b][c][0], out[C+c] = sum_b part[b][c][1]
-// (fp64 accumulation; deterministic order). Optionally also writes into two gradient slots
-// (accumulating if requested).
-__global__ __launch_bounds__(256) void chan_finalize_kernel(const float* __restrict__ part, int nparts, int C,
+// Sum per-block partials (PS floats per (block, channel); fp64 accumulation, deterministic order):
+// out[c] = sum_b part[b][c][0], out[C+c] = sum_b part[b][c][1]. Optionally also writes them into
+// two gradient slots (accumulating if requested), and the conv-bias gradient db = sum_m dy_m:
+//   dbmode 1 (training BN, PS == 3):  sum_m scale*(dz - S0/M - xhat*S1/M) = -scale * S2 * S1 / M
+//   dbmode 2 (eval BN, dy = scale*dz): scale * S0
+// so the bias gradient needs neither per-block partials of dy nor a launch of its own.
+__global__ __launch_bounds__(256) void chan_finalize_kernel(const float* __restrict__ part, int nparts, int C, int PS,
                                                             float* __restrict__ out, float* g0, float* g1,
-                                                            int accumulate) {
-  __shared__ double r0[4], r1[4];
+                                                            int accumulate, float* __restrict__ gdb,
+                                                            const float* __restrict__ scale, double invM,
+                                                            int dbmode) {
+  __shared__ double r0[4], r1[4], r2[4];
   const int c = blockIdx.x;
-  double s0 = 0.0, s1 = 0.0;
+  double s0 = 0.0, s1 = 0.0, s2 = 0.0;
   for (int b = threadIdx.x; b < nparts; b += 256) {
-    s0 += (double)part[((long long)b * C + c) * 2];
-    s1 += (double)part[((long long)b * C + c) * 2 + 1];
+    const float* q = part + ((long long)b * C + c) * PS;
+    s0 += (double)q[0];
+    s1 += (double)q[1];
+    if (PS == 3) s2 += (double)q[2];
   }
   s0 = wave_sum_d(s0);
   s1 = wave_sum_d(s1);
+  if (PS == 3) s2 = wave_sum_d(s2);
   if ((threadIdx.x & 63) == 0) {
     r0[threadIdx.x >> 6] = s0;
     r1[threadIdx.x >> 6] = s1;
+    r2[threadIdx.x >> 6] = s2;
   }
   __syncthreads();
   if (threadIdx.x == 0) {
-    const float t0 = (float)(r0[0] + r0[1] + r0[2] + r0[3]);
-    const float t1 = (float)(r1[0] + r1[1] + r1[2] + r1[3]);
+    const double d0 = r0[0] + r0[1] + r0[2] + r0[3];
+    const double d1 = r1[0] + r1[1] + r1[2] + r1[3];
+    const double d2 = r2[0] + r2[1] + r2[2] + r2[3];
+    const float t0 = (float)d0, t1 = (float)d1;
     if (out) {
-      out[c] = t0;
-      out[C + c] = t1;
+      out[c] = dbmode == 2 ? 0.f : t0;  // eval-mode BN has no batch-statistics terms
+      out[C + c] = dbmode == 2 ? 0.f : t1;
     }
     if (g0) g0[c] = accumulate ? g0[c] + t0 : t0;
     if (g1) g1[c] = accumulate ? g1[c] + t1 : t1;
+    if (dbmode) {
+      const float db = dbmode == 1 ? (float)(-(double)scale[c] * d2 * d1 * invM) : (float)((double)scale[c] * d0);
+      gdb[c] = accumulate ? gdb[c] + db : db;
+    }
   }
 }
 
@@ -439,15 +469,20 @@ void bn_act_fwd_launch(const float* y, const float* stats, const float* res, flo
 }
 
 void bn_bwd_reduce_launch(const float* y, const float* gout, const float* stats, float* part, int nblocks, int N,
-                          int H, int W, int C, bool pool, bool relu, const float* zout, hipStream_t st) {
-  hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(nblocks), dim3(256), 0, st, y, gout, stats, part, N, H, W, C,
-                     pool ? 1 : 0, relu ? 1 : 0, zout);
+                          int H, int W, int C, bool pool, bool relu, const float* zout, hipStream_t st,
+                          bool with_xsum) {
+  if (with_xsum)
+    hipLaunchKernelGGL(bn_bwd_reduce_kernel<3>, dim3(nblocks), dim3(256), 0, st, y, gout, stats, part, N, H, W, C,
+                       pool ? 1 : 0, relu ? 1 : 0, zout);
+  else
+    hipLaunchKernelGGL(bn_bwd_reduce_kernel<2>, dim3(nblocks), dim3(256), 0, st, y, gout, stats, part, N, H, W, C,
+                       pool ? 1 : 0, relu ? 1 : 0, zout);
 }
 
 void chan_finalize_launch(const float* part, int nparts, int C, float* out, float* g0, float* g1, bool accumulate,
-                          hipStream_t st) {
-  hipLaunchKernelGGL(chan_finalize_kernel, dim3(C), dim3(256), 0, st, part, nparts, C, out, g0, g1,
-                     accumulate ? 1 : 0);
+                          hipStream_t st, int ps, float* gdb, const float* scale, long long M, int dbmode) {
+  hipLaunchKernelGGL(chan_finalize_kernel, dim3(C), dim3(256), 0, st, part, nparts, C, ps, out, g0, g1,
+                     accumulate ? 1 : 0, gdb, scale, M > 0 ? 1.0 / (double)M : 0.0, dbmode);
 }
 
 void bn_bwd_apply_launch(const float* y, const float* gout, const float* stats, const float* sums, float* dy,

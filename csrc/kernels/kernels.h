@@ -106,9 +106,11 @@ void bn_eval_stats_launch(int C, const float* gamma, const float* beta, const fl
 void bn_act_fwd_launch(const float* y, const float* stats, const float* res, float* out, int N, int H, int W, int C,
                        bool pool, bool relu, hipStream_t st);
 void bn_bwd_reduce_launch(const float* y, const float* gout, const float* stats, float* part, int nblocks, int N,
-                          int H, int W, int C, bool pool, bool relu, const float* zout, hipStream_t st);
+                          int H, int W, int C, bool pool, bool relu, const float* zout, hipStream_t st,
+                          bool with_xsum = false);
 void chan_finalize_launch(const float* part, int nparts, int C, float* out, float* g0, float* g1, bool accumulate,
-                          hipStream_t st);
+                          hipStream_t st, int ps = 2, float* gdb = nullptr, const float* scale = nullptr,
+                          long long M = 0, int dbmode = 0);
 void bn_bwd_apply_launch(const float* y, const float* gout, const float* stats, const float* sums, float* dy,
                          float* dbias_part, int nblocks, int N, int H, int W, int C, bool pool, bool relu,
                          const float* zout, float* dres, hipStream_t st);

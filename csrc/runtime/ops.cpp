@@ -563,9 +563,16 @@ std::vector<at::Tensor> conv_bn_act_bwd(const at::Tensor& gout_, const at::Tenso
   at::Tensor zout;
   if (zout_.has_value() && zout_->defined()) zout = nhwc(*zout_);
   const int nblk = bn_bwd_grid(N, H, W, C, pool);
-  at::Tensor part = at::empty({nblk, C, 2}, opts);
+  // The conv-bias gradient sum(dy) comes out of the finalize of the statistics reduction
+  // (chan_finalize dbmode): in training mode from one extra partial, sum(xhat); in eval mode as
+  // scale * sum(dz). Only a pooled odd-size map (border pixels outside every window, which the
+  // reduction does not visit) takes the separate partial-sum pass over dy.
+  const bool odd_pool = pool && ((H & 1) || (W & 1));
+  const bool fused_db = has_bias && !odd_pool;
+  const int ps = fused_db && training ? 3 : 2;
+  at::Tensor part = at::empty({nblk, C, ps}, opts);
   bn_bwd_reduce_launch(y.data_ptr<float>(), gout.data_ptr<float>(), stats.data_ptr<float>(), part.data_ptr<float>(),
-                       nblk, N, H, W, C, pool, relu, zout.defined() ? zout.data_ptr<float>() : nullptr, st);
+                       nblk, N, H, W, C, pool, relu, zout.defined() ? zout.data_ptr<float>() : nullptr, st, ps == 3);
   at::Tensor sums = at::empty({2, C}, opts);
   // gradients go straight into the caller's slots (flat-arena views) when provided
   auto slot = [&](const c10::optional<at::Tensor>& o, std::initializer_list<int64_t> shape, bool cl) {
@@ -573,24 +580,26 @@ std::vector<at::Tensor> conv_bn_act_bwd(const at::Tensor& gout_, const at::Tenso
     return cl ? at::empty(shape, opts.memory_format(at::MemoryFormat::ChannelsLast)) : at::empty(shape, opts);
   };
   at::Tensor dgamma = slot(dgamma_out, {C}, false), dbeta = slot(dbeta_out, {C}, false);
-  chan_finalize_launch(part.data_ptr<float>(), nblk, C, sums.data_ptr<float>(), dbeta.data_ptr<float>(),
-                       dgamma.data_ptr<float>(), false, st);
+  at::Tensor db;
+  if (has_bias) db = slot(db_out, {C}, false);
   // eval-mode BatchNorm is a fixed affine map: dy = scale * dz (no batch-statistics terms)
-  if (!training) sums.zero_();
+  const int dbmode = fused_db ? (training ? 1 : 2) : 0;
+  chan_finalize_launch(part.data_ptr<float>(), nblk, C, sums.data_ptr<float>(), dbeta.data_ptr<float>(),
+                       dgamma.data_ptr<float>(), false, st, ps, fused_db ? db.data_ptr<float>() : nullptr,
+                       stats.data_ptr<float>() + 2 * C, (long long)N * H * W, dbmode);
+  if (!training && dbmode != 2) sums.zero_();
   at::Tensor dy = at::empty({N, C, H, W}, opts.memory_format(at::MemoryFormat::ChannelsLast));
   at::Tensor dbpart;
-  if (has_bias) dbpart = at::empty({nblk, C, 2}, opts);
+  const bool sep_db = has_bias && !fused_db;
+  if (sep_db) dbpart = at::empty({nblk, C, 2}, opts);
   at::Tensor dres;
   if (zout.defined()) dres = at::empty({N, C, H, W}, opts.memory_format(at::MemoryFormat::ChannelsLast));
   bn_bwd_apply_launch(y.data_ptr<float>(), gout.data_ptr<float>(), stats.data_ptr<float>(), sums.data_ptr<float>(),
-                      dy.data_ptr<float>(), has_bias ? dbpart.data_ptr<float>() : nullptr, nblk, N, H, W, C, pool,
+                      dy.data_ptr<float>(), sep_db ? dbpart.data_ptr<float>() : nullptr, nblk, N, H, W, C, pool,
                       relu, zout.defined() ? zout.data_ptr<float>() : nullptr,
                       dres.defined() ? dres.data_ptr<float>() : nullptr, st);
-  at::Tensor db;
-  if (has_bias) {
-    db = slot(db_out, {C}, false);
+  if (sep_db)
     chan_finalize_launch(dbpart.data_ptr<float>(), nblk, C, nullptr, db.data_ptr<float>(), nullptr, false, st);
-  }
   // x may carry zero-padded channels (RGB stem, see conv_bn_act_fwd)
   const bool padc = x.size(1) != w.size(1);
   // data- and weight-gradient GEMMs are independent: optionally run the weight gradient on a side

@@ -87,6 +87,7 @@ BLOCK_CASES = [
     (4, 128, 8, 8, 256, False),
     (4, 512, 2, 2, 512, True),
     (4, 512, 4, 4, 512, False),
+    (2, 64, 7, 7, 64, True),  # odd map under pooling: separate conv-bias partial pass
 ]
 
 
