@@ -440,6 +440,51 @@ __global__ __launch_bounds__(256) void slab_sum_kernel(const float* __restrict__
   }
 }
 
+// Unstrided float4 form: dst[i] = (accumulate ? dst[i] : 0) + sum_z slab[z][i] for n % 4 == 0.
+// CB float4 column slots x SL = 256 / CB split lanes per block; every thread keeps up to four
+// independent 16-B loads in flight. CB is chosen at launch so the grid has >= ~1024 blocks.
+template <int CB>
+__global__ __launch_bounds__(256) void slab_sum4_kernel(const float4* __restrict__ slab, int S, long long n4,
+                                                        float4* __restrict__ dst, int accumulate) {
+  constexpr int SL = 256 / CB;
+  __shared__ float4 red[SL > 1 ? SL : 1][CB];
+  const int cl = threadIdx.x % CB, sl = threadIdx.x / CB;
+  const long long i = (long long)blockIdx.x * CB + cl;
+  float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (i < n4) {
+    int z = sl;
+    for (; z + 3 * SL < S; z += 4 * SL) {
+      const float4 a = slab[(long long)z * n4 + i], b = slab[(long long)(z + SL) * n4 + i];
+      const float4 c = slab[(long long)(z + 2 * SL) * n4 + i], d = slab[(long long)(z + 3 * SL) * n4 + i];
+      s.x += (a.x + b.x) + (c.x + d.x);
+      s.y += (a.y + b.y) + (c.y + d.y);
+      s.z += (a.z + b.z) + (c.z + d.z);
+      s.w += (a.w + b.w) + (c.w + d.w);
+    }
+    for (; z < S; z += SL) {
+      const float4 a = slab[(long long)z * n4 + i];
+      s.x += a.x; s.y += a.y; s.z += a.z; s.w += a.w;
+    }
+  }
+  if constexpr (SL > 1) {
+    red[sl][cl] = s;
+    __syncthreads();
+    if (sl != 0) return;
+#pragma unroll
+    for (int k = 1; k < SL; ++k) {
+      const float4 b = red[k][cl];
+      s.x += b.x; s.y += b.y; s.z += b.z; s.w += b.w;
+    }
+  }
+  if (i < n4) {
+    if (accumulate) {
+      const float4 o = dst[i];
+      s.x += o.x; s.y += o.y; s.z += o.z; s.w += o.w;
+    }
+    dst[i] = s;
+  }
+}
+
 }  // namespace
 
 template <int BM, int BN>
@@ -473,6 +518,25 @@ void slab_sum_launch(const float* slab, int S, long long n, float* dst, bool acc
 
 void slab_sum_strided_launch(const float* slab, int S, long long n_src, int src_cols, int dst_cols, float* dst,
                              bool accumulate, hipStream_t st) {
+  const bool vec = src_cols == dst_cols && n_src % 4 == 0 && (reinterpret_cast<uintptr_t>(slab) & 15) == 0 &&
+                   (reinterpret_cast<uintptr_t>(dst) & 15) == 0;
+  if (vec) {
+    const long long n4 = n_src / 4;
+    const float4* s4 = reinterpret_cast<const float4*>(slab);
+    float4* d4 = reinterpret_cast<float4*>(dst);
+    const int acc = accumulate ? 1 : 0;
+    // widest column slot count that still gives >= 1024 blocks (more split lanes when n is short)
+    if (n4 >= 256LL * 1024 || S <= 1)
+      hipLaunchKernelGGL(slab_sum4_kernel<256>, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, st, s4, S, n4, d4,
+                         acc);
+    else if (n4 >= 64LL * 1024 || S <= 4)
+      hipLaunchKernelGGL(slab_sum4_kernel<64>, dim3((unsigned)((n4 + 63) / 64)), dim3(256), 0, st, s4, S, n4, d4,
+                         acc);
+    else
+      hipLaunchKernelGGL(slab_sum4_kernel<16>, dim3((unsigned)((n4 + 15) / 16)), dim3(256), 0, st, s4, S, n4, d4,
+                         acc);
+    return;
+  }
   if (S >= 16 && n_src < (1 << 18)) {
     hipLaunchKernelGGL(slab_sum_kernel<16>, dim3((unsigned)((n_src + 15) / 16)), dim3(256), 0, st, slab, S, n_src,
                        src_cols, dst_cols, dst, accumulate ? 1 : 0);
