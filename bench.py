@@ -44,8 +44,8 @@ def parse():
     p.add_argument("--backend", default="native", choices=["native", "torch"],
                    help="torch = stock PyTorch-ROCm ops + torch DDP (comparison only)")
     p.add_argument("--precision", default="fp32", choices=["fp32", "bf16"],
-                   help="fp32 (default, the reference's precision; conv GEMMs fp32-accurate via the 3-term "
-                        "bf16 split) or bf16 (conv GEMM operands rounded to bf16, fp32 accumulation: "
+                   help="fp32 (default, the reference's precision; conv GEMMs fp32-accurate via the f16x2 "
+                        "split, or CDP_CONV_GEMM=x3|f32) or bf16 (conv GEMM operands rounded to bf16, fp32 accumulation: "
                         "the non-parity fast mode)")
     p.add_argument("--bucket-cap-mb", type=float, default=None)
     p.add_argument("--dataset-size", type=int, default=50000)
@@ -232,9 +232,11 @@ def main():
                 "backend": args.backend,
                 "hipgraph": graph is not None,
                 "optimizer": "SGD(lr=0.1, momentum=0.9, wd=1e-4)",
-                # conv GEMM numerics: fp32 operands/accumulation; "x3" = fp32-accurate 3-term
-                # bf16 split on the bf16 MFMA (error vs fp64 <= the exact fp32 MFMA's, see
-                # docs/PERF.md), "f32" = exact fp32-input MFMA
+                # conv GEMM numerics, all with fp32 operands and fp32 accumulation: "f16x2" =
+                # power-of-two-scaled operands split into two fp16 terms, three products on the
+                # fp16 MFMA; "x3" = 3-term bf16 split, six products on the bf16 MFMA (both: error vs
+                # fp64 <= the exact fp32 MFMA's, tests/test_kernels_gpu.py, docs/PERF.md); "f32" =
+                # exact fp32-input MFMA
                 "conv_gemm": _conv_gemm_engine(args.backend),
             },
         }

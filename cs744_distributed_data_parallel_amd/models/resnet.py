@@ -121,9 +121,21 @@ class ResNet(nn.Module):
     def forward(self, x):
         if CF.use_native(x):
             x = x.contiguous(memory_format=torch.channels_last)
-            x = CF.conv_bn_act(x, self.conv1, self.bn1, relu=True)
-            x = CF.max_pool2d(x, 3, 2, 1)
-            x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
+            # f16x2 engine: every conv weight's operand scale in one launch; each conv module holds
+            # its entry for the duration of this forward (conv_bn_act reads it)
+            convs = [m for m in self.modules() if isinstance(m, nn.Conv2d)]
+            wam = CF.weight_amax([m.weight for m in convs])
+            if wam is not None:
+                for m, a in zip(convs, wam):
+                    m._cdp_wamax = a
+            try:
+                x = CF.conv_bn_act(x, self.conv1, self.bn1, relu=True)
+                x = CF.max_pool2d(x, 3, 2, 1)
+                x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
+            finally:
+                if wam is not None:
+                    for m in convs:
+                        m._cdp_wamax = None
             x = CF.global_avg_pool(x)
             return CF.linear(x, self.fc.weight, self.fc.bias)
         x = self.maxpool(self.relu(self.bn1(self.conv1(x))))

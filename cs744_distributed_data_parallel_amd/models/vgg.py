@@ -76,8 +76,10 @@ class VGG(nn.Module):
         if CF.use_native(x):
             x = x.contiguous(memory_format=torch.channels_last)
             layers = self.layers
-            for ci, bi, pool in self._plan:
-                x = CF.conv_bn_act(x, layers[ci], layers[bi], relu=True, pool=pool)
+            wam = CF.weight_amax([layers[ci].weight for ci, _, _ in self._plan])  # f16x2 operand scales
+            for k, (ci, bi, pool) in enumerate(self._plan):
+                x = CF.conv_bn_act(x, layers[ci], layers[bi], relu=True, pool=pool,
+                                   w_amax=wam[k] if wam is not None else None)
             y = x.reshape(x.size(0), -1)
             return CF.linear(y, self.fc1.weight, self.fc1.bias)
         y = self.layers(x)

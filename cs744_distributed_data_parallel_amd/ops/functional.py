@@ -45,6 +45,31 @@ def _bn_momentum(bn) -> float:
     return -1.0 if bn.momentum is None else float(bn.momentum)
 
 
+# f16x2 conv engine: a tensor produced by one of our kernels carries its producer's partial |max|
+# values (the operand scale of the GEMMs that consume it), tagged with the tensor's version so an
+# in-place change after production invalidates them (the consumer then measures the tensor itself).
+def _get_amax(t):
+    tag = getattr(t, "_cdp_amax", None)
+    if tag is None or tag[1] != t._version:
+        return None
+    return tag[0]
+
+
+def _set_amax(t, amax):
+    if amax is not None:
+        t._cdp_amax = (amax, t._version)
+
+
+def weight_amax(weights):
+    """f16x2 engine: the partial |max| values of a model's conv weights in ONE launch (a list, one
+    entry per weight), for :func:`conv_bn_act`'s ``w_amax``; None for the other engines. Computed
+    from the current weights at every forward, so it is valid whatever changed them."""
+    if not weights or not use_native(weights[0]):
+        return None
+    parts = _native.lib().multi_amax(list(weights))
+    return parts if parts else None
+
+
 # --------------------------------------------------------------------------- conv + BN + act
 class GradSink:
     """Sums the two gradients of a tensor consumed by two fused ops without an autograd add.
@@ -75,16 +100,19 @@ class GradSink:
 class _ConvBNAct(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, b, gamma, beta, rm, rv, nbt, momentum, eps, training, stride, pad, pool, relu, residual,
-                res_sink=None, dx_sink=None):
+                res_sink=None, dx_sink=None, w_amax=None):
         C = _native.lib()
-        out, y, stats, xsave = C.conv_bn_act_fwd(
-            x, w, b, gamma, beta, rm, rv, nbt, momentum, eps, training, stride, pad, pool, relu, residual
+        out, y, stats, xsave, out_amax, x_amax, w_amax = C.conv_bn_act_fwd(
+            x, w, b, gamma, beta, rm, rv, nbt, momentum, eps, training, stride, pad, pool, relu, residual, _get_amax(x),
+            w_amax,
         )
         ctx.cfg = (stride, pad, pool, relu, training, b is not None, residual is not None)
         ctx.params = (w, b, gamma, beta)
         ctx.sinks = (res_sink, dx_sink)
+        ctx.amax = (x_amax, w_amax)  # f16x2 engine only (else None): W and x are unchanged by backward
         zout = out if residual is not None else None
         ctx.save_for_backward(xsave, w, y, stats, zout)  # xsave: x, or x zero-padded to 4k channels
+        _set_amax(out, out_amax)
         return out
 
     @staticmethod
@@ -104,6 +132,7 @@ class _ConvBNAct(torch.autograd.Function):
         dx, dw, db, dgamma, dbeta, dres = C.conv_bn_act_bwd(
             gout, x, w, y, stats, stride, pad, pool, relu, nig[0], has_bias, zout, training,
             _slot(wp, nig[1]), _slot(bp, nig[2] and has_bias), _slot(gp, nig[3]), _slot(betap, nig[4]), addend,
+            *ctx.amax,
         )
         if park_dx:
             dx_sink.grad, dx = dx, None
@@ -121,17 +150,19 @@ class _ConvBNAct(torch.autograd.Function):
             dbeta if ctx.needs_input_grad[4] else None,
             None, None, None, None, None, None, None, None, None, None,
             dres if has_res else None,
-            None, None,
+            None, None, None,
         )
 
 
-def conv_bn_act(x, conv, bn, relu: bool = True, pool: bool = False, residual=None, res_sink=None, dx_sink=None):
+def conv_bn_act(x, conv, bn, relu: bool = True, pool: bool = False, residual=None, res_sink=None, dx_sink=None,
+                w_amax=None):
     """``[maxpool2x2](act(bn(conv(x)) [+ residual]))`` for an ``nn.Conv2d`` / ``nn.BatchNorm2d`` pair.
 
     ``pool`` is the reference's ``MaxPool2d(kernel_size=2, stride=2)``; ``relu`` its
     ``ReLU(inplace=True)``; ``residual`` (ResNet) is added after BN and before the activation.
     ``res_sink`` / ``dx_sink`` (:class:`GradSink`, GPU path only) route the residual gradient of an
     identity block into the data-gradient GEMM of the block's first conv instead of an autograd add.
+    ``w_amax`` (f16x2 engine): ``conv.weight``'s entry of :func:`weight_amax`, else measured here.
     """
     stride = conv.stride[0]
     pad = conv.padding[0]
@@ -157,6 +188,7 @@ def conv_bn_act(x, conv, bn, relu: bool = True, pool: bool = False, residual=Non
             residual,
             res_sink,
             dx_sink,
+            w_amax if w_amax is not None else getattr(conv, "_cdp_wamax", None),
         )
     y = F.conv2d(x, conv.weight, conv.bias, conv.stride, conv.padding)
     y = bn(y)
@@ -236,6 +268,7 @@ class _MaxPool(torch.autograd.Function):
         ctx.save_for_backward(arg)
         ctx.in_shape = list(x.shape)
         ctx.ksp = (k, s, p)
+        _set_amax(y, _get_amax(x))  # max|maxpool(x)| <= max|x|: the input's bound still holds
         return y
 
     @staticmethod

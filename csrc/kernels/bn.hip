@@ -103,12 +103,14 @@ __device__ __forceinline__ float4 affine_act(float4 y, float4 sc, float4 sh, boo
 // out = [pool2](relu(y*scale+shift)) (+ residual before relu when res != null)
 __global__ __launch_bounds__(256) void bn_act_fwd_kernel(const float* __restrict__ y, const float* __restrict__ stats,
                                                          const float* __restrict__ res, float* __restrict__ out,
-                                                         int N, int H, int W, int C, int pool, int relu) {
+                                                         int N, int H, int W, int C, int pool, int relu,
+                                                         float* __restrict__ amax_part) {
   const int C4 = C >> 2;
   const int Ho = pool ? H / 2 : H, Wo = pool ? W / 2 : W;
   const long long total = (long long)N * Ho * Wo * C4;
   const float* scale = stats + 2 * C;
   const float* shift = stats + 3 * C;
+  float am = 0.f;
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
        i += (long long)gridDim.x * blockDim.x) {
     const int c4 = (int)(i % C4);
@@ -124,6 +126,7 @@ __global__ __launch_bounds__(256) void bn_act_fwd_kernel(const float* __restrict
         z.x = fmaxf(z.x, 0.f); z.y = fmaxf(z.y, 0.f); z.z = fmaxf(z.z, 0.f); z.w = fmaxf(z.w, 0.f);
       }
       st4(out + pix * C + 4 * c4, z);
+      am = fmaxf(am, fmaxf(fmaxf(fabsf(z.x), fabsf(z.y)), fmaxf(fabsf(z.z), fabsf(z.w))));
     } else {
       const int wo = (int)(pix % Wo);
       const long long t = pix / Wo;
@@ -140,7 +143,15 @@ __global__ __launch_bounds__(256) void bn_act_fwd_kernel(const float* __restrict
       m.z = fmaxf(fmaxf(z0.z, z1.z), fmaxf(z2.z, z3.z));
       m.w = fmaxf(fmaxf(z0.w, z1.w), fmaxf(z2.w, z3.w));
       st4(out + pix * C + 4 * c4, m);
+      am = fmaxf(am, fmaxf(fmaxf(fabsf(m.x), fabsf(m.y)), fmaxf(fabsf(m.z), fabsf(m.w))));
     }
+  }
+  if (amax_part) {  // |max| of this block's output: operand scale of the consumer's f16x2 GEMMs
+    __shared__ float red[4];
+    am = wave_max(am);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = am;
+    __syncthreads();
+    if (threadIdx.x == 0) amax_part[blockIdx.x] = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
   }
 }
 
@@ -319,8 +330,9 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const float* __restri
                                                            const float* __restrict__ sums, float* __restrict__ dy,
                                                            float* __restrict__ dbias_part, int N, int H, int W,
                                                            int C, int pool, int relu, const float* __restrict__ zout,
-                                                           float* __restrict__ dres) {
+                                                           float* __restrict__ dres, float* __restrict__ amax_part) {
   __shared__ float4 red[256];
+  float am = 0.f;  // |max| of the written dy (operand scale of the f16x2 GEMMs)
   const int C4 = C >> 2;
   const int tid = threadIdx.x;
   const int cq_per_thread = (C4 + 255) / 256;
@@ -360,6 +372,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const float* __restri
         }
         st4(dy + off, o);
         acc.x += o.x; acc.y += o.y; acc.z += o.z; acc.w += o.w;
+        am = fmaxf(am, fmaxf(fmaxf(fabsf(o.x), fabsf(o.y)), fmaxf(fabsf(o.z), fabsf(o.w))));
       };
       for (long long px = (long long)blockIdx.x * ppb + pl; px < npix; px += (long long)gridDim.x * ppb) {
         const float4 g = ld4(gout + px * C + 4 * cq);
@@ -424,6 +437,13 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const float* __restri
     }
     __syncthreads();
   }
+  if (amax_part) {
+    am = wave_max(am);
+    float* r = reinterpret_cast<float*>(red);
+    if ((threadIdx.x & 63) == 0) r[threadIdx.x >> 6] = am;
+    __syncthreads();
+    if (threadIdx.x == 0) amax_part[blockIdx.x] = fmaxf(fmaxf(r[0], r[1]), fmaxf(r[2], r[3]));
+  }
 }
 
 int act_grid(long long work_items) {
@@ -461,11 +481,14 @@ void bn_eval_stats_launch(int C, const float* gamma, const float* beta, const fl
                      stats);
 }
 
+int bn_act_grid(int N, int H, int W, int C, bool pool) {
+  return act_grid((long long)N * (pool ? (H / 2) * (W / 2) : H * W) * (C / 4));
+}
+
 void bn_act_fwd_launch(const float* y, const float* stats, const float* res, float* out, int N, int H, int W, int C,
-                       bool pool, bool relu, hipStream_t st) {
-  const long long items = (long long)N * (pool ? (H / 2) * (W / 2) : H * W) * (C / 4);
-  hipLaunchKernelGGL(bn_act_fwd_kernel, dim3(act_grid(items)), dim3(256), 0, st, y, stats, res, out, N, H, W, C,
-                     pool ? 1 : 0, relu ? 1 : 0);
+                       bool pool, bool relu, hipStream_t st, float* amax_part) {
+  hipLaunchKernelGGL(bn_act_fwd_kernel, dim3(bn_act_grid(N, H, W, C, pool)), dim3(256), 0, st, y, stats, res, out, N,
+                     H, W, C, pool ? 1 : 0, relu ? 1 : 0, amax_part);
 }
 
 void bn_bwd_reduce_launch(const float* y, const float* gout, const float* stats, float* part, int nblocks, int N,
@@ -487,9 +510,9 @@ void chan_finalize_launch(const float* part, int nparts, int C, float* out, floa
 
 void bn_bwd_apply_launch(const float* y, const float* gout, const float* stats, const float* sums, float* dy,
                          float* dbias_part, int nblocks, int N, int H, int W, int C, bool pool, bool relu,
-                         const float* zout, float* dres, hipStream_t st) {
+                         const float* zout, float* dres, hipStream_t st, float* amax_part) {
   hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(nblocks), dim3(256), 0, st, y, gout, stats, sums, dy, dbias_part, N,
-                     H, W, C, pool ? 1 : 0, relu ? 1 : 0, zout, dres);
+                     H, W, C, pool ? 1 : 0, relu ? 1 : 0, zout, dres, amax_part);
 }
 
 }  // namespace cdp

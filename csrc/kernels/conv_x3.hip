@@ -53,11 +53,24 @@ __device__ __forceinline__ void split8(const float (&v)[8], u32x4& s0, u32x4& s1
   }
 }
 
+// Split 8 consecutive-k fp32 values of an operand scaled by s into two fp16x8 planes (f16x2).
+__device__ __forceinline__ void split8h(const float (&v)[8], float s, u32x4& s0, u32x4& s1) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    unsigned a, b;
+    split_pair_h(v[2 * j], v[2 * j + 1], s, a, b);
+    s0[j] = a;
+    s1[j] = b;
+  }
+}
+
 // PS (pre-split): p.x / p.w hold three bf16 planes each ([3][N][H][W][C], [3][Nout][Kdim], as
 // written by split3_launch) and the tiles are copied to LDS without the split (MODE 0 only).
 // ABL (diagnostic builds only): bit 0 drops the in-loop global loads, bit 1 the in-loop LDS stores
-// NP = bf16 planes per operand: 3 = fp32-accurate split (six products), 1 = plain bf16 operands
-// with fp32 accumulation (one product; the non-parity fast mode, CDP_CONV_GEMM=bf16).
+// NP = 16-bit planes per operand: 3 = fp32-accurate bf16 split (six products), 2 = f16x2
+// (power-of-two-scaled operands as two fp16 terms, three products on v_mfma_f32_32x32x16_f16, see
+// x3_common.h), 1 = plain bf16 operands with fp32 accumulation (one product; the non-parity fast
+// mode, CDP_CONV_GEMM=bf16).
 // 8 consecutive-k fp32 values rounded to bf16 (one plane)
 __device__ __forceinline__ u32x4 pack8(const float (&v)[8]) {
   u32x4 r;
@@ -69,7 +82,8 @@ __device__ __forceinline__ u32x4 pack8(const float (&v)[8]) {
 template <int BM, int BN, int MODE, bool DGRAD, bool M16, bool PS = false, int ABL = 0, int NP = 3>
 __global__ __launch_bounds__(waves_m<BM>() * 128, (BM + BN >= 256) ? 1 : 2) void conv_x3_kernel(ConvGemmParams p) {
   static_assert(!PS || MODE == 0, "pre-split operands need C % 32 == 0");
-  static_assert(NP == 3 || (NP == 1 && !PS), "planes");
+  static_assert(NP == 3 || ((NP == 1 || NP == 2) && !PS), "planes");
+  static_assert(NP != 2 || !M16, "f16x2 uses the 32x32x16 tiles");
   constexpr unsigned ES = PS ? 1u : 2u;  // log2 bytes per element of the global operands
   constexpr int WM = waves_m<BM>();  // waves along M (2 x WM waves)
   constexpr int NT = WM * 128;       // threads
@@ -138,6 +152,13 @@ __global__ __launch_bounds__(waves_m<BM>() * 128, (BM + BN >= 256) ? 1 : 2) void
   for (int i = 0; i < B_LD; ++i) {
     const int n = n0 + rrow + RS * i;
     b_off[i] = n < p.Nout ? (unsigned)(mul24(n, p.Kdim) + kq) << ES : kOOB;
+  }
+
+  // f16x2: power-of-two operand scales from the producers' partial maxima (wave-uniform)
+  float sa = 1.f, sb = 1.f;
+  if constexpr (NP == 2) {
+    sa = amax_scale(p.amax_a, p.amax_na);
+    sb = amax_scale(p.amax_b, p.amax_nb);
   }
 
   // byte offset of A row i at filter tap (kh, kw), channel offset c (relative to kq); OOB if padded
@@ -274,6 +295,11 @@ __global__ __launch_bounds__(waves_m<BM>() * 128, (BM + BN >= 256) ? 1 : 2) void
       __bf16* d = st + (rrow + RS * i) * LDH + cp;
       if constexpr (NP == 1) {
         *reinterpret_cast<u32x4*>(d) = pack8(va[i]);
+      } else if constexpr (NP == 2) {
+        u32x4 s0, s1;
+        split8h(va[i], sa, s0, s1);
+        *reinterpret_cast<u32x4*>(d) = s0;
+        *reinterpret_cast<u32x4*>(d + PA) = s1;
       } else {
         u32x4 s0, s1, s2;
         split8(va[i], s0, s1, s2);
@@ -287,6 +313,11 @@ __global__ __launch_bounds__(waves_m<BM>() * 128, (BM + BN >= 256) ? 1 : 2) void
       __bf16* d = st + NP * PA + (rrow + RS * i) * LDH + cp;
       if constexpr (NP == 1) {
         *reinterpret_cast<u32x4*>(d) = pack8(vb[i]);
+      } else if constexpr (NP == 2) {
+        u32x4 s0, s1;
+        split8h(vb[i], sb, s0, s1);
+        *reinterpret_cast<u32x4*>(d) = s0;
+        *reinterpret_cast<u32x4*>(d + PB) = s1;
       } else {
         u32x4 s0, s1, s2;
         split8(vb[i], s0, s1, s2);
@@ -354,6 +385,35 @@ __global__ __launch_bounds__(waves_m<BM>() * 128, (BM + BN >= 256) ? 1 : 2) void
           acc16[a][b] = c;
         }
       }
+    } else if constexpr (NP == 2) {
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        f16x8 af[TM][2], bf[TN][2];
+#pragma unroll
+        for (int a = 0; a < TM; ++a) {
+          const int r = wm * (BM / WM) + a * 32 + l32;
+          const __bf16* src = st + r * LDH + chunk_pos(r, 2 * s + hh) * 8;
+#pragma unroll
+          for (int q = 0; q < 2; ++q) af[a][q] = *reinterpret_cast<const f16x8*>(src + q * PA);
+        }
+#pragma unroll
+        for (int b = 0; b < TN; ++b) {
+          const int r = wn * (BN / 2) + b * 32 + l32;
+          const __bf16* src = st + NP * PA + r * LDH + chunk_pos(r, 2 * s + hh) * 8;
+#pragma unroll
+          for (int q = 0; q < 2; ++q) bf[b][q] = *reinterpret_cast<const f16x8*>(src + q * PB);
+        }
+#pragma unroll
+        for (int a = 0; a < TM; ++a)
+#pragma unroll
+          for (int b = 0; b < TN; ++b) {
+            f32x16 c = acc[a][b];
+            c = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[a][1], bf[b][0], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[a][0], bf[b][1], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[a][0], bf[b][0], c, 0, 0, 0);
+            acc[a][b] = c;
+          }
+      }
     } else {
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
@@ -417,27 +477,35 @@ __global__ __launch_bounds__(waves_m<BM>() * 128, (BM + BN >= 256) ? 1 : 2) void
     if (kt < kt_end) compute(smem);  // odd tile count: the last tile sits in stage 0
   }
 
+  if constexpr (NP == 2) {  // undo the operand scales (exact: powers of two)
+    const float inv = 1.f / (sa * sb);
+#pragma unroll
+    for (int a = 0; a < TM; ++a)
+#pragma unroll
+      for (int b = 0; b < TN; ++b) acc[a][b] *= inv;
+  }
   if constexpr (M16) conv_epilogue16<BM, BN>(p, acc16, reinterpret_cast<float*>(smem), m0, n0, tm_idx, split);
   else conv_epilogue<BM, BN>(p, acc, reinterpret_cast<float*>(smem), m0, n0, tm_idx, split);
 }
 
 template <int BM, int BN, int MODE, bool DGRAD>
-void launch_x3(const ConvGemmParams& p, int ntiles, bool m16, bool bf16, hipStream_t st) {
+void launch_x3(const ConvGemmParams& p, int ntiles, bool m16, int np, hipStream_t st) {
   const dim3 blk(waves_m<BM>() * 128), grd(ntiles * p.splits);
-  if (bf16) hipLaunchKernelGGL((conv_x3_kernel<BM, BN, MODE, DGRAD, false, false, 0, 1>), grd, blk, 0, st, p);
+  if (np == 1) hipLaunchKernelGGL((conv_x3_kernel<BM, BN, MODE, DGRAD, false, false, 0, 1>), grd, blk, 0, st, p);
+  else if (np == 2) hipLaunchKernelGGL((conv_x3_kernel<BM, BN, MODE, DGRAD, false, false, 0, 2>), grd, blk, 0, st, p);
   else if (m16) hipLaunchKernelGGL((conv_x3_kernel<BM, BN, MODE, DGRAD, true>), grd, blk, 0, st, p);
   else hipLaunchKernelGGL((conv_x3_kernel<BM, BN, MODE, DGRAD, false>), grd, blk, 0, st, p);
 }
 
 template <int MODE, bool DGRAD>
-void dispatch_x3(const ConvGemmParams& p, int bm, int bn, bool m16, bool bf16, hipStream_t st) {
+void dispatch_x3(const ConvGemmParams& p, int bm, int bn, bool m16, int np, hipStream_t st) {
   const int ntm = (p.M + bm - 1) / bm, ntn = (p.Nout + bn - 1) / bn;
   const int nt = ntm * ntn;
-  if (bm == 256) launch_x3<256, 128, MODE, DGRAD>(p, nt, m16, bf16, st);
-  else if (bm == 128 && bn == 128) launch_x3<128, 128, MODE, DGRAD>(p, nt, m16, bf16, st);
-  else if (bm == 128 && bn == 64) launch_x3<128, 64, MODE, DGRAD>(p, nt, m16, bf16, st);
-  else if (bm == 64 && bn == 128) launch_x3<64, 128, MODE, DGRAD>(p, nt, m16, bf16, st);
-  else launch_x3<64, 64, MODE, DGRAD>(p, nt, m16, bf16, st);
+  if (bm == 256) launch_x3<256, 128, MODE, DGRAD>(p, nt, m16, np, st);
+  else if (bm == 128 && bn == 128) launch_x3<128, 128, MODE, DGRAD>(p, nt, m16, np, st);
+  else if (bm == 128 && bn == 64) launch_x3<128, 64, MODE, DGRAD>(p, nt, m16, np, st);
+  else if (bm == 64 && bn == 128) launch_x3<64, 128, MODE, DGRAD>(p, nt, m16, np, st);
+  else launch_x3<64, 64, MODE, DGRAD>(p, nt, m16, np, st);
 }
 
 template <int BM, int BN, bool DGRAD>
@@ -476,16 +544,16 @@ void conv_x3ps_launch(const ConvGemmParams& p, int bm, int bn, bool dgrad, hipSt
   else dgrad ? launch_x3ps<64, 64, true>(p, nt, st) : launch_x3ps<64, 64, false>(p, nt, st);
 }
 
-void conv_x3_launch(const ConvGemmParams& p, int bm, int bn, bool dgrad, bool m16, hipStream_t st, bool bf16) {
+void conv_x3_launch(const ConvGemmParams& p, int bm, int bn, bool dgrad, bool m16, hipStream_t st, int np) {
   if ((p.C % BK) == 0 && (p.Kdim % BK) == 0) {
-    if (dgrad) dispatch_x3<0, true>(p, bm, bn, m16, bf16, st);
-    else dispatch_x3<0, false>(p, bm, bn, m16, bf16, st);
+    if (dgrad) dispatch_x3<0, true>(p, bm, bn, m16, np, st);
+    else dispatch_x3<0, false>(p, bm, bn, m16, np, st);
   } else if ((p.C % 4) == 0 && (p.Kdim % 4) == 0) {
-    if (dgrad) dispatch_x3<1, true>(p, bm, bn, m16, bf16, st);
-    else dispatch_x3<1, false>(p, bm, bn, m16, bf16, st);
+    if (dgrad) dispatch_x3<1, true>(p, bm, bn, m16, np, st);
+    else dispatch_x3<1, false>(p, bm, bn, m16, np, st);
   } else {
-    if (dgrad) dispatch_x3<2, true>(p, bm, bn, m16, bf16, st);
-    else dispatch_x3<2, false>(p, bm, bn, m16, bf16, st);
+    if (dgrad) dispatch_x3<2, true>(p, bm, bn, m16, np, st);
+    else dispatch_x3<2, false>(p, bm, bn, m16, np, st);
   }
 }
 

@@ -63,6 +63,11 @@ struct ConvGemmParams {
   int pad_w;    // data gradient, sub-pixel class launches only: column pad (pad is the row pad)
   RowRemap rr;  // sub-pixel class launches: scatter output rows into dX
   const float* addend;  // optional: y += addend (same layout as y; may alias y)
+  // f16x2 engine: partial |max| values of the gathered operand (x / dY) and of the B^T rows,
+  // from their producers; the kernel derives the power-of-two operand scales from them
+  const float* amax_a;
+  const float* amax_b;
+  int amax_na, amax_nb;
 };
 
 struct WgradParams {
@@ -72,15 +77,19 @@ struct WgradParams {
   int N, H, W, C, P, Q, KH, KW, stride, pad;
   int Cout, Kdim, M, splits;
   FastDiv fd_PQ, fd_Q, fd_C, fd_KW;
+  const float* amax_dy;  // f16x2 engine: partial |max| values of dY and of x
+  const float* amax_x;
+  int amax_ndy, amax_nx;
 };
 
 // conv_igemm.hip (exact fp32-input MFMA)
 void conv_igemm_launch(const ConvGemmParams& p, int bm, int bn, bool dgrad, hipStream_t st);
 // conv_x3.hip (fp32-accurate 3-term bf16 split on the bf16 MFMA)
 // (m16: v_mfma_f32_16x16x32_bf16 tiles instead of 32x32x16)
-// (bf16: operands rounded to bf16, one product per MAC -- the non-parity fast mode)
-void conv_x3_launch(const ConvGemmParams& p, int bm, int bn, bool dgrad, bool m16, hipStream_t st,
-                    bool bf16 = false);
+// np = operand planes: 3 = split-bf16 (six products), 2 = f16x2 (power-of-two-scaled operands,
+// two fp16 terms, three products; needs p.amax_*), 1 = operands rounded to bf16, one product per
+// MAC (the non-parity fast mode)
+void conv_x3_launch(const ConvGemmParams& p, int bm, int bn, bool dgrad, bool m16, hipStream_t st, int np = 3);
 // pre-split operands (x, w = three bf16 planes each, from split3_launch); C % 32 == 0 only
 void conv_x3ps_launch(const ConvGemmParams& p, int bm, int bn, bool dgrad, hipStream_t st);
 void split3_launch(const float* x, long long n, void* planes, hipStream_t st);
@@ -90,8 +99,22 @@ void splitk_reduce_launch(const float* slab, int S, int M, int Nout, const float
 int splitk_rows_per_part();
 
 // wgrad.hip
-// x3: fp32-accurate 3-term bf16 split on the bf16 MFMA; otherwise the exact fp32-input MFMA
-void wgrad_launch(const WgradParams& p, int bm, int bn, bool x3, hipStream_t st, bool bf16 = false);
+// x3: the split engines on the 16-bit MFMA (np as for conv_x3_launch); otherwise the exact
+// fp32-input MFMA
+void wgrad_launch(const WgradParams& p, int bm, int bn, bool x3, hipStream_t st, int np = 3);
+// partial |max| of x[0..n) into part[0..nparts) (nparts <= 1024), for operands without a fused
+// producer (the f16x2 engine's scales)
+void amax_launch(const float* x, long long n, float* part, int nparts, hipStream_t st);
+// Many tensors in one launch (a model's conv weights, once per forward): segment i's partials are
+// part[blk0[i] .. blk0[i+1]), one per block.
+constexpr int kMaxAmaxSegs = 64;
+struct MultiAmaxArgs {
+  const float* ptr[kMaxAmaxSegs];
+  long long n[kMaxAmaxSegs];
+  int blk0[kMaxAmaxSegs + 1];
+  int nseg;
+};
+void multi_amax_launch(const MultiAmaxArgs& a, float* part, hipStream_t st);
 void slab_sum_launch(const float* slab, int S, long long n, float* dst, bool accumulate, hipStream_t st);
 void slab_sum_strided_launch(const float* slab, int S, long long n_src, int src_cols, int dst_cols, float* dst,
                              bool accumulate, hipStream_t st);
@@ -103,8 +126,10 @@ void bn_finalize_launch(const float* part, int nparts, int rpp, int M, int C, co
                         float* stats, hipStream_t st);
 void bn_eval_stats_launch(int C, const float* gamma, const float* beta, const float* rm, const float* rv, float eps,
                           float* stats, hipStream_t st);
+// amax_part (optional, bn_act_grid entries): per-block |max| of the written output
+int bn_act_grid(int N, int H, int W, int C, bool pool);
 void bn_act_fwd_launch(const float* y, const float* stats, const float* res, float* out, int N, int H, int W, int C,
-                       bool pool, bool relu, hipStream_t st);
+                       bool pool, bool relu, hipStream_t st, float* amax_part = nullptr);
 void bn_bwd_reduce_launch(const float* y, const float* gout, const float* stats, float* part, int nblocks, int N,
                           int H, int W, int C, bool pool, bool relu, const float* zout, hipStream_t st,
                           bool with_xsum = false);
@@ -113,7 +138,7 @@ void chan_finalize_launch(const float* part, int nparts, int C, float* out, floa
                           long long M = 0, int dbmode = 0);
 void bn_bwd_apply_launch(const float* y, const float* gout, const float* stats, const float* sums, float* dy,
                          float* dbias_part, int nblocks, int N, int H, int W, int C, bool pool, bool relu,
-                         const float* zout, float* dres, hipStream_t st);
+                         const float* zout, float* dres, hipStream_t st, float* amax_part = nullptr);
 
 // misc.hip
 void xent_fwd_launch(const float* logits, const long long* tgt, int B, int C, float* loss, long long* correct,

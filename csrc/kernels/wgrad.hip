@@ -188,7 +188,7 @@ constexpr int XLD = WBK + 8;  // bf16 per LDS row
 // v[r] = row m+r of this thread's 4 columns; write, per column and plane, the RPT m-values
 // (packed bf16 pairs) into the [col][m] image at dst.
 template <int RPT, int NP>
-__device__ __forceinline__ void split_store_cols(const float4 (&v)[RPT], __bf16* dst, int plane) {
+__device__ __forceinline__ void split_store_cols(const float4 (&v)[RPT], __bf16* dst, int plane, float sc = 1.f) {
   // (component access by constant index only: a pointer walk over `v` makes the compiler
   // promote the register array to LDS scratch)
   auto comp = [](const float4& q, int c) { return c == 0 ? q.x : c == 1 ? q.y : c == 2 ? q.z : q.w; };
@@ -198,12 +198,21 @@ __device__ __forceinline__ void split_store_cols(const float4 (&v)[RPT], __bf16*
 #pragma unroll
     for (int r = 0; r < RPT / 2; ++r) {
       if constexpr (NP == 1) h0[r] = pack_bf16x2(f32x2{comp(v[2 * r], c), comp(v[2 * r + 1], c)});
+      else if constexpr (NP == 2) split_pair_h(comp(v[2 * r], c), comp(v[2 * r + 1], c), sc, h0[r], h1[r]);
       else split_pair(comp(v[2 * r], c), comp(v[2 * r + 1], c), h0[r], h1[r], h2[r]);
     }
     __bf16* d = dst + c * XLD;
     if constexpr (NP == 1) {
       if constexpr (RPT == 4) *reinterpret_cast<uint2*>(d) = make_uint2(h0[0], h0[1]);
       else *reinterpret_cast<unsigned*>(d) = h0[0];
+    } else if constexpr (NP == 2) {
+      if constexpr (RPT == 4) {
+        *reinterpret_cast<uint2*>(d) = make_uint2(h0[0], h0[1]);
+        *reinterpret_cast<uint2*>(d + plane) = make_uint2(h1[0], h1[1]);
+      } else {
+        *reinterpret_cast<unsigned*>(d) = h0[0];
+        *reinterpret_cast<unsigned*>(d + plane) = h1[0];
+      }
     } else if constexpr (RPT == 4) {
       *reinterpret_cast<uint2*>(d) = make_uint2(h0[0], h0[1]);
       *reinterpret_cast<uint2*>(d + plane) = make_uint2(h1[0], h1[1]);
@@ -216,7 +225,9 @@ __device__ __forceinline__ void split_store_cols(const float4 (&v)[RPT], __bf16*
   }
 }
 
-template <int BM, int BN, bool FAST, int NP = 3>  // NP = 1: plain bf16 operands (non-parity mode)
+// NP = 3: split-bf16 (six products); 2: f16x2 (scaled operands, two fp16 terms, three products on
+// v_mfma_f32_32x32x16_f16, see x3_common.h); 1: plain bf16 operands (non-parity mode)
+template <int BM, int BN, bool FAST, int NP = 3>
 __global__ __launch_bounds__(256, 2) void wgrad_x3_kernel(WgradParams p) {
   constexpr int TM = BM / 64, TN = BN / 64;
   constexpr int PA = BM * XLD, PB = BN * XLD;
@@ -262,6 +273,11 @@ __global__ __launch_bounds__(256, 2) void wgrad_x3_kernel(WgradParams p) {
   for (int i = 0; i < RPT_A; ++i)
     a_off[i] = co < p.Cout ? (unsigned)(mul24(a_mq * RPT_A + i, p.Cout) + co) * 4u : kOOB;
   const __amdgpu_buffer_rsrc_t xr = make_rsrc(p.x, (unsigned)p.N * (unsigned)HWC * 4u);
+  float sa = 1.f, sb = 1.f;  // f16x2 operand scales (dY, x)
+  if constexpr (NP == 2) {
+    sa = amax_scale(p.amax_dy, p.amax_ndy);
+    sb = amax_scale(p.amax_x, p.amax_nx);
+  }
 
   float4 ra[RPT_A], rb[RPT_B];
   auto load_tile = [&](int kt) {
@@ -322,8 +338,8 @@ __global__ __launch_bounds__(256, 2) void wgrad_x3_kernel(WgradParams p) {
     }
   };
   auto store_tile = [&]() {
-    split_store_cols<RPT_A, NP>(ra, As + (a_cg * 4) * XLD + a_mq * RPT_A, PA);
-    split_store_cols<RPT_B, NP>(rb, Bs + (b_cg * 4) * XLD + b_mq * RPT_B, PB);
+    split_store_cols<RPT_A, NP>(ra, As + (a_cg * 4) * XLD + a_mq * RPT_A, PA, sa);
+    split_store_cols<RPT_B, NP>(rb, Bs + (b_cg * 4) * XLD + b_mq * RPT_B, PB, sb);
   };
 
   f32x16 acc[TM][TN];
@@ -345,6 +361,32 @@ __global__ __launch_bounds__(256, 2) void wgrad_x3_kernel(WgradParams p) {
       if (more) load_tile(kt + 1);
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
+        if constexpr (NP == 2) {
+          f16x8 af[TM][2], bf[TN][2];
+#pragma unroll
+          for (int a = 0; a < TM; ++a) {
+            const __bf16* src = As + (wm * (BM / 2) + a * 32 + l32) * XLD + s * 16 + koff;
+#pragma unroll
+            for (int q = 0; q < 2; ++q) af[a][q] = *reinterpret_cast<const f16x8*>(src + q * PA);
+          }
+#pragma unroll
+          for (int b = 0; b < TN; ++b) {
+            const __bf16* src = Bs + (wn * (BN / 2) + b * 32 + l32) * XLD + s * 16 + koff;
+#pragma unroll
+            for (int q = 0; q < 2; ++q) bf[b][q] = *reinterpret_cast<const f16x8*>(src + q * PB);
+          }
+#pragma unroll
+          for (int a = 0; a < TM; ++a)
+#pragma unroll
+            for (int b = 0; b < TN; ++b) {
+              f32x16 c = acc[a][b];
+              c = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[a][1], bf[b][0], c, 0, 0, 0);
+              c = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[a][0], bf[b][1], c, 0, 0, 0);
+              c = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[a][0], bf[b][0], c, 0, 0, 0);
+              acc[a][b] = c;
+            }
+          continue;
+        }
         bf16x8 af[TM][3], bf[TN][3];
 #pragma unroll
         for (int a = 0; a < TM; ++a) {
@@ -384,6 +426,13 @@ __global__ __launch_bounds__(256, 2) void wgrad_x3_kernel(WgradParams p) {
     }
   }
 
+  if constexpr (NP == 2) {  // undo the operand scales (exact: powers of two)
+    const float inv = 1.f / (sa * sb);
+#pragma unroll
+    for (int a = 0; a < TM; ++a)
+#pragma unroll
+      for (int b = 0; b < TN; ++b) acc[a][b] *= inv;
+  }
   float* out = p.out + (long long)split * p.Cout * p.Kdim;
   const bool full = co0 + BM <= p.Cout && r0 + BN <= p.Kdim;
   auto store = [&](auto pred) {  // unpredicated stores for in-bounds tiles
@@ -488,15 +537,18 @@ __global__ __launch_bounds__(256) void slab_sum4_kernel(const float4* __restrict
 }  // namespace
 
 template <int BM, int BN>
-void wgrad_launch_t(const WgradParams& p, bool x3, hipStream_t st, bool bf16) {
+void wgrad_launch_t(const WgradParams& p, bool x3, hipStream_t st, int np) {
   const int ntn = (p.Kdim + BN - 1) / BN;
   const int ntm = (p.Cout + BM - 1) / BM;
   const bool fast = (p.C % 4) == 0 && (p.Cout % 4) == 0;
   dim3 grid(ntm * ntn * p.splits);
   if (x3) {
-    if (bf16) {
+    if (np == 1) {
       if (fast) hipLaunchKernelGGL((wgrad_x3_kernel<BM, BN, true, 1>), grid, dim3(256), 0, st, p);
       else hipLaunchKernelGGL((wgrad_x3_kernel<BM, BN, false, 1>), grid, dim3(256), 0, st, p);
+    } else if (np == 2) {
+      if (fast) hipLaunchKernelGGL((wgrad_x3_kernel<BM, BN, true, 2>), grid, dim3(256), 0, st, p);
+      else hipLaunchKernelGGL((wgrad_x3_kernel<BM, BN, false, 2>), grid, dim3(256), 0, st, p);
     } else if (fast) hipLaunchKernelGGL((wgrad_x3_kernel<BM, BN, true>), grid, dim3(256), 0, st, p);
     else hipLaunchKernelGGL((wgrad_x3_kernel<BM, BN, false>), grid, dim3(256), 0, st, p);
   } else {
@@ -505,11 +557,74 @@ void wgrad_launch_t(const WgradParams& p, bool x3, hipStream_t st, bool bf16) {
   }
 }
 
-void wgrad_launch(const WgradParams& p, int bm, int bn, bool x3, hipStream_t st, bool bf16) {
-  if (bm == 128 && bn == 128) wgrad_launch_t<128, 128>(p, x3, st, bf16);
-  else if (bm == 128) wgrad_launch_t<128, 64>(p, x3, st, bf16);
-  else if (bn == 128) wgrad_launch_t<64, 128>(p, x3, st, bf16);
-  else wgrad_launch_t<64, 64>(p, x3, st, bf16);
+void wgrad_launch(const WgradParams& p, int bm, int bn, bool x3, hipStream_t st, int np) {
+  if (bm == 128 && bn == 128) wgrad_launch_t<128, 128>(p, x3, st, np);
+  else if (bm == 128) wgrad_launch_t<128, 64>(p, x3, st, np);
+  else if (bn == 128) wgrad_launch_t<64, 128>(p, x3, st, np);
+  else wgrad_launch_t<64, 64>(p, x3, st, np);
+}
+
+// ---------------------------------------------------------------- operand |max| partials
+namespace {
+__global__ __launch_bounds__(256) void amax_kernel(const float* __restrict__ x, long long n, float* __restrict__ part) {
+  __shared__ float red[4];
+  float m = 0.f;
+  const long long stride = (long long)gridDim.x * 256;
+  long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  if ((reinterpret_cast<uintptr_t>(x) & 15) == 0) {
+    const long long n4 = n >> 2;
+    const float4* x4 = reinterpret_cast<const float4*>(x);
+    for (long long j = i; j < n4; j += stride) {
+      const float4 v = x4[j];
+      m = fmaxf(m, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+    }
+    for (long long j = (n4 << 2) + i; j < n; j += stride) m = fmaxf(m, fabsf(x[j]));
+  } else {
+    for (long long j = i; j < n; j += stride) m = fmaxf(m, fabsf(x[j]));
+  }
+  m = wave_max(m);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) part[blockIdx.x] = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+}
+
+// block b of segment i (blk0[i] <= b < blk0[i+1]) reduces a strided share of tensor i
+__global__ __launch_bounds__(256) void multi_amax_kernel(MultiAmaxArgs a, float* __restrict__ part) {
+  __shared__ float red[4];
+  const int b = blockIdx.x;
+  int seg = 0;
+  while (seg + 1 < a.nseg && a.blk0[seg + 1] <= b) ++seg;
+  const int nb = a.blk0[seg + 1] - a.blk0[seg];
+  const float* x = a.ptr[seg];
+  const long long n = a.n[seg];
+  const long long stride = (long long)nb * 256;
+  float m = 0.f;
+  const long long i = (long long)(b - a.blk0[seg]) * 256 + threadIdx.x;
+  if ((reinterpret_cast<uintptr_t>(x) & 15) == 0) {
+    const long long n4 = n >> 2;
+    const float4* x4 = reinterpret_cast<const float4*>(x);
+    for (long long j = i; j < n4; j += stride) {
+      const float4 v = x4[j];
+      m = fmaxf(m, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+    }
+    for (long long j = (n4 << 2) + i; j < n; j += stride) m = fmaxf(m, fabsf(x[j]));
+  } else {
+    for (long long j = i; j < n; j += stride) m = fmaxf(m, fabsf(x[j]));
+  }
+  m = wave_max(m);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) part[b] = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+}
+}  // namespace
+
+void amax_launch(const float* x, long long n, float* part, int nparts, hipStream_t st) {
+  hipLaunchKernelGGL(amax_kernel, dim3(nparts), dim3(256), 0, st, x, n, part);
+}
+
+void multi_amax_launch(const MultiAmaxArgs& a, float* part, hipStream_t st) {
+  if (a.nseg <= 0) return;
+  hipLaunchKernelGGL(multi_amax_kernel, dim3(a.blk0[a.nseg]), dim3(256), 0, st, a, part);
 }
 
 void slab_sum_launch(const float* slab, int S, long long n, float* dst, bool accumulate, hipStream_t st) {

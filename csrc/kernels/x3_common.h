@@ -33,6 +33,48 @@ __device__ __forceinline__ void split_pair(float x, float y, unsigned& h0, unsig
   h2 = pack_bf16x2(r2);
 }
 
+// ---- f16x2 engine: two fp16 terms of a power-of-two-scaled operand ------------------------
+//
+//   s*x = h0 + h1 + r,  h0 = rn_f16(s*x), h1 = rn_f16(s*x - h0),  |r| <= 2^-22 |s*x|
+//
+// fp16 keeps 11 significant bits, so two terms carry 22 -- against 24 for fp32 and 3 x 8 for
+// the bf16 split -- and the product needs three MFMA terms (h0g0 + h0g1 + h1g0, dropped
+// h1g1 <= 2^-22 |ab|) instead of six. fp16's 5-bit exponent is what the per-tensor scale s = 2^e
+// is for: it maps the tensor's |max| to [2^14, 2^15), so nothing overflows and everything within
+// 2^18 of the max keeps all 22 bits (smaller values degrade gracefully to an absolute error of
+// 2^-40 max|x|, far below the fp32 accumulation error of the dot products they enter). s is
+// exact, so dividing the accumulator by s_a s_b in the epilogue is exact too.
+typedef _Float16 f16x2_v __attribute__((ext_vector_type(2)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ unsigned pack_f16x2(f32x2 v) {
+  return __builtin_bit_cast(unsigned, __builtin_convertvector(v, f16x2_v));
+}
+__device__ __forceinline__ f32x2 widen_f16x2(unsigned h) {
+  return __builtin_convertvector(__builtin_bit_cast(f16x2_v, h), f32x2);
+}
+// v_pk_mul, v_cvt_pk_f16_f32, 2 x v_cvt_f32_f16, v_pk_fma, v_cvt_pk_f16_f32: 6 VALU per pair
+__device__ __forceinline__ void split_pair_h(float x, float y, float s, unsigned& h0, unsigned& h1) {
+  const f32x2 v = f32x2{x, y} * s;
+  h0 = pack_f16x2(v);
+  h1 = pack_f16x2(v - widen_f16x2(h0));
+}
+
+// Power-of-two operand scale from a producer's partial |max| values part[0..n): maps the max to
+// [2^14, 2^15). Every lane of the calling wave gets the same value (no LDS, no barrier). A zero,
+// inf or NaN max gives 1 (zeros stay zeros; non-finite inputs propagate as in fp32).
+__device__ __forceinline__ float amax_scale(const float* __restrict__ part, int n) {
+  const int lane = threadIdx.x & 63;
+  float m = 0.f;
+  for (int i = lane; i < n; i += 64) m = fmaxf(m, part[i]);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+  if (!(m > 0.f) || !(m < 3.0e38f)) return 1.f;
+  int e;
+  (void)frexpf(m, &e);  // m < 2^e
+  return ldexpf(1.f, max(-100, min(100, 15 - e)));
+}
+
 // Raw buffer resource over [base, base + bytes): loads past `bytes` return 0 (hardware range
 // check), which implements the implicit-GEMM zero padding without branches or selects.
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, unsigned bytes) {

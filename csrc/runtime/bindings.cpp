@@ -14,21 +14,29 @@ PYBIND11_MODULE(_C, m) {
   m.attr("ARCH") = "gfx950";
 
   // -------------------------------------------------------------- kernels
-  m.def("set_conv_gemm", &set_conv_gemm, py::arg("mode"), "select the conv GEMM engine: x3 (3-term bf16 split, fp32-accurate) or f32 (exact fp32 MFMA)");
+  m.def("set_conv_gemm", &set_conv_gemm, py::arg("mode"),
+        "select the conv GEMM engine: x3 (3-term bf16 split), f16x2 (scaled 2-term fp16 split), f32 (exact fp32 "
+        "MFMA) or bf16 (bf16 operands, non-parity)");
   m.def("get_conv_gemm", &get_conv_gemm);
   m.def("bench_presplit", &bench_presplit, "experiment: in-kernel split vs pre-split bf16 planes (conv fwd GEMM)");
   m.def("conv2d_fwd", &conv2d_fwd, py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("stride"), py::arg("pad"),
-        py::arg("want_stats") = false);
+        py::arg("want_stats") = false, py::arg("x_amax") = py::none(), py::arg("w_amax") = py::none());
   m.def("conv2d_dgrad", &conv2d_dgrad, py::arg("dy"), py::arg("w"), py::arg("in_shape"), py::arg("stride"),
-        py::arg("pad"), py::arg("addend") = py::none());
+        py::arg("pad"), py::arg("addend") = py::none(), py::arg("dy_amax") = py::none(), py::arg("w_amax") = py::none());
   m.def("conv2d_wgrad", &conv2d_wgrad, py::arg("dy"), py::arg("x"), py::arg("w_shape"), py::arg("stride"),
-        py::arg("pad"), py::arg("out") = py::none(), py::arg("accumulate") = false);
-  m.def("conv_bn_act_fwd", &conv_bn_act_fwd);
+        py::arg("pad"), py::arg("out") = py::none(), py::arg("accumulate") = false, py::arg("dy_amax") = py::none(),
+        py::arg("x_amax") = py::none());
+  m.def("conv_bn_act_fwd", &conv_bn_act_fwd, py::arg("x"), py::arg("w"), py::arg("b"), py::arg("gamma"),
+        py::arg("beta"), py::arg("running_mean"), py::arg("running_var"), py::arg("num_batches_tracked"),
+        py::arg("momentum"), py::arg("eps"), py::arg("training"), py::arg("stride"), py::arg("pad"), py::arg("pool"),
+        py::arg("relu"), py::arg("residual"), py::arg("x_amax") = py::none(), py::arg("w_amax") = py::none());
+  m.def("multi_amax", &multi_amax, py::arg("tensors"),
+        "f16x2 engine: partial |max| values of many tensors in one launch (empty list for other engines)");
   m.def("conv_bn_act_bwd", &conv_bn_act_bwd, py::arg("gout"), py::arg("x"), py::arg("w"), py::arg("y"),
         py::arg("stats"), py::arg("stride"), py::arg("pad"), py::arg("pool"), py::arg("relu"), py::arg("need_dx"),
         py::arg("has_bias"), py::arg("zout") = py::none(), py::arg("training") = true, py::arg("dw_out") = py::none(),
         py::arg("db_out") = py::none(), py::arg("dgamma_out") = py::none(), py::arg("dbeta_out") = py::none(),
-        py::arg("dx_addend") = py::none());
+        py::arg("dx_addend") = py::none(), py::arg("x_amax") = py::none(), py::arg("w_amax") = py::none());
   m.def("linear_fwd", &linear_fwd);
   m.def("linear_bwd", &linear_bwd, py::arg("gy"), py::arg("x"), py::arg("w"), py::arg("need_dx"),
         py::arg("has_bias"), py::arg("dw_out") = py::none(), py::arg("db_out") = py::none());

@@ -59,20 +59,88 @@ int num_cus() {
   return cus;
 }
 
-// Conv GEMM engine: 1 = 3-term bf16 split on the bf16 MFMA (conv_x3.hip, fp32-accurate, default),
-// 0 = exact fp32-input MFMA (conv_igemm.hip), 2 = plain bf16 operands with fp32 accumulation
-// (same kernels, one product per MAC: the fast non-parity mode). CDP_CONV_GEMM=f32|bf16 selects
-// at start-up; set_conv_gemm at run time.
+// Conv GEMM engine:
+//   3 = f16x2 (default): power-of-two-scaled operands as two fp16 terms, three products on the
+//       fp16 MFMA (conv_x3.hip / wgrad.hip with NP = 2, see x3_common.h); its error against fp64
+//       is at or below the exact fp32 MFMA's on every conv shape class (tests/test_kernels_gpu.py)
+//   1 = x3: 3-term bf16 split, six products on the bf16 MFMA (same kernels, NP = 3), as accurate
+//   0 = exact fp32-input MFMA (conv_igemm.hip)
+//   2 = plain bf16 operands with fp32 accumulation (one product per MAC: the non-parity fast mode)
+// CDP_CONV_GEMM=f16x2|x3|f32|bf16 selects at start-up; set_conv_gemm at run time.
 int& conv_gemm_mode() {
   static int m = [] {
     const char* e = std::getenv("CDP_CONV_GEMM");
     if (e && std::string(e) == "f32") return 0;
     if (e && std::string(e) == "bf16") return 2;
-    return 1;
+    if (e && std::string(e) == "x3") return 1;
+    return 3;
   }();
   return m;
 }
 bool x3_family() { return conv_gemm_mode() != 0; }
+bool f16x2_mode() { return conv_gemm_mode() == 3; }
+// 16-bit operand planes of the split kernels for the current engine
+int split_planes() { return conv_gemm_mode() == 2 ? 1 : conv_gemm_mode() == 3 ? 2 : 3; }
+
+// Partial |max| values of an f16x2 GEMM operand: the producer's (when the caller has them) or a
+// standalone pass. Undefined outside the f16x2 engine.
+at::Tensor amax_parts(const at::Tensor& t, const c10::optional<at::Tensor>& given, hipStream_t st) {
+  if (!f16x2_mode()) return at::Tensor();
+  if (given.has_value() && given->defined()) return *given;
+  const long long n = t.numel();
+  const int nparts = (int)std::max<long long>(1, std::min<long long>(1024, (n + 8191) / 8192));
+  at::Tensor part = at::empty({nparts}, t.options().dtype(at::kFloat));
+  amax_launch(t.data_ptr<float>(), n, part.data_ptr<float>(), nparts, st);
+  return part;
+}
+}  // namespace
+
+// Partial |max| values of many tensors in one launch per 64 (a model's conv weights, once per
+// forward): returns one view of partials per tensor, or an empty list outside the f16x2 engine.
+std::vector<at::Tensor> multi_amax(const std::vector<at::Tensor>& ts) {
+  std::vector<at::Tensor> out;
+  if (!f16x2_mode() || ts.empty()) return out;
+  hipStream_t st = cur_stream();
+  for (size_t s0 = 0; s0 < ts.size(); s0 += kMaxAmaxSegs) {
+    const size_t ns = std::min<size_t>(kMaxAmaxSegs, ts.size() - s0);
+    MultiAmaxArgs a{};
+    a.nseg = (int)ns;
+    std::vector<at::Tensor> keep;
+    int tot = 0;
+    for (size_t i = 0; i < ns; ++i) {
+      at::Tensor t = ts[s0 + i];
+      check_f32_cuda(t, "multi_amax input");
+      if (!t.is_contiguous() && !t.is_contiguous(at::MemoryFormat::ChannelsLast)) t = t.contiguous();
+      keep.push_back(t);
+      a.ptr[i] = t.data_ptr<float>();
+      a.n[i] = t.numel();
+      a.blk0[i] = tot;
+      tot += (int)std::max<long long>(1, std::min<long long>(128, (t.numel() + 32767) / 32768));
+    }
+    a.blk0[ns] = tot;
+    at::Tensor part = at::empty({tot}, ts[s0].options());
+    multi_amax_launch(a, part.data_ptr<float>(), st);
+    for (size_t i = 0; i < ns; ++i) out.push_back(part.narrow(0, a.blk0[i], a.blk0[i + 1] - a.blk0[i]));
+  }
+  return out;
+}
+
+namespace {
+
+void set_amax(ConvGemmParams& p, const at::Tensor& a, const at::Tensor& b) {
+  if (!a.defined() || !b.defined()) return;
+  p.amax_a = a.data_ptr<float>();
+  p.amax_na = (int)a.numel();
+  p.amax_b = b.data_ptr<float>();
+  p.amax_nb = (int)b.numel();
+}
+void set_amax(WgradParams& p, const at::Tensor& dy, const at::Tensor& x) {
+  if (!dy.defined() || !x.defined()) return;
+  p.amax_dy = dy.data_ptr<float>();
+  p.amax_ndy = (int)dy.numel();
+  p.amax_x = x.data_ptr<float>();
+  p.amax_nx = (int)x.numel();
+}
 
 // The x3 kernels address through 32-bit buffer offsets and 24-bit index multiplies; shapes past
 // those limits (or a strided data-gradient other than stride 2) take the exact fp32 kernels.
@@ -94,16 +162,23 @@ void conv_launch(const ConvGemmParams& p, int bm, int bn, bool dgrad, hipStream_
     const char* e = std::getenv("CDP_MFMA16");
     return e && e[0] == '1';  // measured: 16x16x32 tiles ran ~2% slower on VGG-11
   }();
-  if (x3_family() && x3_ok(p, dgrad)) conv_x3_launch(p, bm, bn, dgrad, m16, st, conv_gemm_mode() == 2);
+  if (x3_family() && x3_ok(p, dgrad)) {
+    TORCH_CHECK(!f16x2_mode() || (p.amax_a && p.amax_b), "f16x2 conv GEMM launched without operand maxima");
+    conv_x3_launch(p, bm, bn, dgrad, m16 && !f16x2_mode(), st, split_planes());
+  }
   else conv_igemm_launch(p, bm, bn, dgrad, st);
 }
 
 // Workgroups each kernel keeps resident per CU (min of the LDS and VGPR limits of the build).
 int conv_blocks_per_cu(int bm, int bn) {
+  if (f16x2_mode()) return (bm + bn) >= 384 ? 1 : (bm + bn) >= 256 ? 2 : 3;  // 2 x 2 x (bm+bn) x 64 B
   if (x3_family()) return (bm + bn) >= 256 ? 1 : (bm + bn) >= 192 ? 2 : 3;  // 2 x 3 x (bm+bn) x 64 B
   return std::max(1, std::min(4, (160 * 1024) / (2 * (bm + bn) * 36 * 4)));
 }
-double conv_mfma_rate() { return conv_gemm_mode() == 1 ? 250.0e12 : conv_gemm_mode() == 2 ? 800.0e12 : 120.0e12; }
+double conv_mfma_rate() {
+  const int m = conv_gemm_mode();
+  return m == 1 ? 250.0e12 : m == 2 ? 800.0e12 : m == 3 ? 450.0e12 : 120.0e12;
+}
 int wgrad_blocks_per_cu(int bm, int bn) {
   if (x3_family()) return (bm + bn) >= 256 ? 2 : (bm + bn) >= 192 ? 3 : 5;
   return std::max(1, std::min(4, (160 * 1024) / (2 * 32 * (bm + bn + 8) * 4)));
@@ -247,20 +322,21 @@ at::Tensor pad_channels4(const at::Tensor& t) {
 }  // namespace
 
 void set_conv_gemm(const std::string& mode) {
-  TORCH_CHECK(mode == "x3" || mode == "f32" || mode == "bf16", "conv gemm engine must be 'x3', 'f32' or 'bf16', got ",
-              mode);
-  conv_gemm_mode() = mode == "x3" ? 1 : mode == "bf16" ? 2 : 0;
+  TORCH_CHECK(mode == "x3" || mode == "f32" || mode == "bf16" || mode == "f16x2",
+              "conv gemm engine must be 'x3', 'f16x2', 'f32' or 'bf16', got ", mode);
+  conv_gemm_mode() = mode == "x3" ? 1 : mode == "bf16" ? 2 : mode == "f16x2" ? 3 : 0;
 }
 std::string get_conv_gemm() {
   const int m = conv_gemm_mode();
-  return m == 1 ? "x3" : m == 2 ? "bf16" : "f32";
+  return m == 1 ? "x3" : m == 2 ? "bf16" : m == 3 ? "f16x2" : "f32";
 }
 
 // ---------------------------------------------------------------- conv forward
 // Returns y (channels_last [N, Cout, P, Q]). When `part` is requested the per-tile BatchNorm
 // partials are returned in a second tensor [nparts, Cout, 2] together with rows-per-part.
 std::vector<at::Tensor> conv2d_fwd(const at::Tensor& x_, const at::Tensor& w_, const c10::optional<at::Tensor>& bias,
-                                   int64_t stride, int64_t pad, bool want_stats) {
+                                   int64_t stride, int64_t pad, bool want_stats, const c10::optional<at::Tensor>& x_amax,
+                                   const c10::optional<at::Tensor>& w_amax) {
   check_f32_cuda(x_, "x");
   check_f32_cuda(w_, "weight");
   TORCH_CHECK(x_.dim() == 4 && w_.dim() == 4, "conv2d_fwd expects 4-D input and weight");
@@ -287,6 +363,8 @@ std::vector<at::Tensor> conv2d_fwd(const at::Tensor& x_, const at::Tensor& w_, c
   set_divs(p);
   at::Tensor part, rpp;
   hipStream_t st = cur_stream();
+  const at::Tensor xa = amax_parts(x, x_amax, st), wa = amax_parts(w, w_amax, st);
+  set_amax(p, xa, wa);
   if (g.splits == 1) {
     p.y = y.data_ptr<float>();
     p.bias = fptr(bias);
@@ -332,7 +410,7 @@ bool subpixel_enabled() {
 }
 
 bool conv2d_dgrad_subpixel(const at::Tensor& dy, const at::Tensor& w, at::Tensor& dx, int pad, hipStream_t st,
-                           const float* addend) {
+                           const float* addend, const at::Tensor& dya, const at::Tensor& wa) {
   const int N = dx.size(0), C = dx.size(1), H = dx.size(2), W = dx.size(3);
   const int Co = w.size(0), KH = w.size(2), KW = w.size(3);
   const int P = dy.size(2), Q = dy.size(3);
@@ -355,6 +433,7 @@ bool conv2d_dgrad_subpixel(const at::Tensor& dy, const at::Tensor& w, at::Tensor
       set_divs(p);
       p.rr = RowRemap{1, H, W, ph, pw, Hc, Wc, make_fastdiv(Hc * Wc), make_fastdiv(Wc)};
       p.x = dy.data_ptr<float>();
+      set_amax(p, dya, wa);  // a sub-filter's |max| is bounded by the whole filter's
       if (!x3_ok(p, true)) return false;
       at::Tensor wt;
       if (Kc > 0) {
@@ -388,7 +467,8 @@ bool conv2d_dgrad_subpixel(const at::Tensor& dy, const at::Tensor& w, at::Tensor
 
 // dX[N, C, H, W] from dY[N, Co, P, Q] and W[Co, C, KH, KW] (any stride / padding).
 at::Tensor conv2d_dgrad(const at::Tensor& dy_, const at::Tensor& w_, std::vector<int64_t> in_shape, int64_t stride,
-                        int64_t pad, const c10::optional<at::Tensor>& addend) {
+                        int64_t pad, const c10::optional<at::Tensor>& addend, const c10::optional<at::Tensor>& dy_amax,
+                        const c10::optional<at::Tensor>& w_amax) {
   check_f32_cuda(dy_, "grad_output");
   check_f32_cuda(w_, "weight");
   const at::Tensor dy = nhwc(dy_);
@@ -406,9 +486,10 @@ at::Tensor conv2d_dgrad(const at::Tensor& dy_, const at::Tensor& w_, std::vector
                     addend->size(0) == N && addend->size(1) == C && addend->size(2) == H && addend->size(3) == W,
                 "dgrad addend must be a channels_last fp32 tensor of the input's shape");
   const float* addp = has_add ? addend->data_ptr<float>() : nullptr;
+  const at::Tensor dya = amax_parts(dy, dy_amax, st), wa = amax_parts(w, w_amax, st);  // |max| W^T = |max| W
   if (stride == 2 && x3_family() && subpixel_enabled()) {
     at::Tensor dx = has_add ? *addend : at::empty({N, C, H, W}, opts.memory_format(at::MemoryFormat::ChannelsLast));
-    if (conv2d_dgrad_subpixel(dy, w, dx, (int)pad, st, addp)) return dx;
+    if (conv2d_dgrad_subpixel(dy, w, dx, (int)pad, st, addp, dya, wa)) return dx;
   }
   // Wt[ci][tap][co] = W[co][tap][ci]
   at::Tensor wt = at::empty({C, KH * KW * Co}, opts);
@@ -424,6 +505,7 @@ at::Tensor conv2d_dgrad(const at::Tensor& dy_, const at::Tensor& w_, std::vector
   p.KH = KH; p.KW = KW; p.stride = (int)stride; p.pad = (int)pad; p.pad_w = (int)pad;
   p.Nout = C; p.M = (int)M; p.Kdim = Kdim; p.ktiles = g.ktiles; p.splits = g.splits;
   set_divs(p);
+  set_amax(p, dya, wa);
   if (g.splits == 1) {
     p.y = dx.data_ptr<float>();
     p.addend = addp;
@@ -441,15 +523,17 @@ at::Tensor conv2d_dgrad(const at::Tensor& dy_, const at::Tensor& w_, std::vector
 // ---------------------------------------------------------------- conv weight gradient
 // dW (channels_last [Co, C, KH, KW]); written into `out` when given (accumulating if asked).
 at::Tensor conv2d_wgrad(const at::Tensor& dy_, const at::Tensor& x_, std::vector<int64_t> w_shape, int64_t stride,
-                        int64_t pad, const c10::optional<at::Tensor>& out, bool accumulate) {
-  return conv2d_wgrad_keep(dy_, x_, w_shape, stride, pad, out, accumulate, -1);
+                        int64_t pad, const c10::optional<at::Tensor>& out, bool accumulate,
+                        const c10::optional<at::Tensor>& dy_amax, const c10::optional<at::Tensor>& x_amax) {
+  return conv2d_wgrad_keep(dy_, x_, w_shape, stride, pad, out, accumulate, -1, dy_amax, x_amax);
 }
 
 // keep_c >= 0: x carries zero-padded channels; only the first keep_c input channels of dW are
 // written (the strip is fused into the split-K slab reduction).
 at::Tensor conv2d_wgrad_keep(const at::Tensor& dy_, const at::Tensor& x_, std::vector<int64_t> w_shape,
                              int64_t stride, int64_t pad, const c10::optional<at::Tensor>& out, bool accumulate,
-                             int64_t keep_c) {
+                             int64_t keep_c, const c10::optional<at::Tensor>& dy_amax,
+                             const c10::optional<at::Tensor>& x_amax) {
   check_f32_cuda(dy_, "grad_output");
   check_f32_cuda(x_, "input");
   const at::Tensor dy = nhwc(dy_);
@@ -480,13 +564,15 @@ at::Tensor conv2d_wgrad_keep(const at::Tensor& dy_, const at::Tensor& x_, std::v
   const WgradPlan wp = plan_wgrad(Co, Kdim, M);
   p.splits = wp.splits;
   set_divs(p);
+  const at::Tensor dya = amax_parts(dy, dy_amax, st), xa = amax_parts(x, x_amax, st);
+  set_amax(p, dya, xa);
   if (p.splits == 1 && !accumulate && Ckeep == C) {
     p.out = dw.data_ptr<float>();
-    wgrad_launch(p, wp.bm, wp.bn, x3_family() && x3_ok(p), st, conv_gemm_mode() == 2);
+    wgrad_launch(p, wp.bm, wp.bn, x3_family() && x3_ok(p), st, split_planes());
   } else {
     at::Tensor slab = at::empty({p.splits, Co, Kdim}, opts);
     p.out = slab.data_ptr<float>();
-    wgrad_launch(p, wp.bm, wp.bn, x3_family() && x3_ok(p), st, conv_gemm_mode() == 2);
+    wgrad_launch(p, wp.bm, wp.bn, x3_family() && x3_ok(p), st, split_planes());
     slab_sum_strided_launch(slab.data_ptr<float>(), p.splits, (long long)Co * Kdim, C, Ckeep, dw.data_ptr<float>(),
                             accumulate, st);
   }
@@ -503,13 +589,19 @@ std::vector<at::Tensor> conv_bn_act_fwd(const at::Tensor& x, const at::Tensor& w
                                         const c10::optional<at::Tensor>& running_var,
                                         const c10::optional<at::Tensor>& num_batches_tracked, double momentum,
                                         double eps, bool training, int64_t stride, int64_t pad, bool pool, bool relu,
-                                        const c10::optional<at::Tensor>& residual) {
+                                        const c10::optional<at::Tensor>& residual,
+                                        const c10::optional<at::Tensor>& x_amax,
+                                        const c10::optional<at::Tensor>& w_amax) {
   // RGB stem: zero-pad 3 -> 4 channels so the float4 gather path runs (the padded input is what
   // backward needs, so it is returned for saving)
   const bool padc = (x.size(1) % 4) != 0;
   const at::Tensor xin = padc ? pad_channels4(nhwc(x)) : x;
   const at::Tensor win = padc ? pad_channels4(nhwc(w)) : w;
-  std::vector<at::Tensor> r = conv2d_fwd(xin, win, b, stride, pad, training);
+  // f16x2 operand maxima: x's from its producer when given; W's once per step, reused by backward
+  // (zero channel padding does not change either)
+  const at::Tensor xa = amax_parts(xin, x_amax, cur_stream());
+  const at::Tensor wa = amax_parts(win, w_amax, cur_stream());
+  std::vector<at::Tensor> r = conv2d_fwd(xin, win, b, stride, pad, training, xa, wa);
   at::Tensor y = r[0];
   const int N = y.size(0), C = y.size(1), H = y.size(2), W = y.size(3);
   TORCH_CHECK(C % 4 == 0, "BatchNorm channel count must be a multiple of 4");
@@ -539,9 +631,12 @@ std::vector<at::Tensor> conv_bn_act_fwd(const at::Tensor& x, const at::Tensor& w
   }
   at::Tensor out = at::empty({N, C, pool ? H / 2 : H, pool ? W / 2 : W},
                              opts.memory_format(at::MemoryFormat::ChannelsLast));
+  at::Tensor out_amax;  // the output's |max| partials: the next conv's operand scale (f16x2)
+  if (f16x2_mode()) out_amax = at::empty({bn_act_grid(N, H, W, C, pool)}, opts);
   bn_act_fwd_launch(y.data_ptr<float>(), stats.data_ptr<float>(), res.defined() ? res.data_ptr<float>() : nullptr,
-                    out.data_ptr<float>(), N, H, W, C, pool, relu, st);
-  return {out, y, stats, xin};
+                    out.data_ptr<float>(), N, H, W, C, pool, relu, st,
+                    out_amax.defined() ? out_amax.data_ptr<float>() : nullptr);
+  return {out, y, stats, xin, out_amax, xa, wa};
 }
 
 // ---------------------------------------------------------------- fused block backward
@@ -554,7 +649,9 @@ std::vector<at::Tensor> conv_bn_act_bwd(const at::Tensor& gout_, const at::Tenso
                                         const c10::optional<at::Tensor>& db_out,
                                         const c10::optional<at::Tensor>& dgamma_out,
                                         const c10::optional<at::Tensor>& dbeta_out,
-                                        const c10::optional<at::Tensor>& dx_addend) {
+                                        const c10::optional<at::Tensor>& dx_addend,
+                                        const c10::optional<at::Tensor>& x_amax,
+                                        const c10::optional<at::Tensor>& w_amax) {
   check_f32_cuda(gout_, "grad_output");
   const at::Tensor gout = nhwc(gout_);
   const int N = y.size(0), C = y.size(1), H = y.size(2), W = y.size(3);
@@ -594,10 +691,14 @@ std::vector<at::Tensor> conv_bn_act_bwd(const at::Tensor& gout_, const at::Tenso
   if (sep_db) dbpart = at::empty({nblk, C, 2}, opts);
   at::Tensor dres;
   if (zout.defined()) dres = at::empty({N, C, H, W}, opts.memory_format(at::MemoryFormat::ChannelsLast));
+  at::Tensor dy_amax;  // dy's |max| partials: operand scale of both gradient GEMMs (f16x2)
+  if (f16x2_mode()) dy_amax = at::empty({nblk}, opts);
   bn_bwd_apply_launch(y.data_ptr<float>(), gout.data_ptr<float>(), stats.data_ptr<float>(), sums.data_ptr<float>(),
                       dy.data_ptr<float>(), sep_db ? dbpart.data_ptr<float>() : nullptr, nblk, N, H, W, C, pool,
                       relu, zout.defined() ? zout.data_ptr<float>() : nullptr,
-                      dres.defined() ? dres.data_ptr<float>() : nullptr, st);
+                      dres.defined() ? dres.data_ptr<float>() : nullptr, st,
+                      dy_amax.defined() ? dy_amax.data_ptr<float>() : nullptr);
+  const c10::optional<at::Tensor> dya = dy_amax.defined() ? c10::optional<at::Tensor>(dy_amax) : c10::nullopt;
   if (sep_db)
     chan_finalize_launch(dbpart.data_ptr<float>(), nblk, C, nullptr, db.data_ptr<float>(), nullptr, false, st);
   // x may carry zero-padded channels (RGB stem, see conv_bn_act_fwd)
@@ -611,19 +712,19 @@ std::vector<at::Tensor> conv_bn_act_bwd(const at::Tensor& gout_, const at::Tenso
   {
     c10::hip::HIPStreamGuard guard(side);
     dw = conv2d_wgrad_keep(dy, x, {w.size(0), x.size(1), w.size(2), w.size(3)}, stride, pad, dw_out, false,
-                           padc ? w.size(1) : -1);
+                           padc ? w.size(1) : -1, dya, x_amax);
   }
   if (overlap && !(dw_out.has_value() && dw_out->defined()))  // allocated on the side stream, consumed on main
     c10::hip::HIPCachingAllocator::recordStream(dw.storage().data_ptr(), c10::hip::getCurrentHIPStream());
   if (need_dx) {
     if (padc) {
       at::Tensor dx4 = conv2d_dgrad(dy, pad_channels4(nhwc(w)), {x.size(0), x.size(1), x.size(2), x.size(3)}, stride,
-                                    pad, c10::nullopt);
+                                    pad, c10::nullopt, dya, w_amax);
       dx = dx4.narrow(1, 0, w.size(1)).contiguous(at::MemoryFormat::ChannelsLast);
       if (dx_addend.has_value() && dx_addend->defined()) dx.add_(*dx_addend);
     } else {
       // residual-branch gradient (dx_addend) is accumulated by the data-gradient GEMM's epilogue
-      dx = conv2d_dgrad(dy, w, {x.size(0), x.size(1), x.size(2), x.size(3)}, stride, pad, dx_addend);
+      dx = conv2d_dgrad(dy, w, {x.size(0), x.size(1), x.size(2), x.size(3)}, stride, pad, dx_addend, dya, w_amax);
     }
   }
   if (overlap) join_from(side);
@@ -652,6 +753,7 @@ at::Tensor linear_fwd(const at::Tensor& x_, const at::Tensor& w_, const c10::opt
   p.Nout = O; p.M = B; p.Kdim = I; p.ktiles = g.ktiles; p.splits = g.splits;
   set_divs(p);
   hipStream_t st = cur_stream();
+  set_amax(p, amax_parts(x, c10::nullopt, st), amax_parts(w, c10::nullopt, st));
   if (g.splits == 1) {
     p.y = y.data_ptr<float>();
     p.bias = fptr(b);
@@ -700,13 +802,14 @@ std::vector<at::Tensor> linear_bwd(const at::Tensor& gy_, const at::Tensor& x_, 
   const WgradPlan wp = plan_wgrad(O, I, B);
   p.splits = wp.splits;
   set_divs(p);
+  set_amax(p, amax_parts(gy, c10::nullopt, st), amax_parts(x, c10::nullopt, st));
   if (p.splits == 1) {
     p.out = dw.data_ptr<float>();
-    wgrad_launch(p, wp.bm, wp.bn, x3_family() && x3_ok(p), st, conv_gemm_mode() == 2);
+    wgrad_launch(p, wp.bm, wp.bn, x3_family() && x3_ok(p), st, split_planes());
   } else {
     at::Tensor slab = at::empty({p.splits, O, I}, x.options());
     p.out = slab.data_ptr<float>();
-    wgrad_launch(p, wp.bm, wp.bn, x3_family() && x3_ok(p), st, conv_gemm_mode() == 2);
+    wgrad_launch(p, wp.bm, wp.bn, x3_family() && x3_ok(p), st, split_planes());
     slab_sum_launch(slab.data_ptr<float>(), p.splits, (long long)O * I, dw.data_ptr<float>(), false, st);
   }
   at::Tensor db;

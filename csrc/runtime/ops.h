@@ -11,20 +11,31 @@ std::vector<double> bench_presplit(const at::Tensor& x, const at::Tensor& w, int
 void set_conv_gemm(const std::string& mode);
 std::string get_conv_gemm();
 std::vector<at::Tensor> conv2d_fwd(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tensor>& bias,
-                                   int64_t stride, int64_t pad, bool want_stats);
+                                   int64_t stride, int64_t pad, bool want_stats,
+                                   const c10::optional<at::Tensor>& x_amax = c10::nullopt,
+                                   const c10::optional<at::Tensor>& w_amax = c10::nullopt);
 at::Tensor conv2d_dgrad(const at::Tensor& dy, const at::Tensor& w, std::vector<int64_t> in_shape, int64_t stride,
-                        int64_t pad, const c10::optional<at::Tensor>& addend);
+                        int64_t pad, const c10::optional<at::Tensor>& addend,
+                        const c10::optional<at::Tensor>& dy_amax = c10::nullopt,
+                        const c10::optional<at::Tensor>& w_amax = c10::nullopt);
 at::Tensor conv2d_wgrad(const at::Tensor& dy, const at::Tensor& x, std::vector<int64_t> w_shape, int64_t stride,
-                        int64_t pad, const c10::optional<at::Tensor>& out, bool accumulate);
+                        int64_t pad, const c10::optional<at::Tensor>& out, bool accumulate,
+                        const c10::optional<at::Tensor>& dy_amax = c10::nullopt,
+                        const c10::optional<at::Tensor>& x_amax = c10::nullopt);
 at::Tensor conv2d_wgrad_keep(const at::Tensor& dy, const at::Tensor& x, std::vector<int64_t> w_shape, int64_t stride,
-                             int64_t pad, const c10::optional<at::Tensor>& out, bool accumulate, int64_t keep_c);
+                             int64_t pad, const c10::optional<at::Tensor>& out, bool accumulate, int64_t keep_c,
+                             const c10::optional<at::Tensor>& dy_amax = c10::nullopt,
+                             const c10::optional<at::Tensor>& x_amax = c10::nullopt);
 std::vector<at::Tensor> conv_bn_act_fwd(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tensor>& b,
                                         const c10::optional<at::Tensor>& gamma, const c10::optional<at::Tensor>& beta,
                                         const c10::optional<at::Tensor>& running_mean,
                                         const c10::optional<at::Tensor>& running_var,
                                         const c10::optional<at::Tensor>& num_batches_tracked, double momentum,
                                         double eps, bool training, int64_t stride, int64_t pad, bool pool, bool relu,
-                                        const c10::optional<at::Tensor>& residual);
+                                        const c10::optional<at::Tensor>& residual,
+                                        const c10::optional<at::Tensor>& x_amax = c10::nullopt,
+                                        const c10::optional<at::Tensor>& w_amax = c10::nullopt);
+std::vector<at::Tensor> multi_amax(const std::vector<at::Tensor>& ts);
 std::vector<at::Tensor> conv_bn_act_bwd(const at::Tensor& gout, const at::Tensor& x, const at::Tensor& w,
                                         const at::Tensor& y, const at::Tensor& stats, int64_t stride, int64_t pad,
                                         bool pool, bool relu, bool need_dx, bool has_bias,
@@ -33,7 +44,9 @@ std::vector<at::Tensor> conv_bn_act_bwd(const at::Tensor& gout, const at::Tensor
                                         const c10::optional<at::Tensor>& db_out,
                                         const c10::optional<at::Tensor>& dgamma_out,
                                         const c10::optional<at::Tensor>& dbeta_out,
-                                        const c10::optional<at::Tensor>& dx_addend);
+                                        const c10::optional<at::Tensor>& dx_addend,
+                                        const c10::optional<at::Tensor>& x_amax = c10::nullopt,
+                                        const c10::optional<at::Tensor>& w_amax = c10::nullopt);
 at::Tensor linear_fwd(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tensor>& b);
 std::vector<at::Tensor> linear_bwd(const at::Tensor& gy, const at::Tensor& x, const at::Tensor& w, bool need_dx,
                                    bool has_bias, const c10::optional<at::Tensor>& dw_out,

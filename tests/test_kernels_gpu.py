@@ -282,34 +282,54 @@ def _rms_rel(a, b):
     return ((a - b).norm() / b.norm().clamp_min(1e-30)).item()
 
 
+def _heavy(shape, scale):
+    """Wide-dynamic-range data (log-normal magnitudes spanning ~6 decades, random signs)."""
+    return torch.randn(shape, device="cuda") * torch.exp(2.0 * torch.randn(shape, device="cuda")) * scale
+
+
+@pytest.mark.parametrize("mode", ["x3", "f16x2"])
 @pytest.mark.parametrize("N,Ci,H,W,Co,k,s,p", [CONV_CASES[i] for i in (0, 1, 3, 5, 7, 9)])
-def test_x3_engine_is_as_accurate_as_fp32_mfma(N, Ci, H, W, Co, k, s, p):
-    """The 3-term bf16 split engine (conv_x3.hip) must match the exact fp32-input MFMA engine's
-    error against fp64, for forward and data-gradient GEMMs."""
+def test_split_engines_are_as_accurate_as_fp32_mfma(N, Ci, H, W, Co, k, s, p, mode):
+    """The split engines (3-term bf16 "x3", scaled 2-term fp16 "f16x2") must match the exact
+    fp32-input MFMA engine's error against fp64, for the forward, data- and weight-gradient GEMMs."""
+    _engine_vs_f32(mode, N, Ci, H, W, Co, k, s, p, torch.randn)
+
+
+@pytest.mark.parametrize("scale", [1e-12, 1e9])
+def test_f16x2_scaling_wide_and_extreme_ranges(scale):
+    """f16x2 operand scales: heavy-tailed magnitudes and values far outside fp16's range (tiny
+    gradients, huge activations) keep fp32-level accuracy -- the power-of-two scales map every
+    operand's max into fp16 range, and what falls below 2^-18 of it contributes only below the
+    dot products' own fp32 rounding."""
+    N, Ci, H, W, Co, k, s, p = CONV_CASES[3]
+    _engine_vs_f32("f16x2", N, Ci, H, W, Co, k, s, p, lambda *sh, device: _heavy(sh, scale))
+
+
+def _engine_vs_f32(mode, N, Ci, H, W, Co, k, s, p, gen):
     torch.manual_seed(1)
-    x = torch.randn(N, Ci, H, W, device="cuda")
+    x = gen(N, Ci, H, W, device="cuda")
     w = torch.randn(Co, Ci, k, k, device="cuda") * (1.0 / (Ci * k * k) ** 0.5)
     xr = x.double().cpu().requires_grad_()
     wr = w.double().cpu().requires_grad_()
     ref = F.conv2d(xr, wr, None, s, p)
-    gy = torch.randn(ref.shape, device="cuda")
+    gy = gen(*ref.shape, device="cuda")
     ref.backward(gy.double().cpu())
     orig = C().get_conv_gemm()
     errs = {}
     try:
-        for mode in ("f32", "x3"):
-            C().set_conv_gemm(mode)
+        for m in ("f32", mode):
+            C().set_conv_gemm(m)
             y = C().conv2d_fwd(cl(x), cl(w), None, s, p, False)[0]
             dx = C().conv2d_dgrad(cl(gy), cl(w), list(x.shape), s, p)
             dw = C().conv2d_wgrad(cl(gy), cl(x), list(w.shape), s, p)
-            errs[mode] = (_rms_rel(y, ref.detach()), _rms_rel(dx, xr.grad), rel_err(y, ref.detach()),
-                          _rms_rel(dw, wr.grad))
+            errs[m] = (_rms_rel(y, ref.detach()), _rms_rel(dx, xr.grad), rel_err(y, ref.detach()),
+                       _rms_rel(dw, wr.grad))
     finally:
         C().set_conv_gemm(orig)
-    print("conv errs (rms fwd, rms dgrad, max fwd, rms wgrad)", errs)
+    print(f"conv errs {mode} (rms fwd, rms dgrad, max fwd, rms wgrad)", errs)
     for i in range(4):
-        assert errs["x3"][i] <= 2.0 * errs["f32"][i] + 1e-9, errs
-    assert max(errs["x3"][0], errs["x3"][1], errs["x3"][3]) < 1e-6, errs
+        assert errs[mode][i] <= 2.0 * errs["f32"][i] + 1e-9, errs
+    assert max(errs[mode][0], errs[mode][1], errs[mode][3]) < 1e-6, errs
 
 
 def test_bf16_engine_runs_at_bf16_accuracy():
