@@ -43,6 +43,12 @@ def _hipcc() -> str:
     raise RuntimeError("hipcc not found (ROCm required to build the native runtime)")
 
 
+# GEMM kernels whose operand split must stay scalar f32: packed-f32 VALU issued between MFMAs
+# costs ~22 extra cycles per MFMA gap on gfx950 (x3_common.h), and the SLP vectorizer would re-pack
+# adjacent scalar multiplies / FMAs into v_pk_mul_f32 / v_pk_fma_f32
+NO_SLP = {"conv_x3.hip", "wgrad.hip"}
+
+
 def _ninja_escape(s: str) -> str:
     return s.replace("$", "$$").replace(" ", "$ ").replace(":", "$:")
 
@@ -77,7 +83,7 @@ def write_ninja() -> str:
         f"rflags = {rflags}",
         f"ldflags = {ldflags}",
         "rule kcc",
-        "  command = $hipcc $kflags -MD -MF $out.d -c $in -o $out",
+        "  command = $hipcc $kflags $kextra -MD -MF $out.d -c $in -o $out",
         "  depfile = $out.d",
         "  deps = gcc",
         "  description = HIPCC(gfx950) $in",
@@ -95,6 +101,8 @@ def write_ninja() -> str:
         src = os.path.join(CSRC, "kernels", f)
         obj = os.path.join(BUILD_DIR, f + ".o")
         lines.append(f"build {_ninja_escape(obj)}: kcc {_ninja_escape(src)}")
+        if f in NO_SLP:
+            lines.append("  kextra = -fno-slp-vectorize")
         objs.append(obj)
     for f in RUNTIME:
         src = os.path.join(CSRC, "runtime", f)

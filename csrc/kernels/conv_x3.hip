@@ -80,7 +80,8 @@ __device__ __forceinline__ u32x4 pack8(const float (&v)[8]) {
 }
 
 template <int BM, int BN, int MODE, bool DGRAD, bool M16, bool PS = false, int ABL = 0, int NP = 3>
-__global__ __launch_bounds__(waves_m<BM>() * 128, (BM + BN >= 256) ? 1 : 2) void conv_x3_kernel(ConvGemmParams p) {
+__global__ __launch_bounds__(waves_m<BM>() * 128, (NP == 2 && BM + BN <= 256) ? 2 : (BM + BN >= 256) ? 1 : 2) void
+conv_x3_kernel(ConvGemmParams p) {
   static_assert(!PS || MODE == 0, "pre-split operands need C % 32 == 0");
   static_assert(NP == 3 || ((NP == 1 || NP == 2) && !PS), "planes");
   static_assert(NP != 2 || !M16, "f16x2 uses the 32x32x16 tiles");

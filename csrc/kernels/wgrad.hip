@@ -11,6 +11,7 @@
 // m-major ([m][co] and [m][k]) exactly as they sit in memory, so no transpose is needed: an MFMA
 // operand lane (i, h) reads row m = 2s + h, column i -- 32 consecutive floats per half-wave,
 // conflict-free ds_read_b32.
+#include <cstdlib>
 #include <type_traits>
 
 #include "common.h"
@@ -227,15 +228,17 @@ __device__ __forceinline__ void split_store_cols(const float4 (&v)[RPT], __bf16*
 
 // NP = 3: split-bf16 (six products); 2: f16x2 (scaled operands, two fp16 terms, three products on
 // v_mfma_f32_32x32x16_f16, see x3_common.h); 1: plain bf16 operands (non-parity mode)
-template <int BM, int BN, bool FAST, int NP = 3>
+// PIPE: two LDS stages and two register sets, one barrier per K-tile (tile t+1 is split into the
+// other stage while the MFMAs consume tile t, tile t+2 in flight); else one stage, register
+// prefetch of t+1 only, two barriers per K-tile.
+template <int BM, int BN, bool FAST, int NP = 3, bool PIPE = false>
 __global__ __launch_bounds__(256, 2) void wgrad_x3_kernel(WgradParams p) {
   constexpr int TM = BM / 64, TN = BN / 64;
   constexpr int PA = BM * XLD, PB = BN * XLD;
   constexpr int RPT_A = BM / 32, RPT_B = BN / 32;  // m rows per thread (4 for 128-wide, 2 for 64)
   constexpr int MQ_A = WBK / RPT_A, MQ_B = WBK / RPT_B;  // m groups per tile (8 or 16)
-  __shared__ __attribute__((aligned(16))) __bf16 smem[NP * (PA + PB)];
-  __bf16* As = smem;
-  __bf16* Bs = smem + NP * PA;
+  constexpr int STAGE = NP * (PA + PB);
+  __shared__ __attribute__((aligned(16))) __bf16 smem[(PIPE ? 2 : 1) * STAGE];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid >> 1, wn = wid & 1;
 
@@ -279,8 +282,8 @@ __global__ __launch_bounds__(256, 2) void wgrad_x3_kernel(WgradParams p) {
     sb = amax_scale(p.amax_x, p.amax_nx);
   }
 
-  float4 ra[RPT_A], rb[RPT_B];
-  auto load_tile = [&](int kt) {
+  float4 ra[RPT_A], rb[RPT_B], ra1[RPT_A], rb1[RPT_B];
+  auto load_tile = [&](int kt, float4 (&ra)[RPT_A], float4 (&rb)[RPT_B]) {
     const int mb = kt * WBK;
     if (FAST) {
       const __amdgpu_buffer_rsrc_t dr =
@@ -337,9 +340,9 @@ __global__ __launch_bounds__(256, 2) void wgrad_x3_kernel(WgradParams p) {
       rb[i] = make_float4(e[0], e[1], e[2], e[3]);
     }
   };
-  auto store_tile = [&]() {
-    split_store_cols<RPT_A, NP>(ra, As + (a_cg * 4) * XLD + a_mq * RPT_A, PA, sa);
-    split_store_cols<RPT_B, NP>(rb, Bs + (b_cg * 4) * XLD + b_mq * RPT_B, PB, sb);
+  auto store_tile = [&](const float4 (&ra)[RPT_A], const float4 (&rb)[RPT_B], __bf16* st) {
+    split_store_cols<RPT_A, NP>(ra, st + (a_cg * 4) * XLD + a_mq * RPT_A, PA, sa);
+    split_store_cols<RPT_B, NP>(rb, st + NP * PA + (b_cg * 4) * XLD + b_mq * RPT_B, PB, sb);
   };
 
   f32x16 acc[TM][TN];
@@ -352,13 +355,8 @@ __global__ __launch_bounds__(256, 2) void wgrad_x3_kernel(WgradParams p) {
 
   const int l32 = lane & 31, hh = lane >> 5;
   const int koff = hh * 8;
-  if (kt_begin < kt_end) {
-    load_tile(kt_begin);
-    store_tile();
-    __syncthreads();
-    for (int kt = kt_begin; kt < kt_end; ++kt) {
-      const bool more = kt + 1 < kt_end;
-      if (more) load_tile(kt + 1);
+  auto compute = [&](const __bf16* As) {
+    const __bf16* Bs = As + NP * PA;
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
         if constexpr (NP == 2) {
@@ -418,9 +416,37 @@ __global__ __launch_bounds__(256, 2) void wgrad_x3_kernel(WgradParams p) {
             acc[a][b] = c;
           }
       }
+  };
+  if constexpr (PIPE) {
+    if (kt_begin < kt_end) {
+      load_tile(kt_begin, ra, rb);
+      if (kt_begin + 1 < kt_end) load_tile(kt_begin + 1, ra1, rb1);
+      store_tile(ra, rb, smem);
+      __syncthreads();
+      int kt = kt_begin;
+      for (; kt + 1 < kt_end; kt += 2) {
+        if (kt + 2 < kt_end) load_tile(kt + 2, ra, rb);
+        compute(smem);
+        store_tile(ra1, rb1, smem + STAGE);
+        __syncthreads();
+        if (kt + 3 < kt_end) load_tile(kt + 3, ra1, rb1);
+        compute(smem + STAGE);
+        store_tile(ra, rb, smem);  // past the last tile: stale registers into a stage nothing reads
+        __syncthreads();
+      }
+      if (kt < kt_end) compute(smem);
+    }
+  } else if (kt_begin < kt_end) {
+    load_tile(kt_begin, ra, rb);
+    store_tile(ra, rb, smem);
+    __syncthreads();
+    for (int kt = kt_begin; kt < kt_end; ++kt) {
+      const bool more = kt + 1 < kt_end;
+      if (more) load_tile(kt + 1, ra, rb);
+      compute(smem);
       __syncthreads();
       if (more) {
-        store_tile();
+        store_tile(ra, rb, smem);
         __syncthreads();
       }
     }
@@ -547,7 +573,12 @@ void wgrad_launch_t(const WgradParams& p, bool x3, hipStream_t st, int np) {
       if (fast) hipLaunchKernelGGL((wgrad_x3_kernel<BM, BN, true, 1>), grid, dim3(256), 0, st, p);
       else hipLaunchKernelGGL((wgrad_x3_kernel<BM, BN, false, 1>), grid, dim3(256), 0, st, p);
     } else if (np == 2) {
-      if (fast) hipLaunchKernelGGL((wgrad_x3_kernel<BM, BN, true, 2>), grid, dim3(256), 0, st, p);
+      static const bool pipe = [] {
+        const char* e = std::getenv("CDP_WGRAD_PIPE");
+        return !(e && e[0] == '0');
+      }();
+      if (fast && pipe) hipLaunchKernelGGL((wgrad_x3_kernel<BM, BN, true, 2, true>), grid, dim3(256), 0, st, p);
+      else if (fast) hipLaunchKernelGGL((wgrad_x3_kernel<BM, BN, true, 2>), grid, dim3(256), 0, st, p);
       else hipLaunchKernelGGL((wgrad_x3_kernel<BM, BN, false, 2>), grid, dim3(256), 0, st, p);
     } else if (fast) hipLaunchKernelGGL((wgrad_x3_kernel<BM, BN, true>), grid, dim3(256), 0, st, p);
     else hipLaunchKernelGGL((wgrad_x3_kernel<BM, BN, false>), grid, dim3(256), 0, st, p);

@@ -180,6 +180,15 @@ double conv_mfma_rate() {
   return m == 1 ? 250.0e12 : m == 2 ? 800.0e12 : m == 3 ? 450.0e12 : 120.0e12;
 }
 int wgrad_blocks_per_cu(int bm, int bn) {
+  // f16x2, two-stage pipeline (default, CDP_WGRAD_PIPE=0 for one stage): 2 stages x 2 planes x
+  // (bm+bn) x 80 B of LDS, 214 / 153 / 110 VGPRs (128x128 / 128x64 / 64x64); one stage: half the
+  // LDS, 156 / 114 / 70 VGPRs
+  static const bool pipe = [] {
+    const char* e = std::getenv("CDP_WGRAD_PIPE");
+    return !(e && e[0] == '0');
+  }();
+  if (f16x2_mode() && pipe) return (bm + bn) >= 192 ? 2 : 3;
+  if (f16x2_mode()) return (bm + bn) >= 256 ? 3 : (bm + bn) >= 192 ? 4 : 6;
   if (x3_family()) return (bm + bn) >= 256 ? 2 : (bm + bn) >= 192 ? 3 : 5;
   return std::max(1, std::min(4, (160 * 1024) / (2 * 32 * (bm + bn + 8) * 4)));
 }
