@@ -195,7 +195,11 @@ conv_x3_kernel(ConvGemmParams p) {
     d[off + 3] = v.w;
   };
 
-  auto load_tile = [&](int kt, auto& va, auto& vb) {
+  // valid == false: every offset is past the buffers, so the loads return zeros without touching
+  // memory. Issuing them unconditionally (no branch around the prefetch) lets the compiler wait
+  // with vmcnt(#newer loads) for the older tile instead of vmcnt(0) at a control-flow merge,
+  // which would have drained the prefetch of the next tile.
+  auto load_tile = [&](int kt, auto& va, auto& vb, bool valid) {
     const int r0 = kt * BK;
     if constexpr (PS) {
       const int tap = fdiv(r0, p.fd_C);
@@ -203,13 +207,13 @@ conv_x3_kernel(ConvGemmParams p) {
       const int kh = fdiv(tap, p.fd_KW), kw = tap - kh * p.KW;
 #pragma unroll
       for (int i = 0; i < A_LD; ++i) {
-        const unsigned o = a_voff(i, kh, kw, c0);
+        const unsigned o = valid ? a_voff(i, kh, kw, c0) : kOOB;
 #pragma unroll
         for (int q = 0; q < 3; ++q) va[i][q] = __builtin_amdgcn_raw_buffer_load_b128(xr, (int)(o + q * xplane), 0, 0);
       }
 #pragma unroll
       for (int i = 0; i < B_LD; ++i) {
-        const unsigned o = b_off[i] + ((unsigned)r0 << ES);
+        const unsigned o = valid ? b_off[i] + ((unsigned)r0 << ES) : kOOB;
 #pragma unroll
         for (int q = 0; q < 3; ++q) vb[i][q] = __builtin_amdgcn_raw_buffer_load_b128(wr, (int)(o + q * wplane), 0, 0);
       }
@@ -221,7 +225,7 @@ conv_x3_kernel(ConvGemmParams p) {
       const int kh = fdiv(tap, p.fd_KW), kw = tap - kh * p.KW;
 #pragma unroll
       for (int i = 0; i < A_LD; ++i) {
-        const unsigned o = a_voff(i, kh, kw, c0);
+        const unsigned o = valid ? a_voff(i, kh, kw, c0) : kOOB;
         put4(va[i], 0, bload4(xr, o));
         put4(va[i], 4, bload4(xr, o + 16u));
       }
@@ -229,7 +233,7 @@ conv_x3_kernel(ConvGemmParams p) {
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
         const int r = r0 + kq + 4 * h;
-        const bool rok = r < p.Kdim;
+        const bool rok = valid && r < p.Kdim;
         const int tap = fdiv(rok ? r : 0, p.fd_C);
         const int c = r - tap * p.C;
         const int kh = fdiv(tap, p.fd_KW), kw = tap - kh * p.KW;
@@ -243,7 +247,7 @@ conv_x3_kernel(ConvGemmParams p) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const int r = r0 + kq + j;
-        const bool rok = r < p.Kdim;
+        const bool rok = valid && r < p.Kdim;
         const int tap = fdiv(rok ? r : 0, p.fd_C);
         const int c = r - tap * p.C;
         const int kh = fdiv(tap, p.fd_KW), kw = tap - kh * p.KW;
@@ -257,7 +261,7 @@ conv_x3_kernel(ConvGemmParams p) {
     if constexpr (!PS) {
 #pragma unroll
     for (int i = 0; i < B_LD; ++i) {
-      const unsigned o = b_off[i] + ((unsigned)r0 << ES);
+      const unsigned o = valid ? b_off[i] + ((unsigned)r0 << ES) : kOOB;
       if (MODE == 0) {
         put4(vb[i], 0, bload4(wr, o));
         put4(vb[i], 4, bload4(wr, o + 16u));
@@ -458,17 +462,17 @@ conv_x3_kernel(ConvGemmParams p) {
   // (loaded into registers one iteration earlier) is split into stage (t+1)&1 and tile t+2 is
   // being fetched into the other register set.
   if (kt_begin < kt_end) {
-    load_tile(kt_begin, va0, vb0);
-    if (kt_begin + 1 < kt_end) load_tile(kt_begin + 1, va1, vb1);
+    load_tile(kt_begin, va0, vb0, true);
+    load_tile(kt_begin + 1, va1, vb1, kt_begin + 1 < kt_end);
     store_tile(va0, vb0, smem);
     __syncthreads();
     int kt = kt_begin;
     for (; kt + 1 < kt_end; kt += 2) {
-      if (!(ABL & 1) && kt + 2 < kt_end) load_tile(kt + 2, va0, vb0);
+      if (!(ABL & 1)) load_tile(kt + 2, va0, vb0, kt + 2 < kt_end);
       compute(smem);
       if (!(ABL & 2)) store_tile(va1, vb1, smem + STAGE);
       __syncthreads();
-      if (!(ABL & 1) && kt + 3 < kt_end) load_tile(kt + 3, va1, vb1);
+      if (!(ABL & 1)) load_tile(kt + 3, va1, vb1, kt + 3 < kt_end);
       compute(smem + STAGE);
       // unconditional (past the last tile it stores stale registers into a stage nothing reads),
       // so the split can interleave with the MFMAs above

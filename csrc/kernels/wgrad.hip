@@ -283,11 +283,13 @@ __global__ __launch_bounds__(256, 2) void wgrad_x3_kernel(WgradParams p) {
   }
 
   float4 ra[RPT_A], rb[RPT_B], ra1[RPT_A], rb1[RPT_B];
-  auto load_tile = [&](int kt, float4 (&ra)[RPT_A], float4 (&rb)[RPT_B]) {
+  // valid == false (FAST only): zero-size / out-of-range buffers, so the loads return zeros without
+  // touching memory and can be issued without a branch (see conv_x3.hip)
+  auto load_tile = [&](int kt, float4 (&ra)[RPT_A], float4 (&rb)[RPT_B], bool valid = true) {
     const int mb = kt * WBK;
     if (FAST) {
-      const __amdgpu_buffer_rsrc_t dr =
-          make_rsrc(p.dy + (long long)mb * p.Cout, (unsigned)(p.M - mb) * (unsigned)p.Cout * 4u);
+      const __amdgpu_buffer_rsrc_t dr = make_rsrc(p.dy + (long long)(valid ? mb : 0) * p.Cout,
+                                                  valid ? (unsigned)(p.M - mb) * (unsigned)p.Cout * 4u : 0u);
 #pragma unroll
       for (int i = 0; i < RPT_A; ++i) ra[i] = bload4(dr, a_off[i]);
 #pragma unroll
@@ -298,7 +300,7 @@ __global__ __launch_bounds__(256, 2) void wgrad_x3_kernel(WgradParams p) {
         const int rem = mm - mul24(n, PQ);
         const int pp = fdiv(rem, p.fd_Q), qq = rem - mul24(pp, p.Q);
         const int ih = mul24(pp, p.stride) - p.pad + b_kh, iw = mul24(qq, p.stride) - p.pad + b_kw;
-        const bool ok = m < p.M && b_kok && (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W;
+        const bool ok = valid && m < p.M && b_kok && (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W;
         rb[i] = bload4(xr, ok ? (unsigned)(mul24(n, HWC) + mul24(mul24(ih, p.W) + iw, p.C) + b_c) * 4u : kOOB);
       }
       return;
@@ -419,17 +421,18 @@ __global__ __launch_bounds__(256, 2) void wgrad_x3_kernel(WgradParams p) {
   };
   if constexpr (PIPE) {
     if (kt_begin < kt_end) {
+      static_assert(!PIPE || FAST, "the pipelined kernel issues branch-free FAST loads");
       load_tile(kt_begin, ra, rb);
-      if (kt_begin + 1 < kt_end) load_tile(kt_begin + 1, ra1, rb1);
+      load_tile(kt_begin + 1, ra1, rb1, kt_begin + 1 < kt_end);
       store_tile(ra, rb, smem);
       __syncthreads();
       int kt = kt_begin;
       for (; kt + 1 < kt_end; kt += 2) {
-        if (kt + 2 < kt_end) load_tile(kt + 2, ra, rb);
+        load_tile(kt + 2, ra, rb, kt + 2 < kt_end);
         compute(smem);
         store_tile(ra1, rb1, smem + STAGE);
         __syncthreads();
-        if (kt + 3 < kt_end) load_tile(kt + 3, ra1, rb1);
+        load_tile(kt + 3, ra1, rb1, kt + 3 < kt_end);
         compute(smem + STAGE);
         store_tile(ra, rb, smem);  // past the last tile: stale registers into a stage nothing reads
         __syncthreads();
