@@ -156,6 +156,9 @@ void wtrans_launch(const float* w, float* wt, int Co, int T, int Ci, hipStream_t
 // sub-filter transpose: wt[ci][a][b][co] = w[co][kh0 + 2a][kw0 + 2b][ci] (a < nkh, b < nkw)
 void wtrans_sub_launch(const float* w, float* wt, int Co, int KH, int KW, int Ci, int kh0, int kw0, int nkh, int nkw,
                        hipStream_t st);
+// NHWC channel padding C (<= 4) -> 4 with zeros; amax_part (optional, pad_c4_grid entries): per-block |max|
+int pad_c4_grid(long long npix);
+void pad_c4_launch(const float* x, long long npix, int C, float* out, float* amax_part, hipStream_t st);
 void stack_mean_launch(const float* const* srcs, int k, long long n, float* dst, hipStream_t st);
 void scale_launch(float* x, long long n, float a, hipStream_t st);
 void colsum_launch(const float* x, int R, int C, float* out, bool accumulate, hipStream_t st);

@@ -8,6 +8,8 @@
 //   optim.SGD(lr .1, mom .9, wd 1e-4)   /root/reference/src/Part 1/main.py:114-115
 //   RandomCrop(32,4)+HFlip+Normalize    /root/reference/src/Part 1/main.py:82-93
 //   torch.mean(torch.stack(inputs), 0)  /root/reference/src/Part 2a/main.py:122
+#include <algorithm>
+
 #include "common.h"
 #include "kernels.h"
 #include "x3_common.h"
@@ -221,6 +223,31 @@ __global__ __launch_bounds__(256) void wtrans_kernel(const float* __restrict__ w
   for (int j = ty; j < 32; j += 8) {
     const int ci = ci0 + j, co = co0 + tx;
     if (ci < Ci && co < Co) wt[((long long)ci * T + tap) * Co + co] = tile[tx][j];
+  }
+}
+
+// ------------------------------------------------------------------ channel padding
+// out[p][0..C4) = (x[p][0..C), 0...) for NHWC pixels p: the RGB stem's 3 -> 4 channel padding in
+// one pass (one float4 store per pixel), plus the per-block |max| the f16x2 GEMM scales need.
+__global__ __launch_bounds__(256) void pad_c4_kernel(const float* __restrict__ x, long long npix, int C,
+                                                     float* __restrict__ out, float* __restrict__ amax_part) {
+  float am = 0.f;
+  for (long long p = (long long)blockIdx.x * 256 + threadIdx.x; p < npix; p += (long long)gridDim.x * 256) {
+    const float* src = x + p * C;
+    float v[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      v[c] = c < C ? src[c] : 0.f;
+      am = fmaxf(am, fabsf(v[c]));
+    }
+    st4(out + p * 4, make_float4(v[0], v[1], v[2], v[3]));
+  }
+  if (amax_part) {
+    __shared__ float red[4];
+    am = wave_max(am);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = am;
+    __syncthreads();
+    if (threadIdx.x == 0) amax_part[blockIdx.x] = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
   }
 }
 
@@ -517,6 +544,10 @@ void counter_inc_launch(long long* c, hipStream_t st) {
 void wtrans_launch(const float* w, float* wt, int Co, int T, int Ci, hipStream_t st) {
   dim3 grid((Ci + 31) / 32, (Co + 31) / 32, T);
   hipLaunchKernelGGL(wtrans_kernel, grid, dim3(256), 0, st, w, wt, Co, T, Ci);
+}
+int pad_c4_grid(long long npix) { return (int)std::min<long long>(1024, std::max<long long>(1, (npix + 255) / 256)); }
+void pad_c4_launch(const float* x, long long npix, int C, float* out, float* amax_part, hipStream_t st) {
+  hipLaunchKernelGGL(pad_c4_kernel, dim3(pad_c4_grid(npix)), dim3(256), 0, st, x, npix, C, out, amax_part);
 }
 void stack_mean_launch(const float* const* srcs, int k, long long n, float* dst, hipStream_t st) {
   hipLaunchKernelGGL(stack_mean_kernel, dim3(grid_for(n)), dim3(256), 0, st, srcs, k, n, dst);

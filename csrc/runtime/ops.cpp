@@ -319,10 +319,21 @@ void set_divs(P& p) {
 }
 
 // Zero-pad the channel dim of a channels_last 4-D tensor up to a multiple of 4 (RGB stems:
-// 3 -> 4) so the float4 gather paths apply.
-at::Tensor pad_channels4(const at::Tensor& t) {
+// 3 -> 4) so the float4 gather paths apply. C < 4 is one kernel that can also emit the padded
+// tensor's |max| partials (f16x2 operand scale) into *amax.
+at::Tensor pad_channels4(const at::Tensor& t, at::Tensor* amax = nullptr) {
   const int64_t C = t.size(1), C4 = (C + 3) / 4 * 4;
   at::Tensor o = at::empty({t.size(0), C4, t.size(2), t.size(3)}, t.options().memory_format(at::MemoryFormat::ChannelsLast));
+  if (C < 4 && t.is_contiguous(at::MemoryFormat::ChannelsLast)) {
+    const long long npix = t.size(0) * t.size(2) * t.size(3);
+    float* ap = nullptr;
+    if (amax) {
+      *amax = at::empty({pad_c4_grid(npix)}, t.options());
+      ap = amax->data_ptr<float>();
+    }
+    pad_c4_launch(t.data_ptr<float>(), npix, (int)C, o.data_ptr<float>(), ap, cur_stream());
+    return o;
+  }
   o.zero_();
   o.narrow(1, 0, C).copy_(t);
   return o;
@@ -604,11 +615,14 @@ std::vector<at::Tensor> conv_bn_act_fwd(const at::Tensor& x, const at::Tensor& w
   // RGB stem: zero-pad 3 -> 4 channels so the float4 gather path runs (the padded input is what
   // backward needs, so it is returned for saving)
   const bool padc = (x.size(1) % 4) != 0;
-  const at::Tensor xin = padc ? pad_channels4(nhwc(x)) : x;
+  const bool have_xa = x_amax.has_value() && x_amax->defined();
+  at::Tensor pad_amax;  // the padding pass measures x on the way (f16x2)
+  const at::Tensor xin = padc ? pad_channels4(nhwc(x), f16x2_mode() && !have_xa ? &pad_amax : nullptr) : x;
   const at::Tensor win = padc ? pad_channels4(nhwc(w)) : w;
   // f16x2 operand maxima: x's from its producer when given; W's once per step, reused by backward
   // (zero channel padding does not change either)
-  const at::Tensor xa = amax_parts(xin, x_amax, cur_stream());
+  const at::Tensor xa = amax_parts(xin, pad_amax.defined() ? c10::optional<at::Tensor>(pad_amax) : x_amax,
+                                   cur_stream());
   const at::Tensor wa = amax_parts(win, w_amax, cur_stream());
   std::vector<at::Tensor> r = conv2d_fwd(xin, win, b, stride, pad, training, xa, wa);
   at::Tensor y = r[0];
