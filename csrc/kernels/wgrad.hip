@@ -231,11 +231,19 @@ __device__ __forceinline__ void split_store_cols(const float4 (&v)[RPT], __bf16*
 // PIPE: two LDS stages and two register sets, one barrier per K-tile (tile t+1 is split into the
 // other stage while the MFMAs consume tile t, tile t+2 in flight); else one stage, register
 // prefetch of t+1 only, two barriers per K-tile.
+// BM = 256 (f16x2 only): 512 threads = 4 (co) x 2 (k) waves of 64x64, one workgroup per CU.
+template <int BM>
+constexpr int wg_threads() { return BM >= 256 ? 512 : 256; }
+
 template <int BM, int BN, bool FAST, int NP = 3, bool PIPE = false>
-__global__ __launch_bounds__(256, 2) void wgrad_x3_kernel(WgradParams p) {
-  constexpr int TM = BM / 64, TN = BN / 64;
+__global__ __launch_bounds__(wg_threads<BM>(), BM >= 256 ? 1 : 2) void wgrad_x3_kernel(WgradParams p) {
+  constexpr int NT = wg_threads<BM>();
+  constexpr int WMW = NT / 128;  // waves along co (x 2 along k)
+  constexpr int TM = BM / WMW / 32, TN = BN / 64;
   constexpr int PA = BM * XLD, PB = BN * XLD;
-  constexpr int RPT_A = BM / 32, RPT_B = BN / 32;  // m rows per thread (4 for 128-wide, 2 for 64)
+  // m rows per thread, 4 columns (one float4) each: 4 for 128-wide / 256-wide tiles, 2 for 64
+  constexpr int RPT_A = BM * WBK / (NT * 4), RPT_B = BN * WBK / (NT * 4);
+  static_assert(RPT_B >= 2, "tile too narrow for the loader");
   constexpr int MQ_A = WBK / RPT_A, MQ_B = WBK / RPT_B;  // m groups per tile (8 or 16)
   constexpr int STAGE = NP * (PA + PB);
   __shared__ __attribute__((aligned(16))) __bf16 smem[(PIPE ? 2 : 1) * STAGE];
@@ -365,7 +373,7 @@ __global__ __launch_bounds__(256, 2) void wgrad_x3_kernel(WgradParams p) {
           f16x8 af[TM][2], bf[TN][2];
 #pragma unroll
           for (int a = 0; a < TM; ++a) {
-            const __bf16* src = As + (wm * (BM / 2) + a * 32 + l32) * XLD + s * 16 + koff;
+            const __bf16* src = As + (wm * (BM / WMW) + a * 32 + l32) * XLD + s * 16 + koff;
 #pragma unroll
             for (int q = 0; q < 2; ++q) af[a][q] = *reinterpret_cast<const f16x8*>(src + q * PA);
           }
@@ -390,7 +398,7 @@ __global__ __launch_bounds__(256, 2) void wgrad_x3_kernel(WgradParams p) {
         bf16x8 af[TM][3], bf[TN][3];
 #pragma unroll
         for (int a = 0; a < TM; ++a) {
-          const __bf16* src = As + (wm * (BM / 2) + a * 32 + l32) * XLD + s * 16 + koff;
+          const __bf16* src = As + (wm * (BM / WMW) + a * 32 + l32) * XLD + s * 16 + koff;
 #pragma unroll
           for (int q = 0; q < NP; ++q) af[a][q] = *reinterpret_cast<const bf16x8*>(src + q * PA);
         }
@@ -472,7 +480,7 @@ __global__ __launch_bounds__(256, 2) void wgrad_x3_kernel(WgradParams p) {
         const int k = r0 + wn * (BN / 2) + b * 32 + l32;
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const int c = co0 + wm * (BM / 2) + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
+          const int c = co0 + wm * (BM / WMW) + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
           if (!decltype(pred)::value || (c < p.Cout && k < p.Kdim)) out[(long long)c * p.Kdim + k] = acc[a][b][r];
         }
       }
@@ -580,7 +588,8 @@ void wgrad_launch_t(const WgradParams& p, bool x3, hipStream_t st, int np) {
         const char* e = std::getenv("CDP_WGRAD_PIPE");
         return !(e && e[0] == '0');
       }();
-      if (fast && pipe) hipLaunchKernelGGL((wgrad_x3_kernel<BM, BN, true, 2, true>), grid, dim3(256), 0, st, p);
+      if (fast && pipe)
+        hipLaunchKernelGGL((wgrad_x3_kernel<BM, BN, true, 2, true>), grid, dim3(wg_threads<BM>()), 0, st, p);
       else if (fast) hipLaunchKernelGGL((wgrad_x3_kernel<BM, BN, true, 2>), grid, dim3(256), 0, st, p);
       else hipLaunchKernelGGL((wgrad_x3_kernel<BM, BN, false, 2>), grid, dim3(256), 0, st, p);
     } else if (fast) hipLaunchKernelGGL((wgrad_x3_kernel<BM, BN, true>), grid, dim3(256), 0, st, p);
@@ -592,6 +601,12 @@ void wgrad_launch_t(const WgradParams& p, bool x3, hipStream_t st, int np) {
 }
 
 void wgrad_launch(const WgradParams& p, int bm, int bn, bool x3, hipStream_t st, int np) {
+  if (bm == 256 && bn == 128 && x3 && np == 2 && (p.C % 4) == 0 && (p.Cout % 4) == 0) {
+    // host plan only picks 256 for the pipelined f16x2 path (plan_wgrad)
+    hipLaunchKernelGGL((wgrad_x3_kernel<256, 128, true, 2, true>), dim3(((p.Cout + 255) / 256) * (p.Kdim / 128) * p.splits),
+                       dim3(512), 0, st, p);
+    return;
+  }
   if (bm == 128 && bn == 128) wgrad_launch_t<128, 128>(p, x3, st, np);
   else if (bm == 128) wgrad_launch_t<128, 64>(p, x3, st, np);
   else if (bn == 128) wgrad_launch_t<64, 128>(p, x3, st, np);

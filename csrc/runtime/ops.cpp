@@ -187,7 +187,7 @@ int wgrad_blocks_per_cu(int bm, int bn) {
     const char* e = std::getenv("CDP_WGRAD_PIPE");
     return !(e && e[0] == '0');
   }();
-  if (f16x2_mode() && pipe) return (bm + bn) >= 192 ? 2 : 3;
+  if (f16x2_mode() && pipe) return bm >= 256 ? 1 : (bm + bn) >= 192 ? 2 : 3;
   if (f16x2_mode()) return (bm + bn) >= 256 ? 3 : (bm + bn) >= 192 ? 4 : 6;
   if (x3_family()) return (bm + bn) >= 256 ? 2 : (bm + bn) >= 192 ? 3 : 5;
   return std::max(1, std::min(4, (160 * 1024) / (2 * 32 * (bm + bn + 8) * 4)));
@@ -255,6 +255,15 @@ WgradPlan plan_wgrad(int Cout, int Kdim, long long M) {
   WgradPlan w;
   w.bm = Cout >= 128 ? 128 : 64;
   w.bn = (Kdim % 128 == 0) ? 128 : 64;
+  // 256x128 f16x2 tiles, 8 waves, one workgroup per CU (pipelined kernel only; CDP_WGRAD_BM=128
+  // for the 128-wide tiles). Measured on MI355X, VGG-11 B=256: 156.0k -> 161.7k img/s (the x
+  // gather and split are shared by four co waves instead of two)
+  static const bool wide = [] {
+    const char* e = std::getenv("CDP_WGRAD_BM");
+    const char* q = std::getenv("CDP_WGRAD_PIPE");
+    return !(e && std::atoi(e) != 256) && !(q && q[0] == '0');
+  }();
+  if (wide && f16x2_mode() && Cout >= 256 && Cout % 4 == 0 && w.bn == 128) w.bm = 256;
   const long long tiles = (long long)((Cout + w.bm - 1) / w.bm) * ((Kdim + w.bn - 1) / w.bn);
   const int mt = (int)std::min<long long>((M + 31) / 32, 1 << 30);
   const int slots = wgrad_blocks_per_cu(w.bm, w.bn) * num_cus();
