@@ -462,7 +462,11 @@ int bn_bwd_grid(int N, int H, int W, int C, bool pool) {
   const long long npix = (long long)N * (pool ? (H / 2) * (W / 2) : H * W);
   long long b = (npix + ppb - 1) / ppb;
   // keep >= ~8 pixels per thread lane for reduction efficiency, <= 1024 partial rows
+  // but never fewer workgroups than CUs while there are rows for them: the deep VGG layers
+  // (2x2 / 4x4 maps) otherwise ran 16-128 workgroups, latency-bound at ~11 us per kernel
+  const long long rows = b;
   b = (b + 7) / 8;
+  if (b < 256) b = rows < 256 ? rows : 256;
   if (b > 1024) b = 1024;
   if (b < 1) b = 1;
   return (int)b;
