@@ -4,205 +4,337 @@
 Metric/config from BASELINE.json: "images/sec (whole node) VGG-11 CIFAR-shaped at 1/2/4/8 MI355X".
 One step = the reference's full training iteration (``/root/reference/src/Part 3/main.py:88-97``):
 batch fetch + RandomCrop/Flip/Normalize (on-GPU kernel), zero_grad, forward, CrossEntropy, backward
-with the bucketed RCCL all-reduce overlapped (DDP wrapper when N > 1), SGD(momentum 0.9,
-wd 1e-4) step. fp32 end to end (the reference's precision), random-init weights, synthetic uint8
-CIFAR-10-shaped images resident on the GPU. Weak scaling by default: 256 images per GPU per step
-(the reference's per-process batch); ``--scaling strong`` keeps the reference's global 256.
+with the gradient sync of ``--strategy`` (DDP wrapper by default: bucketed RCCL all-reduce
+overlapped with backward), SGD(momentum 0.9, wd 1e-4) step. fp32 numerics (the reference's
+precision), random-init weights, synthetic uint8 CIFAR-10-shaped images resident on the GPU. The
+whole step is captured once as a hipGraph and replayed (eager fallback if capture fails).
 
-Usage:  python bench.py [--gpus N --steps K --warmup W]
-        (N > 1 is launched by the driver with torch.distributed.run, one rank per GPU)
-Prints ONE JSON line on rank 0.
+Scaling: ``value`` is for ``--scaling`` (weak by default: 256 images per GPU per step, the
+reference's per-process batch at W=1). For N > 1 the line also carries ``strong``: the reference's
+own rule -- a fixed global batch of 256 split ``int(256/W)`` per rank
+(``/root/reference/src/Part 2a/main.py:22``) -- and ``exposed_comm_ms``: ms/step with sync minus
+ms/step of the same step without gradient sync (the part of the all-reduce backward did not hide).
+
+Launch:
+  python bench.py --gpus N ...            N > 1 without WORLD_SIZE: this process starts N rank
+                                          processes itself (one per GPU) and never touches a GPU
+  torchrun --nproc-per-node N bench.py --gpus N ...   the driver's way; same result
+  python bench.py --gpus 2 --device cpu   gloo/CPU smoke of the multi-process path (no GPU)
+Rank 0 prints ONE JSON line; any failing rank makes the launcher exit non-zero.
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
-import torch
-
 BASELINE_IMG_S = 322.9  # BASELINE.md: reference Part 1, single process, B=256 (measured, CPU)
 METRIC = "images/sec (whole node) VGG-11 CIFAR-shaped at 1/2/4/8 MI355X; scaling eff"
+REF_GLOBAL_BATCH = 256
 
 
-def parse():
+def parse(argv=None):
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=50)
     p.add_argument("--warmup", type=int, default=10)
     p.add_argument("--model", default="vgg11")
-    p.add_argument("--local-batch", type=int, default=256)
+    p.add_argument("--local-batch", type=int, default=256, help="per-rank batch for weak scaling")
     p.add_argument("--scaling", default="weak", choices=["weak", "strong"])
     p.add_argument("--strategy", default="ddp", choices=["ddp", "bucketed_overlap", "allreduce_blocking",
                                                           "gather_scatter"])
     p.add_argument("--no-graph", action="store_true", help="eager steps instead of one hipGraph replay per step")
-    p.add_argument("--graph", action="store_true",
-                   help="force hipGraph capture also for N > 1 (default: graph on 1 GPU, eager multi-GPU: at "
-                        "B=256/GPU the step is GPU-bound, eager and graph time within noise)")
+    p.add_argument("--no-extra", action="store_true",
+                   help="skip the secondary measurements (strong-scaling point, no-sync step for exposed comm)")
     p.add_argument("--backend", default="native", choices=["native", "torch"],
                    help="torch = stock PyTorch-ROCm ops + torch DDP (comparison only)")
     p.add_argument("--precision", default="fp32", choices=["fp32", "bf16"],
                    help="fp32 (default, the reference's precision; conv GEMMs fp32-accurate via the f16x2 "
-                        "split, or CDP_CONV_GEMM=x3|f32) or bf16 (conv GEMM operands rounded to bf16, fp32 accumulation: "
-                        "the non-parity fast mode)")
+                        "split, or CDP_CONV_GEMM=x3|f32) or bf16 (conv GEMM operands rounded to bf16, fp32 "
+                        "accumulation: the non-parity fast mode)")
     p.add_argument("--bucket-cap-mb", type=float, default=None)
     p.add_argument("--dataset-size", type=int, default=50000)
-    return p.parse_args()
+    p.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
+                   help="cpu = gloo smoke mode of the multi-process path (reference ops, tiny sizes)")
+    return p.parse_args(argv)
 
 
-def _dbg(msg):
-    if os.environ.get("CDP_BENCH_DEBUG"):
-        print(f"[bench] {msg}", file=sys.stderr, flush=True)
+# ---------------------------------------------------------------------------------- launcher
+def _free_port() -> int:
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
 
 
-def main():
+def launch(args) -> int:
+    """Start ``--gpus`` rank processes (this process imports no GPU code and never execs)."""
+    n = args.gpus
+    port = os.environ.get("MASTER_PORT") or str(_free_port())
+    procs = []
+    for r in range(n):
+        env = dict(os.environ)
+        env.update(RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+        env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        if args.device == "cpu":
+            env.setdefault("OMP_NUM_THREADS", "1")
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc = 0
+    try:
+        alive = list(procs)
+        while alive:
+            for p in list(alive):
+                r = p.poll()
+                if r is None:
+                    continue
+                alive.remove(p)
+                if r != 0 and rc == 0:
+                    rc = r
+                    print(f"[bench] rank {procs.index(p)} exited with {r}; stopping the others", file=sys.stderr)
+                    for q in alive:
+                        q.terminate()
+            time.sleep(0.05)
+    except KeyboardInterrupt:
+        for p in procs:
+            p.terminate()
+        rc = 130
+    for p in procs:
+        try:
+            p.wait(timeout=30)
+        except subprocess.TimeoutExpired:
+            p.kill()
+    return rc if rc >= 0 else 128 - rc
+
+
+# ---------------------------------------------------------------------------------- one rank
+class _Run:
+    """Builds model/optimizer/data for one (local batch, sync on/off) point and times it."""
+
+    def __init__(self, args, world, rank, dev, local_batch, sync_grads=True):
+        import torch
+
+        import cs744_distributed_data_parallel_amd as cdp
+        from cs744_distributed_data_parallel_amd.data import (
+            DeviceLoader,
+            DistributedSampler,
+            synthetic_cifar10,
+            synthetic_imagenet,
+        )
+
+        self.torch, self.cdp = torch, cdp
+        self.args, self.world, self.dev, self.local_batch = args, world, dev, local_batch
+        self.sync_grads = sync_grads and world > 1
+        cdp.utils.seed_everything(0)
+        self.imagenet = args.model.startswith("resnet")
+        size = args.dataset_size if dev.type == "cuda" else min(args.dataset_size, 8 * local_batch)
+        size = max(size, local_batch * world)  # at least one batch per rank
+        if self.imagenet:  # BASELINE.json config #5: ResNet-50, ImageNet-shaped synthetic
+            ds = synthetic_imagenet(min(size, 4 * local_batch * world), seed=0, device=dev)
+        else:
+            ds = synthetic_cifar10(size, seed=0, device=dev)
+        sampler = DistributedSampler(ds, num_replicas=world, rank=rank) if world > 1 else None
+        self.loader = DeviceLoader(ds, local_batch, sampler=sampler, shuffle=(world == 1), train=True)
+        strategy = args.strategy
+        self.sync = None
+        if args.backend == "native":
+            model = cdp.get_model(args.model).to(dev)
+            if world > 1 and strategy == "ddp":
+                model = cdp.DistributedDataParallel(model, bucket_cap_mb=args.bucket_cap_mb)
+            if world > 1 and strategy == "bucketed_overlap":
+                self.sync = cdp.parallel.BucketedOverlap(model, bucket_cap_mb=args.bucket_cap_mb)
+            self.opt = cdp.SGD(model.parameters(), lr=0.1, momentum=0.9, weight_decay=1e-4)
+            self.crit = cdp.CrossEntropyLoss()
+        else:
+            os.environ["CDP_FORCE_REFERENCE"] = "1"
+            model = cdp.get_model(args.model).to(dev).to(memory_format=torch.channels_last)
+            if world > 1:
+                model = torch.nn.parallel.DistributedDataParallel(
+                    model, device_ids=[dev.index] if dev.type == "cuda" else None)
+            self.opt = torch.optim.SGD(model.parameters(), lr=0.1, momentum=0.9, weight_decay=1e-4)
+            self.crit = torch.nn.CrossEntropyLoss()
+        self.model = model
+        self.order = self.loader._order()
+        self.nb = max(1, self.order.numel() // local_batch)
+        self.static_idx = torch.empty(local_batch, dtype=torch.int64, device=dev)
+        self.graph = None
+
+    def _set_batch(self, i):
+        s = (i % self.nb) * self.local_batch
+        self.static_idx.copy_(self.order[s:s + self.local_batch], non_blocking=True)
+
+    def body(self):
+        import contextlib
+
+        cdp, strategy = self.cdp, self.args.strategy
+        x, y = self.loader.batch(self.static_idx, 0, self.local_batch)
+        self.opt.zero_grad()
+        nosync = (not self.sync_grads and self.world > 1 and hasattr(self.model, "no_sync"))
+        with (self.model.no_sync() if nosync else contextlib.nullcontext()):
+            out = self.model(x)
+            if self.sync is not None and self.sync_grads:
+                self.sync.prepare(out)
+            loss = self.crit(out, y)
+            loss.backward()
+        if self.sync_grads and strategy == "allreduce_blocking":
+            cdp.parallel.average_gradients_allreduce(self.model)
+        elif self.sync_grads and strategy == "gather_scatter":
+            cdp.parallel.average_gradients_gather_scatter(self.model)
+        self.opt.step()
+        return loss
+
+    def prepare(self, warmup, dbg):
+        torch = self.torch
+        cuda = self.dev.type == "cuda"
+        # eager warmup (includes the bucket rebuild in ready order after iteration 1)
+        for i in range(max(3, warmup)):
+            self._set_batch(i)
+            self.body()
+        if cuda:
+            torch.cuda.synchronize()
+        dbg("eager warmup done")
+        if self.args.no_graph or not cuda:
+            return
+        try:
+            s = torch.cuda.Stream()
+            s.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(s):
+                for _ in range(2):
+                    self.body()
+            torch.cuda.current_stream().wait_stream(s)
+            torch.cuda.synchronize()
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                self.body()
+            torch.cuda.synchronize()
+            for i in range(2):  # warm replays
+                self._set_batch(i)
+                g.replay()
+            torch.cuda.synchronize()
+            self.graph = g
+            dbg("captured")
+        except Exception as e:  # pragma: no cover - depends on the runtime
+            print(f"[bench] hipGraph capture failed ({e!r}); timing eager steps", file=sys.stderr)
+            self.graph = None
+            torch.cuda.synchronize()
+
+    def time(self, steps, dist):
+        torch = self.torch
+        cuda = self.dev.type == "cuda"
+        if self.world > 1:
+            dist.barrier()
+        if cuda:
+            torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for i in range(steps):
+            self._set_batch(i)
+            if self.graph is not None:
+                self.graph.replay()
+            else:
+                self.body()
+        if cuda:
+            torch.cuda.synchronize()
+        if self.world > 1:
+            dist.barrier()
+        el = time.perf_counter() - t0
+        el_t = torch.tensor([el], dtype=torch.float64, device=self.dev)
+        if self.world > 1:
+            dist.all_reduce(el_t, "max")  # the slowest rank defines the step
+        return float(el_t.item()) / steps * 1e3
+
+    def release(self):
+        if self.graph is not None:
+            self.graph.reset()
+        self.graph = None
+        # drop the autograd hooks of this point's reducer before the next point builds its own
+        if isinstance(getattr(self.model, "reducer", None), self.cdp.parallel.reducer.GradReducer):
+            self.model.reducer.remove()
+        if self.sync is not None:
+            self.sync.remove()
+            self.sync = None
+
+
+def rank_main(args) -> int:
     import faulthandler
 
     faulthandler.enable()
-    args = parse()
     # hang guard: a stuck collective or kernel ends the process (with every thread's traceback)
     # instead of holding the node; generous against the ~1 min a run takes
     faulthandler.dump_traceback_later(float(os.environ.get("CDP_BENCH_TIMEOUT_S", "1200")), exit=True)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if os.environ.get("CDP_BENCH_FAIL_RANK") == str(rank):  # launcher test hook
+        raise SystemExit(f"[bench] rank {rank}: CDP_BENCH_FAIL_RANK")
     if world != args.gpus:
         print(f"[bench] note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
 
+    import torch
+
     import cs744_distributed_data_parallel_amd as cdp
     from cs744_distributed_data_parallel_amd import distributed as dist
-    from cs744_distributed_data_parallel_amd.data import (
-        DeviceLoader,
-        DistributedSampler,
-        synthetic_cifar10,
-        synthetic_imagenet,
-    )
 
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
-    if world > 1:
-        # collectives that stall longer than 5 minutes are aborted by the communicator's watchdog
-        dist.init_process_group("rccl" if args.backend == "native" else "nccl", rank=rank, world_size=world,
-                                comm_timeout_s=300.0)
-    if args.backend == "native":
-        cdp._native.lib()  # fail loudly if the HIP extension is missing
-        if args.precision == "bf16":
-            cdp._native.lib().set_conv_gemm("bf16")
+    def dbg(msg):
+        if os.environ.get("CDP_BENCH_DEBUG"):
+            print(f"[bench r{rank}] {msg}", file=sys.stderr, flush=True)
 
-    local_batch = args.local_batch if args.scaling == "weak" else max(1, 256 // world)
-    global_batch = local_batch * world
-    cdp.utils.seed_everything(0)
-
-    imagenet = args.model.startswith("resnet")
-    if imagenet:  # BASELINE.json config #5: ResNet-50, ImageNet-shaped synthetic
-        ds = synthetic_imagenet(min(args.dataset_size, 4 * local_batch * world), seed=0, device=dev)
-    else:
-        ds = synthetic_cifar10(args.dataset_size, seed=0, device=dev)
-    sampler = DistributedSampler(ds, num_replicas=world, rank=rank) if world > 1 else None
-    loader = DeviceLoader(ds, local_batch, sampler=sampler, shuffle=(world == 1), train=True)
-
-    if args.backend == "native":
-        model = cdp.get_model(args.model).to(dev)
-        if world > 1 and args.strategy == "ddp":
-            model = cdp.DistributedDataParallel(model, bucket_cap_mb=args.bucket_cap_mb)
-        sync = None
-        if world > 1 and args.strategy == "bucketed_overlap":
-            sync = cdp.parallel.BucketedOverlap(model, bucket_cap_mb=args.bucket_cap_mb)
-        opt = cdp.SGD(model.parameters(), lr=0.1, momentum=0.9, weight_decay=1e-4)
-        crit = cdp.CrossEntropyLoss()
-    else:
-        os.environ["CDP_FORCE_REFERENCE"] = "1"
-        model = cdp.get_model(args.model).to(dev).to(memory_format=torch.channels_last)
-        sync = None
+    cpu = args.device == "cpu"
+    if cpu:
+        dev = torch.device("cpu")
+        torch.set_num_threads(int(os.environ.get("OMP_NUM_THREADS", "1")))
         if world > 1:
-            model = torch.nn.parallel.DistributedDataParallel(model, device_ids=[local])
-        opt = torch.optim.SGD(model.parameters(), lr=0.1, momentum=0.9, weight_decay=1e-4)
-        crit = torch.nn.CrossEntropyLoss()
+            dist.init_process_group("gloo", rank=rank, world_size=world)
+    else:
+        torch.cuda.set_device(local)
+        dev = torch.device("cuda", local)
+        if world > 1:
+            # collectives that stall longer than 5 minutes are aborted by the communicator's watchdog
+            dist.init_process_group("rccl" if args.backend == "native" else "nccl", rank=rank, world_size=world,
+                                    comm_timeout_s=300.0)
+        if args.backend == "native":
+            cdp._native.lib()  # fail loudly if the HIP extension is missing
+            if args.precision == "bf16":
+                cdp._native.lib().set_conv_gemm("bf16")
+    ranks_seen = dist.ranks_seen() if world > 1 else 1
+    comm_kind = ("rccl-native" if dist.native_communicator() is not None else
+                 ("gloo" if cpu else "torch-nccl")) if world > 1 else "none"
 
-    order = loader._order()
-    nb = max(1, order.numel() // local_batch)
-    static_idx = torch.empty(local_batch, dtype=torch.int64, device=dev)
+    strong_lb = max(1, REF_GLOBAL_BATCH // world)
+    main_lb = args.local_batch if args.scaling == "weak" else strong_lb
 
-    def step(i):
-        s = (i % nb) * local_batch
-        static_idx.copy_(order[s:s + local_batch], non_blocking=True)
-        return i
+    run = _Run(args, world, rank, dev, main_lb, sync_grads=True)
+    run.prepare(args.warmup, dbg)
+    ms = run.time(args.steps, dist)
+    hipgraph = run.graph is not None
+    run.release()
+    del run
 
-    def body():
-        x, y = loader.batch(static_idx, 0, local_batch)
-        opt.zero_grad()
-        out = model(x)
-        if sync is not None:
-            sync.prepare(out)
-        loss = crit(out, y)
-        loss.backward()
-        if world > 1 and args.strategy == "allreduce_blocking":
-            cdp.parallel.average_gradients_allreduce(model)
-        elif world > 1 and args.strategy == "gather_scatter":
-            cdp.parallel.average_gradients_gather_scatter(model)
-        opt.step()
-        return loss
+    extra = {}
+    if world > 1 and not args.no_extra:
+        nos = _Run(args, world, rank, dev, main_lb, sync_grads=False)
+        nos.prepare(args.warmup, dbg)
+        ms_nosync = nos.time(args.steps, dist)
+        nos.release()
+        del nos
+        extra["ms_per_step_no_sync"] = round(ms_nosync, 4)
+        extra["exposed_comm_ms"] = round(max(0.0, ms - ms_nosync), 4)
+        other_lb = strong_lb if args.scaling == "weak" else args.local_batch
+        if other_lb != main_lb:
+            oth = _Run(args, world, rank, dev, other_lb, sync_grads=True)
+            oth.prepare(args.warmup, dbg)
+            ms_o = oth.time(args.steps, dist)
+            oth.release()
+            del oth
+            key = "strong" if args.scaling == "weak" else "weak"
+            extra[key] = {"value": round(other_lb * world / ms_o * 1e3, 1), "ms_per_step": round(ms_o, 4),
+                          "global_batch": other_lb * world, "local_batch": other_lb}
 
-    # warmup (eager; includes bucket rebuild in ready order after iteration 1)
-    n_eager_warm = max(3, args.warmup)
-    for i in range(n_eager_warm):
-        step(i)
-        body()
-    torch.cuda.synchronize()
-    _dbg("eager warmup done")
-
-    graph = None
-    use_graph = (not args.no_graph and args.strategy in ("ddp", "bucketed_overlap")
-                 and (world == 1 or args.graph))
-    if use_graph:
-        try:
-            s = torch.cuda.Stream()
-            s.wait_stream(torch.cuda.current_stream())
-            with torch.cuda.stream(s):
-                for _ in range(2):
-                    body()
-            torch.cuda.current_stream().wait_stream(s)
-            torch.cuda.synchronize()
-            _dbg("side-stream warmup done")
-            graph = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(graph):
-                static_loss = body()
-            torch.cuda.synchronize()
-            _dbg("captured")
-            for i in range(2):  # warm replays
-                step(i)
-                graph.replay()
-            torch.cuda.synchronize()
-        except Exception as e:  # pragma: no cover - depends on the runtime
-            print(f"[bench] hipGraph capture failed ({e!r}); timing eager steps", file=sys.stderr)
-            graph = None
-            torch.cuda.synchronize()
-
-    def run_one(i):
-        step(i)
-        if graph is not None:
-            graph.replay()
-        else:
-            body()
-
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        run_one(i)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    el = time.perf_counter() - t0
-    el_t = torch.tensor([el], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(el_t, "max")
-    el = float(el_t.item())
-    ms = el / args.steps * 1e3
-    img_s = global_batch * args.steps / el
+    global_batch = main_lb * world
+    img_s = global_batch / ms * 1e3
+    imagenet = args.model.startswith("resnet")
     if rank == 0:
         rec = {
             "metric": METRIC if not imagenet else
@@ -221,29 +353,33 @@ def main():
                      if imagenet else
                      "synthetic (random uint8 CIFAR-10-shaped 32x32x3, GPU-resident, on-GPU crop/flip/normalize); ")
                     + "random-init weights",
+            "ranks_seen": ranks_seen,
             "config": {
                 "model": {"vgg11": "VGG-11", "resnet50": "ResNet-50"}.get(args.model, args.model),
                 "global_batch": global_batch,
-                "local_batch": local_batch,
+                "local_batch": main_lb,
                 "seq_len": None,
                 "image_shape": [3, 224, 224] if imagenet else [3, 32, 32],
                 "parallelism": f"dp{world}",
                 "strategy": args.strategy if world > 1 else "single",
+                "comm": comm_kind,
                 "backend": args.backend,
-                "hipgraph": graph is not None,
+                "device": "cpu" if cpu else "mi355x",
+                "hipgraph": hipgraph,
                 "optimizer": "SGD(lr=0.1, momentum=0.9, wd=1e-4)",
                 # conv GEMM numerics, all with fp32 operands and fp32 accumulation: "f16x2" =
                 # power-of-two-scaled operands split into two fp16 terms, three products on the
-                # fp16 MFMA; "x3" = 3-term bf16 split, six products on the bf16 MFMA (both: error vs
-                # fp64 <= the exact fp32 MFMA's, tests/test_kernels_gpu.py, docs/PERF.md); "f32" =
-                # exact fp32-input MFMA
-                "conv_gemm": _conv_gemm_engine(args.backend),
+                # fp16 MFMA; "x3" = 3-term bf16 split, six products on the bf16 MFMA; "f32" =
+                # exact fp32-input MFMA (docs/PERF.md, tests/test_kernels_gpu.py)
+                "conv_gemm": "reference" if cpu else _conv_gemm_engine(args.backend),
             },
         }
+        rec.update(extra)
         print(json.dumps(rec), flush=True)
     if world > 1:
         dist.destroy_process_group()
     faulthandler.cancel_dump_traceback_later()
+    return 0
 
 
 def _conv_gemm_engine(backend):
@@ -257,5 +393,12 @@ def _conv_gemm_engine(backend):
         return "reference"
 
 
+def main(argv=None) -> int:
+    args = parse(argv)
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        return launch(args)
+    return rank_main(args)
+
+
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

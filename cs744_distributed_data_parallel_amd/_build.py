@@ -73,6 +73,7 @@ def write_ninja() -> str:
             "-shared -fPIC",
             f"-L{lib}",
             "-lc10 -lc10_hip -ltorch -ltorch_cpu -ltorch_hip -ltorch_python -lrccl",
+            "-L/opt/rocm/lib -lrocprofiler-sdk-roctx -Wl,-rpath,/opt/rocm/lib",
             f"-Wl,-rpath,{lib}",
         ]
     )

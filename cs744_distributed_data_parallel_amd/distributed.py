@@ -30,7 +30,7 @@ __all__ = [
     "ReduceOp", "reduce_op", "init_process_group", "destroy_process_group", "is_initialized", "get_rank",
     "get_world_size", "get_local_rank", "get_backend", "all_reduce", "broadcast", "gather", "scatter", "all_gather",
     "all_gather_into_tensor", "reduce_scatter_tensor", "reduce", "barrier", "communicator_for", "device",
-    "set_timeout", "healthy",
+    "set_timeout", "healthy", "ranks_seen",
 ]
 
 
@@ -73,6 +73,40 @@ def _local_rank(rank: int) -> int:
     return rank % n
 
 
+_init_generation = 0
+
+
+def _init_native_rccl(rank, world_size, local, store, timeout_s) -> Optional[RcclCommunicator]:
+    """Start the native communicator; every rank makes the SAME choice.
+
+    Each rank posts ok/fail to the TCP store and reads every peer's flag before deciding, so a
+    failure on one rank can never leave the others on a different communicator (which would hang or
+    mismatch the next collective). Any failure is fatal on every rank unless
+    ``CDP_RCCL_FALLBACK=1``, in which case all ranks agree to use the torch nccl (=RCCL) group.
+    """
+    global _init_generation
+    _init_generation += 1
+    gen = _init_generation
+    comm, err = None, ""
+    try:
+        comm = RcclCommunicator(rank, world_size, local, store, timeout_s, tag=f"g{gen}")
+    except RuntimeError as e:  # e.g. an RCCL build without this topology
+        err = str(e) or "RuntimeError"
+    store.set(f"cdp_rccl_ok/g{gen}/{rank}", "0" if comm is None else "1")
+    keys = [f"cdp_rccl_ok/g{gen}/{r}" for r in range(world_size)]
+    store.wait(keys, datetime.timedelta(seconds=max(60.0, timeout_s)))
+    failed = [r for r, k in enumerate(keys) if store.get(k) != b"1"]
+    if not failed:
+        return comm
+    if comm is not None:
+        comm.shutdown()
+    msg = f"native RCCL communicator failed on rank(s) {failed}" + (f" (here: {err})" if err else "")
+    if os.environ.get("CDP_RCCL_FALLBACK", "0") != "1":
+        raise RuntimeError(msg + "; set CDP_RCCL_FALLBACK=1 to run every rank on the torch nccl process group")
+    warnings.warn(msg + "; all ranks use the torch nccl process group")
+    return None
+
+
 def init_process_group(
     backend: Optional[str] = None,
     init_method: Optional[str] = None,
@@ -100,11 +134,7 @@ def init_process_group(
         if backend == "rccl" and _native.available():
             store = tdist.distributed_c10d._get_default_store()
             t = comm_timeout_s if comm_timeout_s is not None else timeout.total_seconds()
-            try:
-                _S.rccl = RcclCommunicator(rank, world_size, local, store, t)
-            except RuntimeError as e:  # e.g. an RCCL build without this topology: keep torch's RCCL PG
-                warnings.warn(f"native RCCL communicator unavailable ({e}); using the torch nccl process group")
-                _S.rccl = None
+            _S.rccl = _init_native_rccl(rank, world_size, local, store, t)
     elif backend == "gloo":
         tdist.init_process_group("gloo", init_method=init_method, rank=rank, world_size=world_size, timeout=timeout)
         _S.device = torch.device("cpu")
@@ -164,6 +194,19 @@ def communicator_for(t: Optional[torch.Tensor] = None) -> Communicator:
 
 def native_communicator() -> Optional[RcclCommunicator]:
     return _S.rccl
+
+
+def ranks_seen() -> int:
+    """How many ranks the data-path communicator actually formed: ``ncclCommCount`` on the native
+    RCCL communicator, else a SUM all-reduce of ones over the process group (gloo / torch nccl)."""
+    if not tdist.is_initialized():
+        return 1
+    if _S.rccl is not None:
+        return _S.rccl.count()
+    dev = _S.device if (_S.device is not None and _S.device.type == "cuda") else torch.device("cpu")
+    t = torch.ones(1, dtype=torch.int64, device=dev)
+    tdist.all_reduce(t)
+    return int(t.item())
 
 
 def set_timeout(seconds: float):

@@ -15,6 +15,7 @@ Reference call sites covered: ``dist.gather``/``dist.scatter`` (Part 2a ``:121-1
 from __future__ import annotations
 
 import datetime
+import os
 from typing import List, Optional
 
 import torch
@@ -122,9 +123,18 @@ class RcclCommunicator(Communicator):
         self.rank, self.size, self.device = rank, size, device
         self._c = C.RcclComm(bytes(uid), rank, size, device, float(timeout_s))
 
+        spec = os.environ.get("CDP_REDUCER_TEST_POSTOP")
+        if spec:  # "delay_us:scale" -- test hook, see RcclComm::set_test_postop
+            d, sc = spec.split(":")
+            self._c.set_test_postop(float(d), float(sc))
+
     @property
     def native(self):
         return self._c
+
+    def count(self) -> int:
+        """Ranks in the communicator as RCCL reports them (``ncclCommCount``)."""
+        return int(self._c.count())
 
     def all_reduce(self, t, op="sum", async_op=False):
         w = self._c.all_reduce(t, _norm_op(op), async_op)

@@ -13,6 +13,7 @@ all-reduce overlapped with autograd" (BASELINE.json).
 from __future__ import annotations
 
 import threading
+import time
 from typing import List, Optional, Sequence, Tuple
 
 import torch
@@ -54,6 +55,8 @@ class _PyReducer:
         self.iterations = 0
         self.launched_total = 0
         self._lock = threading.Lock()
+        self.trace = False
+        self.log: List[Tuple[str, int, int]] = []
         self._handles = [p.register_post_accumulate_grad_hook(self._make_hook(i)) for i, p in enumerate(params)]
 
     @property
@@ -75,6 +78,12 @@ class _PyReducer:
 
     def disarm(self):
         self.armed = False
+
+    def set_trace(self, on):
+        self.trace, self.log = bool(on), []
+
+    def trace_log(self):
+        return list(self.log)
 
     def prepare_for_backward(self, outputs):
         with self._lock:
@@ -120,6 +129,8 @@ class _PyReducer:
         if from_hook:
             if self.record_order:
                 self.order.append(i)
+            if self.trace:
+                self.log.append(("h", i, time.monotonic_ns()))
             if not self.callback_queued:
                 self.callback_queued = True
                 torch.autograd.Variable._execution_engine.queue_callback(self._finalize)
@@ -131,6 +142,8 @@ class _PyReducer:
                 self.next_launch += 1
 
     def _launch(self, b):
+        if self.trace:
+            self.log.append(("l", b, time.monotonic_ns()))
         self.works[b] = self.comm.all_reduce(self.bucket_views[b], "avg" if self.average else "sum", async_op=True)
         self.launched_total += 1
 
@@ -138,6 +151,8 @@ class _PyReducer:
         with self._lock:
             if not self.armed:
                 return
+            if self.trace:
+                self.log.append(("f", -1, time.monotonic_ns()))
             if self.next_launch < len(self.pending):
                 if self.find_unused:
                     for i in range(len(self.params)):
@@ -208,6 +223,8 @@ class GradReducer:
             starts.append(hi + 1 if self.arena_in_ready_order else lo)
         self.bucket_starts = starts
         grad_views = a.grad_views()
+        if self._impl is not None and getattr(self, "_trace", False):
+            self._old_log = self._old_log + [tuple(e) for e in self._impl.trace_log()]  # keep across rebuilds
         if self._impl is not None:
             # drop every reference to the old AccumulateGrad nodes first so that fresh ones are
             # created on the current stream (see rebind_if_stream_changed)
@@ -226,6 +243,8 @@ class GradReducer:
             self._impl = C.Reducer(list(a.params), grad_views, views, starts, rccl, pg, self.find_unused, self.average)
         else:
             self._impl = _PyReducer(list(a.params), grad_views, views, starts, self.comm, self.find_unused, self.average)
+        if getattr(self, "_trace", False):
+            self._impl.set_trace(True)
 
     @property
     def native(self) -> bool:
@@ -264,6 +283,16 @@ class GradReducer:
 
     def disarm(self):
         self._impl.disarm()
+
+    def set_trace(self, on: bool = True):
+        """Record ('h', param) at every gradient-ready hook, ('l', bucket) at every bucket
+        launch and ('f', -1) at the end-of-backward callback (see :meth:`trace_log`)."""
+        self._trace = bool(on)
+        self._old_log = []
+        self._impl.set_trace(bool(on))
+
+    def trace_log(self) -> List[Tuple[str, int, int]]:
+        return list(getattr(self, "_old_log", [])) + [tuple(e) for e in self._impl.trace_log()]
 
     def ready_order(self) -> List[int]:
         return list(self._impl.ready_order())

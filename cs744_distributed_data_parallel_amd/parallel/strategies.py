@@ -120,12 +120,26 @@ class BucketedOverlap:
         )
         self._rebuild = rebuild_in_ready_order
         self._rebuilt = False
+        # bucket rebuild and AccumulateGrad re-binding must happen BEFORE the forward that builds
+        # the autograd graph: afterwards that graph holds the old AccumulateGrad nodes (bound to
+        # the stream they were created on, illegal to run inside a hipGraph capture on another)
+        self._pre_hook = model.register_forward_pre_hook(self._before_forward)
 
-    def prepare(self, *outputs):
+    def _before_forward(self, module, inputs):
+        if not torch.is_grad_enabled():
+            return None
         if self._rebuild and not self._rebuilt and self.reducer.iterations >= 1:
             self.reducer.rebuild_in_ready_order()
             self._rebuilt = True
         self.reducer.rebind_if_stream_changed()
+        return None
+
+    def remove(self):
+        """Detach from the model (autograd hooks and the forward pre-hook)."""
+        self._pre_hook.remove()
+        self.reducer.remove()
+
+    def prepare(self, *outputs):
         outs = []
         for o in outputs:
             if isinstance(o, torch.Tensor):

@@ -38,7 +38,13 @@ from .parallel import (
     average_gradients_gather_scatter,
 )
 from .utils import PhaseTimer, latest_checkpoint, load_checkpoint, save_checkpoint, seed_everything
+from .utils import profiling
 from .utils.profiling import TraceRecorder
+
+
+def _phase(trace, name):
+    """A traced phase (chrome trace + roctx) or just a roctx range (emitted when CDP_ROCTX=1)."""
+    return trace.phase(name) if trace is not None else profiling.range(name)
 
 
 def train_model(model, train_loader, optimizer, criterion, rank=0, sync=None, strategy="none", max_iters=None,
@@ -47,20 +53,28 @@ def train_model(model, train_loader, optimizer, criterion, rank=0, sync=None, st
     iter_number = 1
     epoch_loss = 0
     timer = timer or PhaseTimer(None)
+    # Part 1/2a/2b print "epochs", Part 3 "iterations" (src/Part 1/main.py:49, src/Part 2a/main.py:104,
+    # src/Part 2b/main.py:104, src/Part 3/main.py:105)
+    unit = "iterations" if strategy in ("ddp", "bucketed_overlap") else "epochs"
     for batch_idx, (data, target) in enumerate(train_loader):
         timer.mark("start")
-        optimizer.zero_grad()
-        predictions = model(data)
-        if isinstance(sync, BucketedOverlap):
-            sync.prepare(predictions)
+        with _phase(trace, "forward"):
+            optimizer.zero_grad()
+            predictions = model(data)
+            if isinstance(sync, BucketedOverlap):
+                sync.prepare(predictions)
         timer.mark("forward")
-        loss = criterion(predictions, target)
-        loss.backward()
-        if strategy == "gather_scatter":
-            average_gradients_gather_scatter(model, rank)
-        elif strategy == "allreduce_blocking":
-            average_gradients_allreduce(model)
-        optimizer.step()
+        with _phase(trace, "backward"):
+            loss = criterion(predictions, target)
+            loss.backward()
+        if strategy in ("gather_scatter", "allreduce_blocking"):
+            with _phase(trace, "sync"):
+                if strategy == "gather_scatter":
+                    average_gradients_gather_scatter(model, rank)
+                else:
+                    average_gradients_allreduce(model)
+        with _phase(trace, "step"):
+            optimizer.step()
         timer.mark("backward")
 
         epoch_loss += loss.detach()
@@ -68,7 +82,7 @@ def train_model(model, train_loader, optimizer, criterion, rank=0, sync=None, st
             on_iter(iter_number, loss)
         if iter_number % 20 == 0:
             epoch_loss = epoch_loss / 20
-            print_fn("Training loss after {} iterations is {}".format(iter_number, epoch_loss))
+            print_fn("Training loss after {} {} is {}".format(iter_number, unit, epoch_loss))
             epoch_loss = 0
             fwd = timer.pop("forward")
             bwd = timer.pop("backward")
@@ -139,19 +153,22 @@ def run(rank, size, epochs, batch_size, args):
 
     start_epoch = 0
     if args.resume and args.checkpoint_dir:
-        path = latest_checkpoint(args.checkpoint_dir)
+        path = _agreed_checkpoint(args.checkpoint_dir, size)
         if path:
             st = load_checkpoint(path, model, optimizer, map_location=device)
             start_epoch = st.get("epoch", 0)
             print("Resumed from {} (epoch {})".format(path, start_epoch))
     trace = TraceRecorder(rank, device) if args.trace else None
+    reducer = _reducer_of(model, sync)
+    if trace is not None and reducer is not None:
+        reducer.set_trace(True)
     for epoch in range(start_epoch, epochs):
         if not args.reference_bn_quirk or epoch == 0:
             model.train()
         start_time = time.time()
         timer = PhaseTimer(device)
         train_model(model, train_loader, optimizer, criterion, rank, sync=sync, strategy=strategy,
-                    max_iters=args.iters, timer=timer)
+                    max_iters=args.iters, timer=timer, trace=trace)
         if device.type == "cuda":
             torch.cuda.synchronize()
         print("Training time after {} epoch is {}".format(epoch + 1, (time.time() - start_time)))
@@ -160,8 +177,45 @@ def run(rank, size, epochs, batch_size, args):
             save_checkpoint(os.path.join(args.checkpoint_dir, f"ckpt_{epoch + 1}.pt"), model, optimizer,
                             epoch=epoch + 1, rank=rank)
     if trace is not None:
-        trace.dump(args.trace)
+        if reducer is not None:
+            trace.add_reducer_log(reducer.trace_log())
+        path = args.trace if size == 1 else "{}.rank{}{}".format(*os.path.splitext(args.trace)[:1], rank,
+                                                                 os.path.splitext(args.trace)[1] or ".json")
+        trace.dump(path)
     return model
+
+
+def _reducer_of(model, sync):
+    if isinstance(model, DistributedDataParallel):
+        return model.reducer
+    if isinstance(sync, BucketedOverlap):
+        return sync.reducer
+    return None
+
+
+def _agreed_checkpoint(directory, size):
+    """Rank 0 picks the checkpoint; every rank must be able to read that same file.
+
+    Only rank 0 writes checkpoints, so without a shared filesystem other ranks would silently start
+    from scratch while rank 0 resumes (diverged replicas, mismatched epoch counts, hung collectives).
+    """
+    path = latest_checkpoint(directory) if dist.get_rank() == 0 else None
+    if size == 1 or not dist.is_initialized():
+        return path
+    import torch.distributed as tdist
+
+    box = [path]
+    tdist.broadcast_object_list(box, src=0)
+    path = box[0]
+    if path is None:
+        return None
+    ok = torch.tensor([1 if os.path.isfile(path) else 0], dtype=torch.int64,
+                      device=dist.device() if dist.device().type == "cuda" else "cpu")
+    tdist.all_reduce(ok, op=tdist.ReduceOp.MIN)
+    if int(ok.item()) != 1:
+        raise RuntimeError(f"--resume: checkpoint {path} (chosen by rank 0) is not readable on every rank; "
+                           "use a shared --checkpoint-dir")
+    return path
 
 
 def init_process(master, port, rank, size, fn, epochs=1, batch_size=256, backend="rccl", args=None):
@@ -197,7 +251,11 @@ def parse_args(argv=None):
     p.add_argument("--seed", type=int, default=0)
     p.add_argument("--checkpoint-dir", default=None)
     p.add_argument("--resume", action="store_true")
-    p.add_argument("--trace", default=None, help="write a chrome trace of phases to this path")
+    p.add_argument("--trace", default=None,
+                   help="write a chrome trace (phases + reducer hook/bucket-launch events) to this path "
+                        "(.rankN suffix per rank when distributed)")
+    p.add_argument("--num-threads", type=int, default=4,
+                   help="CPU intra-op threads for the CPU path (the reference pins 4: src/Part 1/main.py:11)")
     p.add_argument("--reference-bn-quirk", action="store_true",
                    help="reproduce the reference's missing model.train() after the first eval")
     return p.parse_args(argv)
@@ -211,6 +269,8 @@ def main(argv=None):
         args.device_obj = torch.device("cuda" if torch.cuda.is_available() else "cpu")
     else:
         args.device_obj = torch.device(args.device)
+    if args.device_obj.type == "cpu":
+        torch.set_num_threads(args.num_threads)
     if args.strategy is None:
         args.strategy = "ddp" if size > 1 else "none"
     if size > 1 or args.strategy != "none":

@@ -66,7 +66,6 @@ __device__ __forceinline__ void split8h(const float (&v)[8], float s, u32x4& s0,
 
 // PS (pre-split): p.x / p.w hold three bf16 planes each ([3][N][H][W][C], [3][Nout][Kdim], as
 // written by split3_launch) and the tiles are copied to LDS without the split (MODE 0 only).
-// ABL (diagnostic builds only): bit 0 drops the in-loop global loads, bit 1 the in-loop LDS stores
 // NP = 16-bit planes per operand: 3 = fp32-accurate bf16 split (six products), 2 = f16x2
 // (power-of-two-scaled operands as two fp16 terms, three products on v_mfma_f32_32x32x16_f16, see
 // x3_common.h), 1 = plain bf16 operands with fp32 accumulation (one product; the non-parity fast
@@ -79,7 +78,7 @@ __device__ __forceinline__ u32x4 pack8(const float (&v)[8]) {
   return r;
 }
 
-template <int BM, int BN, int MODE, bool DGRAD, bool M16, bool PS = false, int ABL = 0, int NP = 3>
+template <int BM, int BN, int MODE, bool DGRAD, bool M16, bool PS = false, int NP = 3>
 __global__ __launch_bounds__(waves_m<BM>() * 128, (NP == 2 && BM + BN <= 256) ? 2 : (BM + BN >= 256) ? 1 : 2) void
 conv_x3_kernel(ConvGemmParams p) {
   static_assert(!PS || MODE == 0, "pre-split operands need C % 32 == 0");
@@ -468,15 +467,15 @@ conv_x3_kernel(ConvGemmParams p) {
     __syncthreads();
     int kt = kt_begin;
     for (; kt + 1 < kt_end; kt += 2) {
-      if (!(ABL & 1)) load_tile(kt + 2, va0, vb0, kt + 2 < kt_end);
+      load_tile(kt + 2, va0, vb0, kt + 2 < kt_end);
       compute(smem);
-      if (!(ABL & 2)) store_tile(va1, vb1, smem + STAGE);
+      store_tile(va1, vb1, smem + STAGE);
       __syncthreads();
-      if (!(ABL & 1)) load_tile(kt + 3, va1, vb1, kt + 3 < kt_end);
+      load_tile(kt + 3, va1, vb1, kt + 3 < kt_end);
       compute(smem + STAGE);
       // unconditional (past the last tile it stores stale registers into a stage nothing reads),
       // so the split can interleave with the MFMAs above
-      if (!(ABL & 2)) store_tile(va0, vb0, smem);
+      store_tile(va0, vb0, smem);
       __syncthreads();
     }
     if (kt < kt_end) compute(smem);  // odd tile count: the last tile sits in stage 0
@@ -496,8 +495,8 @@ conv_x3_kernel(ConvGemmParams p) {
 template <int BM, int BN, int MODE, bool DGRAD>
 void launch_x3(const ConvGemmParams& p, int ntiles, bool m16, int np, hipStream_t st) {
   const dim3 blk(waves_m<BM>() * 128), grd(ntiles * p.splits);
-  if (np == 1) hipLaunchKernelGGL((conv_x3_kernel<BM, BN, MODE, DGRAD, false, false, 0, 1>), grd, blk, 0, st, p);
-  else if (np == 2) hipLaunchKernelGGL((conv_x3_kernel<BM, BN, MODE, DGRAD, false, false, 0, 2>), grd, blk, 0, st, p);
+  if (np == 1) hipLaunchKernelGGL((conv_x3_kernel<BM, BN, MODE, DGRAD, false, false, 1>), grd, blk, 0, st, p);
+  else if (np == 2) hipLaunchKernelGGL((conv_x3_kernel<BM, BN, MODE, DGRAD, false, false, 2>), grd, blk, 0, st, p);
   else if (m16) hipLaunchKernelGGL((conv_x3_kernel<BM, BN, MODE, DGRAD, true>), grd, blk, 0, st, p);
   else hipLaunchKernelGGL((conv_x3_kernel<BM, BN, MODE, DGRAD, false>), grd, blk, 0, st, p);
 }
@@ -513,41 +512,7 @@ void dispatch_x3(const ConvGemmParams& p, int bm, int bn, bool m16, int np, hipS
   else launch_x3<64, 64, MODE, DGRAD>(p, nt, m16, np, st);
 }
 
-template <int BM, int BN, bool DGRAD>
-void launch_x3ps(const ConvGemmParams& p, int ntiles, hipStream_t st) {
-  hipLaunchKernelGGL((conv_x3_kernel<BM, BN, 0, DGRAD, false, true>), dim3(ntiles * p.splits), dim3(256), 0, st, p);
-}
-
 }  // namespace
-
-// diagnostic: 128x128 forward x3 kernel with parts of the pipeline removed (results are wrong)
-void conv_x3_ablate_launch(const ConvGemmParams& p, int abl, bool ps, hipStream_t st) {
-  const int nt = ((p.M + 127) / 128) * ((p.Nout + 127) / 128);
-  dim3 g(nt * p.splits), b(256);
-  if (ps) {
-    if (abl == 1) hipLaunchKernelGGL((conv_x3_kernel<128, 128, 0, false, false, true, 1>), g, b, 0, st, p);
-    else if (abl == 2) hipLaunchKernelGGL((conv_x3_kernel<128, 128, 0, false, false, true, 2>), g, b, 0, st, p);
-    else if (abl == 3) hipLaunchKernelGGL((conv_x3_kernel<128, 128, 0, false, false, true, 3>), g, b, 0, st, p);
-    else hipLaunchKernelGGL((conv_x3_kernel<128, 128, 0, false, false, true, 0>), g, b, 0, st, p);
-  } else {
-    if (abl == 1) hipLaunchKernelGGL((conv_x3_kernel<128, 128, 0, false, false, false, 1>), g, b, 0, st, p);
-    else if (abl == 2) hipLaunchKernelGGL((conv_x3_kernel<128, 128, 0, false, false, false, 2>), g, b, 0, st, p);
-    else if (abl == 3) hipLaunchKernelGGL((conv_x3_kernel<128, 128, 0, false, false, false, 3>), g, b, 0, st, p);
-    else hipLaunchKernelGGL((conv_x3_kernel<128, 128, 0, false, false, false, 0>), g, b, 0, st, p);
-  }
-}
-
-namespace {
-
-}  // namespace
-
-void conv_x3ps_launch(const ConvGemmParams& p, int bm, int bn, bool dgrad, hipStream_t st) {
-  const int nt = ((p.M + bm - 1) / bm) * ((p.Nout + bn - 1) / bn);
-  if (bm == 128 && bn == 128) dgrad ? launch_x3ps<128, 128, true>(p, nt, st) : launch_x3ps<128, 128, false>(p, nt, st);
-  else if (bm == 128) dgrad ? launch_x3ps<128, 64, true>(p, nt, st) : launch_x3ps<128, 64, false>(p, nt, st);
-  else if (bn == 128) dgrad ? launch_x3ps<64, 128, true>(p, nt, st) : launch_x3ps<64, 128, false>(p, nt, st);
-  else dgrad ? launch_x3ps<64, 64, true>(p, nt, st) : launch_x3ps<64, 64, false>(p, nt, st);
-}
 
 void conv_x3_launch(const ConvGemmParams& p, int bm, int bn, bool dgrad, bool m16, hipStream_t st, int np) {
   if ((p.C % BK) == 0 && (p.Kdim % BK) == 0) {

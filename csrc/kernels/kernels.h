@@ -90,10 +90,6 @@ void conv_igemm_launch(const ConvGemmParams& p, int bm, int bn, bool dgrad, hipS
 // two fp16 terms, three products; needs p.amax_*), 1 = operands rounded to bf16, one product per
 // MAC (the non-parity fast mode)
 void conv_x3_launch(const ConvGemmParams& p, int bm, int bn, bool dgrad, bool m16, hipStream_t st, int np = 3);
-// pre-split operands (x, w = three bf16 planes each, from split3_launch); C % 32 == 0 only
-void conv_x3ps_launch(const ConvGemmParams& p, int bm, int bn, bool dgrad, hipStream_t st);
-void split3_launch(const float* x, long long n, void* planes, hipStream_t st);
-void conv_x3_ablate_launch(const ConvGemmParams& p, int abl, bool ps, hipStream_t st);
 void splitk_reduce_launch(const float* slab, int S, int M, int Nout, const float* bias, float* y, float* part,
                           hipStream_t st, const RowRemap* rr = nullptr, const float* addend = nullptr);
 int splitk_rows_per_part();
@@ -161,6 +157,7 @@ int pad_c4_grid(long long npix);
 void pad_c4_launch(const float* x, long long npix, int C, float* out, float* amax_part, hipStream_t st);
 void stack_mean_launch(const float* const* srcs, int k, long long n, float* dst, hipStream_t st);
 void scale_launch(float* x, long long n, float a, hipStream_t st);
+void delay_scale_launch(float* x, long long n, float a, double delay_us, hipStream_t st);
 void colsum_launch(const float* x, int R, int C, float* out, bool accumulate, hipStream_t st);
 void small_linear_fwd_launch(const float* x, const float* w, const float* b, int B, int I, int O, float* y,
                              hipStream_t st);

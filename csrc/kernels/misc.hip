@@ -480,19 +480,6 @@ int grid_for(long long n) {
 }
 
 
-// ------------------------------------------------------------------ split3
-// x (fp32, n elements) -> three bf16 planes [3][n] with x = h0 + h1 + h2 (x3_common.h)
-__global__ __launch_bounds__(256) void split3_kernel(const float* __restrict__ x, long long n, unsigned* __restrict__ out) {
-  const long long npair = n >> 1;
-  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < npair; i += (long long)gridDim.x * blockDim.x) {
-    const float2 v = reinterpret_cast<const float2*>(x)[i];
-    unsigned a, b, c;
-    split_pair(v.x, v.y, a, b, c);
-    out[i] = a;
-    out[npair + i] = b;
-    out[2 * npair + i] = c;
-  }
-}
 
 // sub-filter transpose for the sub-pixel data gradient: wt[ci][a][b][co] = w[co][kh0+2a][kw0+2b][ci]
 __global__ __launch_bounds__(256) void wtrans_sub_kernel(const float* __restrict__ w, float* __restrict__ wt, int Co,
@@ -552,6 +539,19 @@ void pad_c4_launch(const float* x, long long npix, int C, float* out, float* ama
 void stack_mean_launch(const float* const* srcs, int k, long long n, float* dst, hipStream_t st) {
   hipLaunchKernelGGL(stack_mean_kernel, dim3(grid_for(n)), dim3(256), 0, st, srcs, k, n, dst);
 }
+// Test-only post-op (RcclComm::set_test_postop): every wave first idles ~delay_us with s_sleep
+// (no memory traffic), then scales. Used to prove that consumers wait on the collective's event.
+__global__ __launch_bounds__(256) void delay_scale_kernel(float* __restrict__ x, long long n, float a, int sleeps) {
+  for (int i = 0; i < sleeps; ++i) __builtin_amdgcn_s_sleep(127);
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x)
+    x[i] *= a;
+}
+
+void delay_scale_launch(float* x, long long n, float a, double delay_us, hipStream_t st) {
+  // s_sleep 127 ~ 127*64 cycles ~ 3.4 us at 2.4 GHz
+  const int sleeps = (int)(delay_us / 3.4) + 1;
+  hipLaunchKernelGGL(delay_scale_kernel, dim3(grid_for(n)), dim3(256), 0, st, x, n, a, sleeps);
+}
 void scale_launch(float* x, long long n, float a, hipStream_t st) {
   hipLaunchKernelGGL(scale_kernel, dim3(grid_for(n)), dim3(256), 0, st, x, n, a);
 }
@@ -584,13 +584,6 @@ void maxpool_bwd_launch(const float* gy, const unsigned char* arg, int N, int H,
                         int Ho, int Wo, float* gx, hipStream_t st) {
   hipLaunchKernelGGL(maxpool_bwd_kernel, dim3(grid_for((long long)N * H * W * (C / 4))), dim3(256), 0, st, gy, arg,
                      N, H, W, C, k, s, p, Ho, Wo, gx);
-}
-
-void split3_launch(const float* x, long long n, void* planes, hipStream_t st) {
-  long long b = (n / 2 + 255) / 256;
-  if (b > 4096) b = 4096;
-  if (b < 1) b = 1;
-  hipLaunchKernelGGL(split3_kernel, dim3((unsigned)b), dim3(256), 0, st, x, n, reinterpret_cast<unsigned*>(planes));
 }
 
 void wtrans_sub_launch(const float* w, float* wt, int Co, int KH, int KW, int Ci, int kh0, int kw0, int nkh, int nkw,

@@ -18,7 +18,6 @@ PYBIND11_MODULE(_C, m) {
         "select the conv GEMM engine: x3 (3-term bf16 split), f16x2 (scaled 2-term fp16 split), f32 (exact fp32 "
         "MFMA) or bf16 (bf16 operands, non-parity)");
   m.def("get_conv_gemm", &get_conv_gemm);
-  m.def("bench_presplit", &bench_presplit, "experiment: in-kernel split vs pre-split bf16 planes (conv fwd GEMM)");
   m.def("conv2d_fwd", &conv2d_fwd, py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("stride"), py::arg("pad"),
         py::arg("want_stats") = false, py::arg("x_amax") = py::none(), py::arg("w_amax") = py::none());
   m.def("conv2d_dgrad", &conv2d_dgrad, py::arg("dy"), py::arg("w"), py::arg("in_shape"), py::arg("stride"),
@@ -70,11 +69,14 @@ PYBIND11_MODULE(_C, m) {
       .def_property_readonly("size", &RcclComm::size)
       .def_property_readonly("device", &RcclComm::device)
       .def_property_readonly("stream_ptr", [](RcclComm& c) { return reinterpret_cast<intptr_t>(c.stream()); })
+      .def("count", &RcclComm::count)
       .def("healthy", &RcclComm::healthy)
       .def("error", &RcclComm::error)
       .def("abort", &RcclComm::abort)
       .def("shutdown", &RcclComm::shutdown, py::call_guard<py::gil_scoped_release>())
       .def("set_timeout", &RcclComm::set_timeout)
+      .def("set_test_postop", &RcclComm::set_test_postop, py::arg("delay_us"), py::arg("scale"),
+           "test hook: delay + scale after every all_reduce, inside its completion event")
       .def("timeout", &RcclComm::timeout)
       .def("all_reduce", &RcclComm::all_reduce, py::arg("t"), py::arg("op") = "sum", py::arg("async_op") = false)
       .def("broadcast", &RcclComm::broadcast, py::arg("t"), py::arg("root") = 0, py::arg("async_op") = false)
@@ -102,6 +104,8 @@ PYBIND11_MODULE(_C, m) {
       .def("remove_hooks", &Reducer::remove_hooks)
       .def("ready_order", &Reducer::ready_order)
       .def("disarm", &Reducer::disarm)
+      .def("set_trace", &Reducer::set_trace)
+      .def("trace_log", &Reducer::trace_log)
       .def_property_readonly("iterations", &Reducer::iterations)
       .def_property_readonly("launched_total", &Reducer::launched_total)
       .def_property_readonly("num_buckets", &Reducer::num_buckets);

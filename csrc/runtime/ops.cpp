@@ -980,66 +980,4 @@ at::Tensor avgpool_bwd(const at::Tensor& gy_, std::vector<int64_t> in_shape) {
 }
 
 
-// ---------------------------------------------------------------- experiment: pre-split operands
-// Times the forward conv GEMM with in-kernel splitting (conv_x3) against the same GEMM fed with
-// pre-split bf16 planes (conv_x3ps), same tile plan, splits forced to 1. Returns
-// {ms_in_kernel_split, ms_presplit, ms_split3_of_x, max_abs_diff}.
-std::vector<double> bench_presplit(const at::Tensor& x_, const at::Tensor& w_, int64_t stride, int64_t pad,
-                                   int64_t iters, bool dgrad) {
-  const at::Tensor x = nhwc(x_), w = nhwc(w_);
-  const int N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
-  const int Co = w.size(0), KH = w.size(2), KW = w.size(3);
-  TORCH_CHECK(C % 32 == 0, "pre-split experiment needs C % 32 == 0");
-  const int P = dgrad ? H : (H + 2 * pad - KH) / stride + 1, Q = dgrad ? W : (W + 2 * pad - KW) / stride + 1;
-  const long long M = (long long)N * P * Q;
-  const int Kdim = KH * KW * C;
-  GemmPlan g = plan_gemm(M, Co, Kdim);
-  ConvGemmParams p{};
-  p.N = N; p.H = H; p.W = W; p.C = C; p.P = P; p.Q = Q;
-  p.KH = KH; p.KW = KW; p.stride = (int)stride; p.pad = (int)pad; p.pad_w = (int)pad;
-  p.Nout = Co; p.M = (int)M; p.Kdim = Kdim; p.ktiles = g.ktiles; p.splits = 1;
-  set_divs(p);
-  auto opts = x.options();
-  at::Tensor y1 = at::empty({M, Co}, opts), y2 = at::empty({M, Co}, opts);
-  at::Tensor xp = at::empty({3 * x.numel()}, opts.dtype(at::kBFloat16));
-  at::Tensor wp = at::empty({3 * w.numel()}, opts.dtype(at::kBFloat16));
-  hipStream_t st = cur_stream();
-  split3_launch(w.data_ptr<float>(), w.numel(), wp.data_ptr(), st);
-  hipEvent_t e0, e1;
-  hipEventCreate(&e0);
-  hipEventCreate(&e1);
-  auto timeit = [&](auto fn) {
-    fn();
-    hipEventRecord(e0, st);
-    for (int i = 0; i < iters; ++i) fn();
-    hipEventRecord(e1, st);
-    hipEventSynchronize(e1);
-    float ms = 0.f;
-    hipEventElapsedTime(&ms, e0, e1);
-    return (double)ms / (double)iters;
-  };
-  const double t_split = timeit([&] { split3_launch(x.data_ptr<float>(), x.numel(), xp.data_ptr(), st); });
-  ConvGemmParams p1 = p;
-  p1.x = x.data_ptr<float>();
-  p1.w = w.data_ptr<float>();
-  p1.y = y1.data_ptr<float>();
-  const double t1 = timeit([&] { conv_x3_launch(p1, g.bm, g.bn, dgrad, false, st); });
-  ConvGemmParams p2 = p;
-  p2.x = reinterpret_cast<const float*>(xp.data_ptr());
-  p2.w = reinterpret_cast<const float*>(wp.data_ptr());
-  p2.y = y2.data_ptr<float>();
-  const double t2 = timeit([&] { conv_x3ps_launch(p2, g.bm, g.bn, dgrad, st); });
-  std::vector<double> abl;
-  if (g.bm == 128 && g.bn == 128 && !dgrad)
-    for (int ps = 0; ps < 2; ++ps)
-      for (int a = 1; a < 4; ++a)
-        abl.push_back(timeit([&] { conv_x3_ablate_launch(ps ? p2 : p1, a, ps == 1, st); }));
-  hipEventDestroy(e0);
-  hipEventDestroy(e1);
-  const double diff = (y1 - y2).abs().max().item<double>();
-  std::vector<double> r{t1, t2, t_split, diff};
-  r.insert(r.end(), abl.begin(), abl.end());
-  return r;
-}
-
 }  // namespace cdp

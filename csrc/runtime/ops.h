@@ -6,8 +6,6 @@
 
 namespace cdp {
 
-std::vector<double> bench_presplit(const at::Tensor& x, const at::Tensor& w, int64_t stride, int64_t pad,
-                                   int64_t iters, bool dgrad);
 void set_conv_gemm(const std::string& mode);
 std::string get_conv_gemm();
 std::vector<at::Tensor> conv2d_fwd(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tensor>& bias,

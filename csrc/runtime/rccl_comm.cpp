@@ -13,6 +13,8 @@
 #include <torch/extension.h>
 
 #include <cstring>
+
+#include "../kernels/kernels.h"
 #include <sstream>
 
 namespace cdp {
@@ -102,7 +104,9 @@ RcclComm::RcclComm(const std::string& uid, int rank, int world, int device, doub
   HIP_CHECK(hipDeviceGetStreamPriorityRange(&lo, &hi));
   HIP_CHECK(hipStreamCreateWithPriority(&stream_, hipStreamNonBlocking, hi));
   HIP_CHECK(hipEventCreateWithFlags(&start_ev_, hipEventDisableTiming));
-  RCCL_CHECK(ncclCommInitRank(&comm_, world, id, rank));
+  ncclComm_t c = nullptr;
+  RCCL_CHECK(ncclCommInitRank(&c, world, id, rank));
+  comm_.store(c);
   wd_thread_ = std::thread([this] { watchdog_loop(); });
 }
 
@@ -116,10 +120,10 @@ void RcclComm::shutdown() {
     std::lock_guard<std::mutex> g(wd_mu_);
     pending_.clear();
   }
-  if (comm_) {
-    if (failed_.load()) ncclCommAbort(comm_);
-    else ncclCommDestroy(comm_);
-    comm_ = nullptr;
+  std::lock_guard<std::mutex> g(mu_);  // no collective is mid-enqueue while the comm is torn down
+  if (ncclComm_t c = comm_.exchange(nullptr)) {
+    if (failed_.load()) ncclCommAbort(c);
+    else ncclCommDestroy(c);
   }
 }
 
@@ -148,7 +152,16 @@ void RcclComm::abort(const std::string& why) {
     std::lock_guard<std::mutex> g(err_mu_);
     if (err_.empty()) err_ = why;
   }
-  if (!failed_.exchange(true) && comm_) ncclCommAbort(comm_), comm_ = nullptr;
+  if (failed_.exchange(true)) return;  // first caller only
+  // From here on every collective fails its check() under mu_ before touching comm_. Wait (bounded)
+  // for a collective that is mid-enqueue to leave RCCL, so the comm is not freed under it. If the
+  // holder stays inside RCCL (blocked on a dead peer, e.g. p2p connection setup), abort anyway:
+  // ncclCommAbort is what unblocks it, and it re-checks failed_ on return.
+  std::unique_lock<std::mutex> g(mu_, std::defer_lock);
+  const auto t0 = std::chrono::steady_clock::now();
+  while (!g.try_lock() && std::chrono::steady_clock::now() - t0 < std::chrono::seconds(2))
+    std::this_thread::sleep_for(std::chrono::milliseconds(1));
+  if (ncclComm_t c = comm_.exchange(nullptr)) ncclCommAbort(c);
 }
 
 hipEvent_t RcclComm::get_event() {
@@ -226,9 +239,10 @@ void RcclComm::watchdog_loop() {
         break;
       }
     }
-    if (comm_ && !failed_.load()) {
+    ncclComm_t c = comm_.load();  // only this thread and shutdown() (which joined it) free the comm
+    if (c && !failed_.load()) {
       ncclResult_t ae = ncclSuccess;
-      if (ncclCommGetAsyncError(comm_, &ae) == ncclSuccess && ae != ncclSuccess && ae != ncclInProgress)
+      if (ncclCommGetAsyncError(c, &ae) == ncclSuccess && ae != ncclSuccess && ae != ncclInProgress)
         timed_out = std::string("asynchronous RCCL error: ") + ncclGetErrorString(ae);
     }
     if (!timed_out.empty()) {
@@ -244,6 +258,10 @@ std::shared_ptr<RcclWork> RcclComm::all_reduce(at::Tensor t, const std::string& 
   std::lock_guard<std::mutex> g(mu_);
   hipStream_t cur = begin();
   RCCL_CHECK(ncclAllReduce(t.data_ptr(), t.data_ptr(), t.numel(), to_nccl(t.scalar_type()), to_op(op), comm_, stream_));
+  if (postop_delay_us_ > 0.0 || postop_scale_ != 1.0) {
+    TORCH_CHECK(t.scalar_type() == at::kFloat, "test post-op needs fp32 tensors");
+    delay_scale_launch(t.data_ptr<float>(), t.numel(), (float)postop_scale_, postop_delay_us_, stream_);
+  }
   return end(cur, async, {t}, "all_reduce");
 }
 
@@ -365,6 +383,16 @@ std::shared_ptr<RcclWork> RcclComm::recv(at::Tensor t, int peer, bool async) {
   hipStream_t cur = begin();
   RCCL_CHECK(ncclRecv(t.data_ptr(), t.numel(), to_nccl(t.scalar_type()), peer, comm_, stream_));
   return end(cur, async, {t}, "recv");
+}
+
+int RcclComm::count() {
+  std::lock_guard<std::mutex> g(mu_);
+  check();
+  ncclComm_t c = comm_.load();
+  TORCH_CHECK(c != nullptr, "RCCL communicator is shut down");
+  int n = 0;
+  RCCL_CHECK(ncclCommCount(c, &n));
+  return n;
 }
 
 void RcclComm::barrier() {

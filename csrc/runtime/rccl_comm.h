@@ -55,6 +55,7 @@ class RcclComm : public std::enable_shared_from_this<RcclComm> {
   int rank() const { return rank_; }
   int size() const { return world_; }
   int device() const { return device_; }
+  int count();  // ranks in the communicator as RCCL sees them (ncclCommCount)
   hipStream_t stream() const { return stream_; }
   bool healthy() const { return !failed_.load(); }
   std::string error() const;
@@ -75,6 +76,14 @@ class RcclComm : public std::enable_shared_from_this<RcclComm> {
   std::shared_ptr<RcclWork> recv(at::Tensor t, int peer, bool async);
   void barrier();
 
+  // Test hook (CDP_REDUCER_TEST_POSTOP): after every all_reduce, enqueue on the communicator
+  // stream a ~delay_us spin followed by x *= scale, *inside* the collective's completion event.
+  // A consumer that is not correctly ordered after the collective then reads unscaled data.
+  void set_test_postop(double delay_us, double scale) {
+    postop_delay_us_ = delay_us;
+    postop_scale_ = scale;
+  }
+
   hipEvent_t get_event();
   void put_event(hipEvent_t e);
   void check() const;
@@ -84,7 +93,11 @@ class RcclComm : public std::enable_shared_from_this<RcclComm> {
   std::shared_ptr<RcclWork> end(hipStream_t cur, bool async, std::vector<at::Tensor> keep, const char* what);
   void watchdog_loop();
 
-  ncclComm_t comm_ = nullptr;
+  // Atomic: the watchdog's abort() and shutdown() hand the comm off with exchange(nullptr), so
+  // exactly one of them frees it, and collectives (which re-check failed_ under mu_) never see
+  // a freed comm.
+  std::atomic<ncclComm_t> comm_{nullptr};
+  double postop_delay_us_ = 0.0, postop_scale_ = 1.0;
   int rank_, world_, device_;
   hipStream_t stream_ = nullptr;
   hipEvent_t start_ev_ = nullptr;

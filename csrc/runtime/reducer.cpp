@@ -23,6 +23,12 @@
 #include <torch/csrc/autograd/functions/accumulate_grad.h>
 #include <torch/csrc/autograd/variable.h>
 
+#include <rocprofiler-sdk-roctx/roctx.h>
+#include <time.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
 #include <unordered_set>
 
 #include "../kernels/kernels.h"
@@ -71,6 +77,8 @@ Reducer::Reducer(std::vector<at::Tensor> params, std::vector<at::Tensor> grad_vi
   }
   for (size_t i = 0; i < params_.size(); ++i) TORCH_CHECK(bucket_of_[i] >= 0, "parameter ", i, " has no bucket");
   world_ = rccl_ ? rccl_->size() : pg_->getSize();
+  const char* rx = std::getenv("CDP_ROCTX");
+  roctx_ = rx && std::strcmp(rx, "1") == 0;
   pending_.assign(nb, 0);
   works_.resize(nb);
   pg_works_.resize(nb);
@@ -85,6 +93,12 @@ Reducer::Reducer(std::vector<at::Tensor> params, std::vector<at::Tensor> grad_vi
 }
 
 Reducer::~Reducer() { remove_hooks(); }
+
+void Reducer::log_event(const char* kind, int64_t idx) {
+  timespec ts;
+  clock_gettime(CLOCK_MONOTONIC, &ts);
+  trace_log_.emplace_back(kind, idx, (int64_t)ts.tv_sec * 1000000000LL + ts.tv_nsec);
+}
 
 void Reducer::remove_hooks() {
   for (size_t i = 0; i < accumulators_.size(); ++i) accumulators_[i]->del_post_hook(hook_keys_[i]);
@@ -154,6 +168,7 @@ void Reducer::mark_ready_locked(size_t i, bool from_hook) {
       gref = view;
     }
     if (record_order_) order_.push_back((int64_t)i);
+    if (trace_) log_event("h", (int64_t)i);
     if (!callback_queued_) {
       callback_queued_ = true;
       torch::autograd::Engine::get_default_engine().queue_callback([this] { this->finalize(); });
@@ -173,18 +188,26 @@ void Reducer::mark_ready_locked(size_t i, bool from_hook) {
 
 void Reducer::launch(int b) {
   at::Tensor& v = bucket_views_[b];
+  if (trace_) log_event("l", (int64_t)b);
+  if (roctx_) {
+    char name[48];
+    std::snprintf(name, sizeof(name), "cdp.bucket_allreduce[%d]", b);
+    roctxRangePushA(name);
+  }
   if (rccl_) {
     works_[b] = rccl_->all_reduce(v, average_ ? "avg" : "sum", /*async=*/true);
   } else {
     std::vector<at::Tensor> ts{v};
     pg_works_[b] = pg_->allreduce(ts);
   }
+  if (roctx_) roctxRangePop();
   ++launched_total_;
 }
 
 void Reducer::finalize() {
   std::lock_guard<std::mutex> g(mu_);
   if (!armed_) return;
+  if (trace_) log_event("f", -1);
   if (next_launch_ < (int)pending_.size()) {
     if (find_unused_) {
       for (size_t i = 0; i < params_.size(); ++i) mark_ready_locked(i, false);

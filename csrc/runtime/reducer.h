@@ -5,6 +5,9 @@
 
 #include <memory>
 #include <mutex>
+#include <string>
+#include <tuple>
+#include <utility>
 #include <vector>
 
 #include "rccl_comm.h"
@@ -29,6 +32,18 @@ class Reducer {
   int64_t iterations() const { return iterations_; }
   int64_t launched_total() const { return launched_total_; }
   int num_buckets() const { return (int)bucket_views_.size(); }
+  // Event log for overlap tests/tracing: ('h', param index) when a gradient-ready hook fires,
+  // ('l', bucket) when a bucket collective is launched, ('f', -1) at the end-of-backward callback;
+  // each with its host CLOCK_MONOTONIC time in ns (same clock as Python's time.monotonic_ns()).
+  void set_trace(bool on) {
+    std::lock_guard<std::mutex> g(mu_);
+    trace_ = on;
+    trace_log_.clear();
+  }
+  std::vector<std::tuple<std::string, int64_t, int64_t>> trace_log() const {
+    std::lock_guard<std::mutex> g(mu_);
+    return trace_log_;
+  }
   void disarm() {
     std::lock_guard<std::mutex> g(mu_);
     armed_ = false;
@@ -56,6 +71,10 @@ class Reducer {
   int next_launch_ = 0;
   bool armed_ = false, callback_queued_ = false, record_order_ = true, have_order_ = false;
   int64_t iterations_ = 0, launched_total_ = 0;
+  bool trace_ = false;
+  bool roctx_ = false;  // CDP_ROCTX=1: roctx range per bucket launch (rocprofv3 --marker-trace)
+  std::vector<std::tuple<std::string, int64_t, int64_t>> trace_log_;  // (kind, index, CLOCK_MONOTONIC ns)
+  void log_event(const char* kind, int64_t idx);
 };
 
 }  // namespace cdp

@@ -87,3 +87,107 @@ def test_rccl_single_rank_ddp_and_graph():
     env["PYTHONPATH"] = repo + os.pathsep + env.get("PYTHONPATH", "")
     r = subprocess.run([sys.executable, "-c", SCRIPT], env=env, capture_output=True, text=True, timeout=300)
     assert "COMM_OK" in r.stdout, r.stdout[-3000:] + r.stderr[-5000:]
+
+
+ORDER_SCRIPT = textwrap.dedent(
+    r"""
+    import os, torch
+    # every all_reduce on the native communicator is followed, on the comm stream and inside its
+    # completion event, by a ~3 ms idle wait and then grad *= 2 (RcclComm::set_test_postop)
+    os.environ["CDP_REDUCER_TEST_POSTOP"] = "3000:2"
+    import cs744_distributed_data_parallel_amd as cdp
+    from cs744_distributed_data_parallel_amd import distributed as dist
+    dist.init_process_group("rccl", rank=0, world_size=1)
+    assert dist.native_communicator() is not None
+    crit = cdp.CrossEntropyLoss()
+    x = torch.randn(64, 3, 32, 32, device="cuda"); y = torch.randint(0, 10, (64,), device="cuda")
+
+    def fresh():
+        torch.manual_seed(0)
+        return cdp.VGG11().cuda()
+
+    m0 = fresh()
+    crit(m0(x), y).backward()
+    ref = [p.grad.detach().clone() for p in m0.parameters()]
+    snap = [p.detach().clone() for p in m0.parameters()]
+    torch.cuda.synchronize()
+
+    # tensors whose gradient is numerically zero (conv biases ahead of BatchNorm: analytically 0,
+    # rounding noise in practice) carry no ordering signal and are skipped
+    rms = [float(v.pow(2).mean().sqrt()) for v in ref]
+    keep = [r > 1e-3 * max(rms) for r in rms]
+
+    def ratios(a, b):
+        return [float((u * v).sum() / (v * v).sum()) for u, v, k in zip(a, b, keep) if k]
+
+    for kind in ("ddp", "bucketed_overlap"):
+        for graph in (False, True):
+            base = fresh()
+            model, sync = base, None
+            if kind == "ddp":
+                model = cdp.DistributedDataParallel(base, bucket_cap_mb=2.0)
+            else:
+                sync = cdp.parallel.BucketedOverlap(base, bucket_cap_mb=2.0)
+            opt = cdp.SGD(base.parameters(), lr=1.0, momentum=0.0, weight_decay=0.0)
+
+            def body():
+                opt.zero_grad()
+                out = model(x)
+                if sync is not None:
+                    sync.prepare(out)
+                crit(out, y).backward()
+                opt.step()
+
+            for _ in range(3):  # includes the bucket rebuild in ready order
+                body()
+            g = None
+            if graph:
+                s = torch.cuda.Stream(); s.wait_stream(torch.cuda.current_stream())
+                with torch.cuda.stream(s):
+                    body()
+                torch.cuda.current_stream().wait_stream(s)
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g):
+                    body()
+            torch.cuda.synchronize()
+            with torch.no_grad():
+                for p, v in zip(base.parameters(), snap):
+                    p.copy_(v)
+            if g is not None:
+                g.replay()
+            else:
+                body()
+            # read the update on the compute stream right away: SGD (p -= 1.0 * grad) must have run
+            # after the delayed post-op, i.e. consumed exactly 2x the gradient
+            delta = [v - p.detach() for p, v in zip(base.parameters(), snap)]
+            torch.cuda.synchronize()
+            final = [p.grad.detach() for p in base.parameters()]
+            r_step = ratios(delta, final)  # 1.0: SGD consumed the post-op'd gradient
+            r_grad = ratios(final, ref)    # 2.0: the post-op ran on every bucket
+            assert all(abs(r - 1.0) < 2e-3 for r in r_step), (kind, graph, "SGD saw", r_step)
+            assert all(abs(r - 2.0) < 2e-3 for r in r_grad), (kind, graph, r_grad)
+            print("ORDER_OK", kind, "graph" if graph else "eager", len(r_step), flush=True)
+            if g is not None:
+                g.reset()
+            if kind == "ddp":
+                model.reducer.remove()
+            else:
+                sync.remove()
+    dist.destroy_process_group()
+    print("ORDER_ALL_OK")
+    """
+)
+
+
+def test_reducer_comm_to_compute_ordering_with_delayed_postop():
+    """Proves the comm->compute event edge on ONE GPU: each bucket's collective is followed on the
+    communicator stream by a delay and a scale-by-2; SGD must see exactly 2x the gradient, eager and
+    under hipGraph capture, for DDP and BucketedOverlap (csrc/runtime/reducer.cpp finalize ->
+    RcclWork::wait)."""
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()), RANK="0", WORLD_SIZE="1",
+               LOCAL_RANK="0")
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env["PYTHONPATH"] = repo + os.pathsep + env.get("PYTHONPATH", "")
+    r = subprocess.run([sys.executable, "-c", ORDER_SCRIPT], env=env, capture_output=True, text=True, timeout=300)
+    assert "ORDER_ALL_OK" in r.stdout, r.stdout[-3000:] + r.stderr[-5000:]
+    assert r.stdout.count("ORDER_OK") == 4

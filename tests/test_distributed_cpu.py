@@ -260,3 +260,52 @@ def test_dead_peer_is_detected_by_timeout():
     status, dt = res[0]
     assert status == "raised", res
     assert dt < 6.0, res
+
+
+# ----------------------------------------------------------------------------- overlap
+def _overlap_trace(rank, world, strategy):
+    import cs744_distributed_data_parallel_amd as cdp
+    from cs744_distributed_data_parallel_amd.parallel import BucketedOverlap, DistributedDataParallel
+
+    cdp.utils.seed_everything(0)
+    model = cdp.VGG11(channels_last=False)
+    sync = None
+    if strategy == "ddp":
+        model = DistributedDataParallel(model, bucket_cap_mb=2.0)
+        reducer = model.reducer
+    else:
+        sync = BucketedOverlap(model, bucket_cap_mb=2.0)
+        reducer = sync.reducer
+    crit = cdp.CrossEntropyLoss()
+    logs = []
+    for step in range(3):  # step 0 records the ready order, step 1 runs on the rebuilt buckets
+        reducer.set_trace(True)
+        x, y = _make_batch(rank, step, B=4)
+        out = model(x)
+        if sync is not None:
+            sync.prepare(out)
+        crit(out, y).backward()
+        logs.append(reducer.trace_log())
+    return logs, reducer.num_buckets
+
+
+@pytest.mark.parametrize("strategy", ["ddp", "bucketed_overlap"])
+def test_bucket_allreduce_overlaps_backward(strategy):
+    """Part 2b/3 semantics: bucket all-reduces are launched from the autograd hooks WHILE backward
+    is still producing gradients -- not after it. Bucket 0 launches before the last gradient-ready
+    hook, more than one bucket is in flight before backward ends, launches are in bucket order, and
+    the end-of-backward callback comes last."""
+    res = run_ranks(_overlap_trace, 2, (strategy,))
+    for logs, nb in res:
+        assert nb >= 4
+        for log in logs[1:]:
+            kinds = [k for k, _, _ in log]
+            launches = [i for k, i, _ in log if k == "l"]
+            assert launches == list(range(nb)), launches
+            first_launch = kinds.index("l")
+            last_hook = len(kinds) - 1 - kinds[::-1].index("h")
+            assert first_launch < last_hook, kinds
+            assert sum(1 for k in kinds[:last_hook] if k == "l") >= 2, kinds
+            assert kinds[-1] == "f"
+            ts = [t for _, _, t in log]
+            assert ts == sorted(ts)

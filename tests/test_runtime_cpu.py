@@ -207,7 +207,7 @@ def test_phase_timer_and_trace(tmp_path):
         pass
     p = tr.dump(str(tmp_path / "t.json"))
     ev = json.load(open(p))["traceEvents"]
-    assert ev[0]["name"] == "fwd"
+    assert [e["name"] for e in ev if e["ph"] == "X"] == ["fwd"]
 
 
 # ----------------------------------------------------------------------------- CLI
@@ -220,13 +220,47 @@ def test_train_cli_single_process_log_format():
                     "--device", "cpu"])
     out = buf.getvalue()
     assert "Size of training set is 50" in out
-    assert re.search(r"Training loss after 20 iterations is \d", out)
+    # Part 1 prints "epochs" here (src/Part 1/main.py:49); only Part 3 (ddp) says "iterations"
+    assert re.search(r"Training loss after 20 epochs is \d", out)
     assert re.search(r"Forward Pass time in iter 40 is ", out)
     assert re.search(r"Backward Pass time in iter 40 is ", out)
     assert re.search(r"Average Pass time in iter 40 is ", out)
     assert "Forward Pass time in iter 20" not in out  # first window discarded like the reference
     assert re.search(r"Training time after 1 epoch is ", out)
     assert re.search(r"Test set: Average loss: \d+\.\d{4}, Accuracy: \d+/400 \(\d+%\)", out)
+
+
+def test_train_cli_ddp_log_format_and_trace(tmp_path):
+    """Part 3 log string ("iterations") and --trace: phases plus the reducer's hook / bucket-launch
+    events, with bucket launches interleaved with gradient-ready hooks (overlap)."""
+    import os
+    import subprocess
+    import sys
+
+    from _dist_util import free_port
+
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(free_port()), RANK="0", WORLD_SIZE="1",
+               PYTHONPATH=repo, OMP_NUM_THREADS="2")
+    tr = str(tmp_path / "trace.json")
+    r = subprocess.run([sys.executable, "-m", "cs744_distributed_data_parallel_amd.train", "--strategy", "ddp",
+                        "--backend", "gloo", "--device", "cpu", "--iters", "20", "--batch-size", "4",
+                        "--synthetic-size", "80", "--bucket-cap-mb", "2", "--trace", tr],
+                       env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert re.search(r"Training loss after 20 iterations is \d", r.stdout), r.stdout
+    ev = json.load(open(tr))["traceEvents"]
+    phases = {e["name"] for e in ev if e["ph"] == "X"}
+    assert {"forward", "backward", "step"} <= phases
+    host = [e["name"] for e in ev if e["ph"] == "i"]
+    assert sum(n.startswith("bucket_allreduce_launch") for n in host) >= 20 * 3
+    assert host.count("backward_done") == 20
+    # within the last iteration the first bucket launches before the last gradient is ready
+    done = [i for i, n in enumerate(host) if n == "backward_done"]
+    last = host[done[-2] + 1:done[-1]]
+    first_launch = next(i for i, n in enumerate(last) if n.startswith("bucket_allreduce_launch"))
+    last_hook = max(i for i, n in enumerate(last) if n.startswith("grad_ready"))
+    assert first_launch < last_hook, last
 
 
 # ----------------------------------------------------------------------------- native surface
@@ -250,3 +284,40 @@ def test_gpu_tensor_without_extension_raises(monkeypatch):
     monkeypatch.setattr(_native, "_err", RuntimeError("missing"))
     with pytest.raises(RuntimeError, match="native runtime"):
         _native.require(Fake())
+
+
+# ----------------------------------------------------------------------------- bench.py contract
+def _bench(args, env_extra=None, timeout=600):
+    import os
+    import subprocess
+    import sys
+
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, PYTHONPATH=repo, OMP_NUM_THREADS="1")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT"):
+        env.pop(k, None)
+    env.update(env_extra or {})
+    return subprocess.run([sys.executable, os.path.join(repo, "bench.py")] + args, env=env, capture_output=True,
+                          text=True, timeout=timeout, cwd=repo)
+
+
+def test_bench_self_launches_ranks_cpu():
+    """`bench.py --gpus 2` without WORLD_SIZE starts both ranks itself; rank 0 prints one JSON line
+    with n_gpus == ranks_seen == 2, the strong-scaling point and the exposed-comm estimate."""
+    r = _bench(["--gpus", "2", "--device", "cpu", "--steps", "2", "--warmup", "1", "--local-batch", "4",
+                "--dataset-size", "64"])
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    rec = json.loads(lines[0])
+    assert rec["n_gpus"] == 2 and rec["ranks_seen"] == 2
+    assert rec["config"]["parallelism"] == "dp2" and rec["config"]["global_batch"] == 8
+    assert rec["strong"]["global_batch"] == 256 and rec["strong"]["local_batch"] == 128
+    assert rec["exposed_comm_ms"] >= 0 and rec["value"] > 0
+
+
+def test_bench_failing_rank_fails_the_launcher():
+    r = _bench(["--gpus", "2", "--device", "cpu", "--steps", "1", "--warmup", "1", "--local-batch", "2",
+                "--dataset-size", "16", "--no-extra"], env_extra={"CDP_BENCH_FAIL_RANK": "1"})
+    assert r.returncode != 0
+    assert not [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
