@@ -220,6 +220,20 @@ class _Run:
             print(f"[bench] hipGraph capture failed ({e!r}); timing eager steps", file=sys.stderr)
             self.graph = None
             torch.cuda.synchronize()
+        if self.world > 1:
+            # all ranks replay graphs or all run eager (a capture records collectives without running
+            # them, so dropping every rank's graph after one rank's failure keeps the order matched)
+            import torch.distributed as tdist
+
+            store = tdist.distributed_c10d._get_default_store()
+            _Run._gen = getattr(_Run, "_gen", 0) + 1
+            keys = [f"cdp_bench_graph/{_Run._gen}/{r}" for r in range(self.world)]
+            store.set(keys[tdist.get_rank()], "1" if self.graph is not None else "0")
+            store.wait(keys)
+            if any(store.get(k) != b"1" for k in keys) and self.graph is not None:
+                print("[bench] another rank could not capture; all ranks time eager steps", file=sys.stderr)
+                self.graph.reset()
+                self.graph = None
 
     def time(self, steps, dist):
         torch = self.torch
@@ -332,6 +346,24 @@ def rank_main(args) -> int:
             extra[key] = {"value": round(other_lb * world / ms_o * 1e3, 1), "ms_per_step": round(ms_o, 4),
                           "global_batch": other_lb * world, "local_batch": other_lb}
 
+    engine = "reference" if cpu else _conv_gemm_engine(args.backend)
+    if (world == 1 and not args.no_extra and not cpu and args.backend == "native" and args.precision == "fp32"
+            and engine == "f16x2"):
+        # the same step on the strict engine (3-term bf16 split: every conv GEMM output within the
+        # fp32 per-element error bound, tests/test_accuracy_gpu.py), so both numbers are measured here
+        C = cdp._native.lib()
+        C.set_conv_gemm("x3")
+        try:
+            sx = _Run(args, world, rank, dev, main_lb, sync_grads=True)
+            sx.prepare(args.warmup, dbg)
+            ms_x3 = sx.time(args.steps, dist)
+            sx.release()
+            del sx
+        finally:
+            C.set_conv_gemm(engine)
+        extra["strict_fp32"] = {"conv_gemm": "x3", "value": round(main_lb * world / ms_x3 * 1e3, 1),
+                                "ms_per_step": round(ms_x3, 4)}
+
     global_batch = main_lb * world
     img_s = global_batch / ms * 1e3
     imagenet = args.model.startswith("resnet")
@@ -371,7 +403,7 @@ def rank_main(args) -> int:
                 # power-of-two-scaled operands split into two fp16 terms, three products on the
                 # fp16 MFMA; "x3" = 3-term bf16 split, six products on the bf16 MFMA; "f32" =
                 # exact fp32-input MFMA (docs/PERF.md, tests/test_kernels_gpu.py)
-                "conv_gemm": "reference" if cpu else _conv_gemm_engine(args.backend),
+                "conv_gemm": engine,
             },
         }
         rec.update(extra)
