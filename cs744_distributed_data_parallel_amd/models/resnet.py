@@ -121,21 +121,24 @@ class ResNet(nn.Module):
     def forward(self, x):
         if CF.use_native(x):
             x = x.contiguous(memory_format=torch.channels_last)
-            # f16x2 engine: every conv weight's operand scale in one launch; each conv module holds
-            # its entry for the duration of this forward (conv_bn_act reads it)
+            # one launch: every conv weight's f16x2 operand scale and its W^T for the data gradient
+            # (stride-1 convs; the stem's input needs no gradient, stride-2 convs use sub-filters);
+            # each conv module holds its entries for the duration of this forward (conv_bn_act
+            # reads them)
             convs = [m for m in self.modules() if isinstance(m, nn.Conv2d)]
-            wam = CF.weight_amax([m.weight for m in convs])
-            if wam is not None:
-                for m, a in zip(convs, wam):
-                    m._cdp_wamax = a
+            need = [m.stride[0] == 1 and (m is not self.conv1 or x.requires_grad) for m in convs]
+            wam, wts = CF.weight_prep([m.weight for m in convs], need)
+            for i, m in enumerate(convs):
+                m._cdp_wamax = wam[i] if wam is not None else None
+                m._cdp_wt = wts[i] if wts is not None else None
             try:
                 x = CF.conv_bn_act(x, self.conv1, self.bn1, relu=True)
                 x = CF.max_pool2d(x, 3, 2, 1)
                 x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
             finally:
-                if wam is not None:
-                    for m in convs:
-                        m._cdp_wamax = None
+                for m in convs:
+                    m._cdp_wamax = None
+                    m._cdp_wt = None
             x = CF.global_avg_pool(x)
             return CF.linear(x, self.fc.weight, self.fc.bias)
         x = self.maxpool(self.relu(self.bn1(self.conv1(x))))

@@ -76,10 +76,13 @@ class VGG(nn.Module):
         if CF.use_native(x):
             x = x.contiguous(memory_format=torch.channels_last)
             layers = self.layers
-            wam = CF.weight_amax([layers[ci].weight for ci, _, _ in self._plan])  # f16x2 operand scales
+            # one launch: f16x2 operand scales of every conv weight + W^T for the data gradients
+            # (the first conv's input needs no gradient: no transpose)
+            need = [k > 0 or x.requires_grad for k in range(len(self._plan))]
+            wam, wts = CF.weight_prep([layers[ci].weight for ci, _, _ in self._plan], need)
             for k, (ci, bi, pool) in enumerate(self._plan):
                 x = CF.conv_bn_act(x, layers[ci], layers[bi], relu=True, pool=pool,
-                                   w_amax=wam[k] if wam is not None else None)
+                                   w_amax=wam[k] if wam is not None else None, w_t=wts[k])
             y = x.reshape(x.size(0), -1)
             return CF.linear(y, self.fc1.weight, self.fc1.bias)
         y = self.layers(x)

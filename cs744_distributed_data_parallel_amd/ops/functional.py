@@ -70,6 +70,19 @@ def weight_amax(weights):
     return parts if parts else None
 
 
+def weight_prep(weights, need_dgrad=None):
+    """Per-step preparation of a model's conv weights in ONE launch (csrc weight_prep_kernel):
+    ``(amax, wts)`` -- the f16x2 |max| partials per weight (None for the other engines) and the
+    transposed data-gradient operand W^T per weight (None where ``need_dgrad[i]`` is False, e.g.
+    the first conv, whose input needs no gradient). Both are computed from the current weights at
+    every forward, so they are valid whatever changed the weights."""
+    if not weights or not use_native(weights[0]):
+        return None, None
+    want = [True] * len(weights) if need_dgrad is None else [bool(f) for f in need_dgrad]
+    amax, wts = _native.lib().weight_prep(list(weights), want)
+    return (amax if amax else None), [t if f else None for t, f in zip(wts, want)]
+
+
 # --------------------------------------------------------------------------- conv + BN + act
 class GradSink:
     """Sums the two gradients of a tensor consumed by two fused ops without an autograd add.
@@ -100,7 +113,7 @@ class GradSink:
 class _ConvBNAct(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, b, gamma, beta, rm, rv, nbt, momentum, eps, training, stride, pad, pool, relu, residual,
-                res_sink=None, dx_sink=None, w_amax=None):
+                res_sink=None, dx_sink=None, w_amax=None, w_t=None):
         C = _native.lib()
         out, y, stats, xsave, out_amax, x_amax, w_amax = C.conv_bn_act_fwd(
             x, w, b, gamma, beta, rm, rv, nbt, momentum, eps, training, stride, pad, pool, relu, residual, _get_amax(x),
@@ -110,6 +123,7 @@ class _ConvBNAct(torch.autograd.Function):
         ctx.params = (w, b, gamma, beta)
         ctx.sinks = (res_sink, dx_sink)
         ctx.amax = (x_amax, w_amax)  # f16x2 engine only (else None): W and x are unchanged by backward
+        ctx.w_t = w_t  # W^T from weight_prep (this step's weights), or None: dgrad transposes itself
         zout = out if residual is not None else None
         ctx.save_for_backward(xsave, w, y, stats, zout)  # xsave: x, or x zero-padded to 4k channels
         _set_amax(out, out_amax)
@@ -132,8 +146,9 @@ class _ConvBNAct(torch.autograd.Function):
         dx, dw, db, dgamma, dbeta, dres = C.conv_bn_act_bwd(
             gout, x, w, y, stats, stride, pad, pool, relu, nig[0], has_bias, zout, training,
             _slot(wp, nig[1]), _slot(bp, nig[2] and has_bias), _slot(gp, nig[3]), _slot(betap, nig[4]), addend,
-            *ctx.amax,
+            *ctx.amax, ctx.w_t,
         )
+        ctx.w_t = None
         if park_dx:
             dx_sink.grad, dx = dx, None
         if has_res and res_sink is not None and nig[15]:
@@ -150,12 +165,12 @@ class _ConvBNAct(torch.autograd.Function):
             dbeta if ctx.needs_input_grad[4] else None,
             None, None, None, None, None, None, None, None, None, None,
             dres if has_res else None,
-            None, None, None,
+            None, None, None, None,
         )
 
 
 def conv_bn_act(x, conv, bn, relu: bool = True, pool: bool = False, residual=None, res_sink=None, dx_sink=None,
-                w_amax=None):
+                w_amax=None, w_t=None):
     """``[maxpool2x2](act(bn(conv(x)) [+ residual]))`` for an ``nn.Conv2d`` / ``nn.BatchNorm2d`` pair.
 
     ``pool`` is the reference's ``MaxPool2d(kernel_size=2, stride=2)``; ``relu`` its
@@ -163,6 +178,7 @@ def conv_bn_act(x, conv, bn, relu: bool = True, pool: bool = False, residual=Non
     ``res_sink`` / ``dx_sink`` (:class:`GradSink`, GPU path only) route the residual gradient of an
     identity block into the data-gradient GEMM of the block's first conv instead of an autograd add.
     ``w_amax`` (f16x2 engine): ``conv.weight``'s entry of :func:`weight_amax`, else measured here.
+    ``w_t``: ``conv.weight``'s W^T from :func:`weight_prep` (else backward transposes it).
     """
     stride = conv.stride[0]
     pad = conv.padding[0]
@@ -189,6 +205,7 @@ def conv_bn_act(x, conv, bn, relu: bool = True, pool: bool = False, residual=Non
             res_sink,
             dx_sink,
             w_amax if w_amax is not None else getattr(conv, "_cdp_wamax", None),
+            w_t if w_t is not None else getattr(conv, "_cdp_wt", None),
         )
     y = F.conv2d(x, conv.weight, conv.bias, conv.stride, conv.padding)
     y = bn(y)

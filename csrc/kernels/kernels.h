@@ -111,6 +111,17 @@ struct MultiAmaxArgs {
   int nseg;
 };
 void multi_amax_launch(const MultiAmaxArgs& a, float* part, hipStream_t st);
+// Per-step weight preparation of a model's conv weights in one launch: for every segment (a
+// channels_last weight [Co][T][Ci]) the |max| partials (one per 32x32 (co, ci) block, f16x2
+// operand scale) and, when wt[s] != nullptr, the data-gradient operand W^T [Ci][T][Co].
+struct WeightPrepArgs {
+  const float* w[kMaxAmaxSegs];
+  float* wt[kMaxAmaxSegs];
+  int co[kMaxAmaxSegs], t[kMaxAmaxSegs], ci[kMaxAmaxSegs];
+  int blk0[kMaxAmaxSegs + 1];
+  int nseg;
+};
+void weight_prep_launch(const WeightPrepArgs& a, float* part, hipStream_t st);
 void slab_sum_launch(const float* slab, int S, long long n, float* dst, bool accumulate, hipStream_t st);
 void slab_sum_strided_launch(const float* slab, int S, long long n_src, int src_cols, int dst_cols, float* dst,
                              bool accumulate, hipStream_t st);

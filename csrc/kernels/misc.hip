@@ -226,6 +226,48 @@ __global__ __launch_bounds__(256) void wtrans_kernel(const float* __restrict__ w
   }
 }
 
+// ------------------------------------------------------------------ weight preparation
+// One launch for all conv weights of a step (replaces a transpose launch per layer plus the
+// |max| pass): block (segment, co32, ci32) walks the T taps of its 32x32 (co, ci) block, keeps the
+// block's |max| (one partial per block) and, when asked, writes the tile transposed through LDS.
+__global__ __launch_bounds__(256) void weight_prep_kernel(WeightPrepArgs a, float* __restrict__ part) {
+  __shared__ float tile[32][33];
+  __shared__ float red[4];
+  const int b = blockIdx.x;
+  int seg = 0;
+  while (seg + 1 < a.nseg && a.blk0[seg + 1] <= b) ++seg;
+  const int Co = a.co[seg], T = a.t[seg], Ci = a.ci[seg];
+  const float* __restrict__ w = a.w[seg];
+  float* __restrict__ wt = a.wt[seg];
+  const int local = b - a.blk0[seg];
+  const int nci = (Ci + 31) / 32;
+  const int co0 = (local / nci) * 32, ci0 = (local % nci) * 32;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 32 x 8
+  float m = 0.f;
+  for (int tap = 0; tap < T; ++tap) {
+#pragma unroll
+    for (int j = ty; j < 32; j += 8) {
+      const int co = co0 + j, ci = ci0 + tx;
+      const float v = (co < Co && ci < Ci) ? w[((long long)co * T + tap) * Ci + ci] : 0.f;
+      m = fmaxf(m, fabsf(v));
+      tile[j][tx] = v;
+    }
+    if (wt) {
+      __syncthreads();
+#pragma unroll
+      for (int j = ty; j < 32; j += 8) {
+        const int ci = ci0 + j, co = co0 + tx;
+        if (ci < Ci && co < Co) wt[((long long)ci * T + tap) * Co + co] = tile[tx][j];
+      }
+      __syncthreads();
+    }
+  }
+  m = wave_max(m);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) part[b] = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+}
+
 // ------------------------------------------------------------------ channel padding
 // out[p][0..C4) = (x[p][0..C), 0...) for NHWC pixels p: the RGB stem's 3 -> 4 channel padding in
 // one pass (one float4 store per pixel), plus the per-block |max| the f16x2 GEMM scales need.
@@ -527,6 +569,9 @@ void augment_launch(const unsigned char* imgs, const long long* idx, long long i
 }
 void counter_inc_launch(long long* c, hipStream_t st) {
   hipLaunchKernelGGL(counter_inc_kernel, dim3(1), dim3(1), 0, st, c);
+}
+void weight_prep_launch(const WeightPrepArgs& a, float* part, hipStream_t st) {
+  hipLaunchKernelGGL(weight_prep_kernel, dim3(a.blk0[a.nseg]), dim3(256), 0, st, a, part);
 }
 void wtrans_launch(const float* w, float* wt, int Co, int T, int Ci, hipStream_t st) {
   dim3 grid((Ci + 31) / 32, (Co + 31) / 32, T);

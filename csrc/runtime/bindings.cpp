@@ -21,7 +21,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("conv2d_fwd", &conv2d_fwd, py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("stride"), py::arg("pad"),
         py::arg("want_stats") = false, py::arg("x_amax") = py::none(), py::arg("w_amax") = py::none());
   m.def("conv2d_dgrad", &conv2d_dgrad, py::arg("dy"), py::arg("w"), py::arg("in_shape"), py::arg("stride"),
-        py::arg("pad"), py::arg("addend") = py::none(), py::arg("dy_amax") = py::none(), py::arg("w_amax") = py::none());
+        py::arg("pad"), py::arg("addend") = py::none(), py::arg("dy_amax") = py::none(), py::arg("w_amax") = py::none(),
+        py::arg("w_t") = py::none());
   m.def("conv2d_wgrad", &conv2d_wgrad, py::arg("dy"), py::arg("x"), py::arg("w_shape"), py::arg("stride"),
         py::arg("pad"), py::arg("out") = py::none(), py::arg("accumulate") = false, py::arg("dy_amax") = py::none(),
         py::arg("x_amax") = py::none());
@@ -35,7 +36,11 @@ PYBIND11_MODULE(_C, m) {
         py::arg("stats"), py::arg("stride"), py::arg("pad"), py::arg("pool"), py::arg("relu"), py::arg("need_dx"),
         py::arg("has_bias"), py::arg("zout") = py::none(), py::arg("training") = true, py::arg("dw_out") = py::none(),
         py::arg("db_out") = py::none(), py::arg("dgamma_out") = py::none(), py::arg("dbeta_out") = py::none(),
-        py::arg("dx_addend") = py::none(), py::arg("x_amax") = py::none(), py::arg("w_amax") = py::none());
+        py::arg("dx_addend") = py::none(), py::arg("x_amax") = py::none(), py::arg("w_amax") = py::none(),
+        py::arg("w_t") = py::none());
+  m.def("weight_prep", &weight_prep, py::arg("weights"), py::arg("want_t"),
+        "one launch per step: conv weights' |max| partials (f16x2; else empty) and W^T [Ci, KH*KW*Co] per weight "
+        "with want_t (the data-gradient operand)");
   m.def("linear_fwd", &linear_fwd);
   m.def("linear_bwd", &linear_bwd, py::arg("gy"), py::arg("x"), py::arg("w"), py::arg("need_dx"),
         py::arg("has_bias"), py::arg("dw_out") = py::none(), py::arg("db_out") = py::none());

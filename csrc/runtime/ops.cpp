@@ -17,6 +17,7 @@
 
 #include <algorithm>
 #include <cstdlib>
+#include <functional>
 #include <string>
 
 #include "../kernels/kernels.h"
@@ -125,6 +126,47 @@ std::vector<at::Tensor> multi_amax(const std::vector<at::Tensor>& ts) {
   return out;
 }
 
+// Per-step preparation of a model's conv weights in one launch per 64 weights: {amax partials per
+// weight (f16x2 engine; empty list otherwise), W^T [Ci][KH*KW*Co] per weight with want_t[i]
+// (undefined tensor otherwise)}. The transposes are the data-gradient B operand, so backward no
+// longer transposes every weight in its own launch.
+std::vector<std::vector<at::Tensor>> weight_prep(const std::vector<at::Tensor>& ts, const std::vector<bool>& want_t) {
+  TORCH_CHECK(ts.size() == want_t.size(), "weight_prep: one want_t flag per weight");
+  std::vector<at::Tensor> amax, wts;
+  hipStream_t st = cur_stream();
+  for (size_t s0 = 0; s0 < ts.size(); s0 += kMaxAmaxSegs) {
+    const size_t ns = std::min<size_t>(kMaxAmaxSegs, ts.size() - s0);
+    WeightPrepArgs a{};
+    a.nseg = (int)ns;
+    std::vector<at::Tensor> keep;
+    int tot = 0;
+    for (size_t i = 0; i < ns; ++i) {
+      const at::Tensor& t0 = ts[s0 + i];
+      check_f32_cuda(t0, "weight_prep input");
+      TORCH_CHECK(t0.dim() == 4, "weight_prep expects conv weights [Co, Ci, KH, KW]");
+      const at::Tensor t = nhwc(t0);
+      keep.push_back(t);
+      const int Co = t.size(0), Ci = t.size(1), T = t.size(2) * t.size(3);
+      a.w[i] = t.data_ptr<float>();
+      a.co[i] = Co;
+      a.t[i] = T;
+      a.ci[i] = Ci;
+      at::Tensor wt;
+      if (want_t[s0 + i]) wt = at::empty({Ci, (long long)T * Co}, t.options());
+      a.wt[i] = wt.defined() ? wt.data_ptr<float>() : nullptr;
+      wts.push_back(wt);
+      a.blk0[i] = tot;
+      tot += ((Co + 31) / 32) * ((Ci + 31) / 32);
+    }
+    a.blk0[ns] = tot;
+    at::Tensor part = at::empty({tot}, ts[s0].options());
+    weight_prep_launch(a, part.data_ptr<float>(), st);
+    if (f16x2_mode())
+      for (size_t i = 0; i < ns; ++i) amax.push_back(part.narrow(0, a.blk0[i], a.blk0[i + 1] - a.blk0[i]));
+  }
+  return {amax, wts};
+}
+
 namespace {
 
 void set_amax(ConvGemmParams& p, const at::Tensor& a, const at::Tensor& b) {
@@ -157,16 +199,56 @@ bool x3_ok(const WgradParams& p) {
          (long long)p.P * p.Q < kIdx;
 }
 
-void conv_launch(const ConvGemmParams& p, int bm, int bn, bool dgrad, hipStream_t st) {
+bool m16_on() {
   static const bool m16 = [] {
     const char* e = std::getenv("CDP_MFMA16");
     return e && e[0] == '1';  // measured: 16x16x32 tiles ran ~2% slower on VGG-11
   }();
+  return m16 && !f16x2_mode();
+}
+
+void conv_launch(const ConvGemmParams& p, int bm, int bn, bool dgrad, hipStream_t st) {
   if (x3_family() && x3_ok(p, dgrad)) {
     TORCH_CHECK(!f16x2_mode() || (p.amax_a && p.amax_b), "f16x2 conv GEMM launched without operand maxima");
-    conv_x3_launch(p, bm, bn, dgrad, m16 && !f16x2_mode(), st, split_planes());
+    conv_x3_launch(p, bm, bn, dgrad, m16_on(), st, split_planes());
   }
   else conv_igemm_launch(p, bm, bn, dgrad, st);
+}
+
+// Launch a conv GEMM with g.splits split-K slices. p.y / p.bias / p.addend / p.part / p.rr describe
+// the final output; split slices meet through an fp32 slab and the reduction kernel, which also
+// applies bias / addend / the sub-pixel row scatter and emits the BN partials (then per
+// splitk_rows_per_part() rows). Returns the rows per BN partial.
+//
+// Measured and rejected (round 2): an in-kernel fixup (last-arriving split of a tile sums the
+// slabs) is 3-10x slower on MI355X -- cross-XCD visibility of the partials needs either a full L2
+// writeback/invalidate per workgroup or write-through stores, both far costlier than one extra
+// launch (docs/PERF.md).
+// alloc_part(rows_per_part), when given, returns the BN partial buffer for that layout.
+int conv_gemm_splitk(ConvGemmParams p, const GemmPlan& g, bool dgrad, hipStream_t st, at::TensorOptions opts,
+                     std::vector<at::Tensor>& keep, const std::function<float*(int)>& alloc_part = nullptr) {
+  p.splits = g.splits;
+  if (g.splits == 1) {
+    if (alloc_part) p.part = alloc_part(g.bm);
+    conv_launch(p, g.bm, g.bn, dgrad, st);
+    return g.bm;
+  }
+  at::Tensor slab = at::empty({g.splits, (long long)p.M, p.Nout}, opts);
+  keep.push_back(slab);
+  float* y = p.y;
+  const float* bias = p.bias;
+  const float* addend = p.addend;
+  float* part = alloc_part ? alloc_part(splitk_rows_per_part()) : p.part;
+  RowRemap rr = p.rr;
+  p.y = slab.data_ptr<float>();
+  p.bias = nullptr;
+  p.addend = nullptr;
+  p.part = nullptr;
+  p.rr.on = 0;  // slabs are class-local; the reduction scatters
+  conv_launch(p, g.bm, g.bn, dgrad, st);
+  splitk_reduce_launch(slab.data_ptr<float>(), g.splits, p.M, p.Nout, bias, y, part, st, rr.on ? &rr : nullptr,
+                       addend);
+  return splitk_rows_per_part();
 }
 
 // Workgroups each kernel keeps resident per CU (min of the LDS and VGPR limits of the build).
@@ -394,30 +476,18 @@ std::vector<at::Tensor> conv2d_fwd(const at::Tensor& x_, const at::Tensor& w_, c
   hipStream_t st = cur_stream();
   const at::Tensor xa = amax_parts(x, x_amax, st), wa = amax_parts(w, w_amax, st);
   set_amax(p, xa, wa);
-  if (g.splits == 1) {
-    p.y = y.data_ptr<float>();
-    p.bias = fptr(bias);
-    if (want_stats) {
-      const int nparts = (int)((M + g.bm - 1) / g.bm);
-      part = at::empty({nparts, Co, 2}, opts);
-      p.part = part.data_ptr<float>();
-      rpp = at::full({1}, g.bm, opts.dtype(at::kInt).device(at::kCPU));
-    }
-    conv_launch(p, g.bm, g.bn, false, st);
-  } else {
-    at::Tensor slab = at::empty({g.splits, M, Co}, opts);
-    p.y = slab.data_ptr<float>();
-    conv_launch(p, g.bm, g.bn, false, st);
-    float* partp = nullptr;
-    if (want_stats) {
-      const int rb = splitk_rows_per_part();
-      const int nparts = (int)((M + rb - 1) / rb);
-      part = at::empty({nparts, Co, 2}, opts);
-      partp = part.data_ptr<float>();
-      rpp = at::full({1}, rb, opts.dtype(at::kInt).device(at::kCPU));
-    }
-    splitk_reduce_launch(slab.data_ptr<float>(), g.splits, (int)M, Co, fptr(bias), y.data_ptr<float>(), partp, st);
-  }
+  p.y = y.data_ptr<float>();
+  p.bias = fptr(bias);
+  // BN partials: one per BM-row tile (splits == 1) or per reduction row block (split-K)
+  std::function<float*(int)> alloc_part;
+  if (want_stats)
+    alloc_part = [&](int rows_pp) {
+      part = at::empty({(M + rows_pp - 1) / rows_pp, Co, 2}, opts);
+      return part.data_ptr<float>();
+    };
+  std::vector<at::Tensor> keep;
+  const int rb = conv_gemm_splitk(p, g, false, st, opts, keep, alloc_part);
+  if (want_stats) rpp = at::full({1}, rb, opts.dtype(at::kInt).device(at::kCPU));
   if (want_stats) return {y, part, rpp};
   return {y};
 }
@@ -475,21 +545,10 @@ bool conv2d_dgrad_subpixel(const at::Tensor& dy, const at::Tensor& w, at::Tensor
       }
       GemmPlan g = plan_gemm(Mc, C, std::max(Kc, 32));
       p.ktiles = (Kc + 31) / 32;
-      p.splits = Kc > 0 ? g.splits : 1;
-      if (p.splits == 1) {
-        p.y = dx.data_ptr<float>();
-        p.addend = addend;
-        conv_launch(p, g.bm, g.bn, true, st);
-      } else {
-        at::Tensor slab = at::empty({p.splits, Mc, C}, dy.options());
-        keep.push_back(slab);
-        p.y = slab.data_ptr<float>();
-        RowRemap rr = p.rr;
-        p.rr.on = 0;  // slabs are class-local; the reduction scatters
-        conv_launch(p, g.bm, g.bn, true, st);
-        splitk_reduce_launch(slab.data_ptr<float>(), p.splits, (int)Mc, C, nullptr, dx.data_ptr<float>(), nullptr,
-                             st, &rr, addend);
-      }
+      if (Kc == 0) g.splits = 1;
+      p.y = dx.data_ptr<float>();
+      p.addend = addend;
+      conv_gemm_splitk(p, g, true, st, dy.options(), keep);
     }
   return true;
 }
@@ -497,7 +556,7 @@ bool conv2d_dgrad_subpixel(const at::Tensor& dy, const at::Tensor& w, at::Tensor
 // dX[N, C, H, W] from dY[N, Co, P, Q] and W[Co, C, KH, KW] (any stride / padding).
 at::Tensor conv2d_dgrad(const at::Tensor& dy_, const at::Tensor& w_, std::vector<int64_t> in_shape, int64_t stride,
                         int64_t pad, const c10::optional<at::Tensor>& addend, const c10::optional<at::Tensor>& dy_amax,
-                        const c10::optional<at::Tensor>& w_amax) {
+                        const c10::optional<at::Tensor>& w_amax, const c10::optional<at::Tensor>& w_t) {
   check_f32_cuda(dy_, "grad_output");
   check_f32_cuda(w_, "weight");
   const at::Tensor dy = nhwc(dy_);
@@ -520,9 +579,15 @@ at::Tensor conv2d_dgrad(const at::Tensor& dy_, const at::Tensor& w_, std::vector
     at::Tensor dx = has_add ? *addend : at::empty({N, C, H, W}, opts.memory_format(at::MemoryFormat::ChannelsLast));
     if (conv2d_dgrad_subpixel(dy, w, dx, (int)pad, st, addp, dya, wa)) return dx;
   }
-  // Wt[ci][tap][co] = W[co][tap][ci]
-  at::Tensor wt = at::empty({C, KH * KW * Co}, opts);
-  wtrans_launch(w.data_ptr<float>(), wt.data_ptr<float>(), Co, KH * KW, C, st);
+  // Wt[ci][tap][co] = W[co][tap][ci]: from the step's weight_prep when given, else transposed here
+  at::Tensor wt;
+  if (w_t.has_value() && w_t->defined()) {
+    wt = *w_t;
+    TORCH_CHECK(wt.is_contiguous() && wt.numel() == (long long)C * KH * KW * Co, "dgrad: w_t must be [Ci, KH*KW*Co]");
+  } else {
+    wt = at::empty({C, KH * KW * Co}, opts);
+    wtrans_launch(w.data_ptr<float>(), wt.data_ptr<float>(), Co, KH * KW, C, st);
+  }
   at::Tensor dx = has_add ? *addend : at::empty({N, C, H, W}, opts.memory_format(at::MemoryFormat::ChannelsLast));
   const long long M = (long long)N * H * W;
   const int Kdim = KH * KW * Co;
@@ -535,17 +600,10 @@ at::Tensor conv2d_dgrad(const at::Tensor& dy_, const at::Tensor& w_, std::vector
   p.Nout = C; p.M = (int)M; p.Kdim = Kdim; p.ktiles = g.ktiles; p.splits = g.splits;
   set_divs(p);
   set_amax(p, dya, wa);
-  if (g.splits == 1) {
-    p.y = dx.data_ptr<float>();
-    p.addend = addp;
-    conv_launch(p, g.bm, g.bn, true, st);
-  } else {
-    at::Tensor slab = at::empty({g.splits, M, C}, opts);
-    p.y = slab.data_ptr<float>();
-    conv_launch(p, g.bm, g.bn, true, st);
-    splitk_reduce_launch(slab.data_ptr<float>(), g.splits, (int)M, C, nullptr, dx.data_ptr<float>(), nullptr, st,
-                         nullptr, addp);
-  }
+  p.y = dx.data_ptr<float>();
+  p.addend = addp;
+  std::vector<at::Tensor> keep;
+  conv_gemm_splitk(p, g, true, st, opts, keep);
   return dx;
 }
 
@@ -683,7 +741,8 @@ std::vector<at::Tensor> conv_bn_act_bwd(const at::Tensor& gout_, const at::Tenso
                                         const c10::optional<at::Tensor>& dbeta_out,
                                         const c10::optional<at::Tensor>& dx_addend,
                                         const c10::optional<at::Tensor>& x_amax,
-                                        const c10::optional<at::Tensor>& w_amax) {
+                                        const c10::optional<at::Tensor>& w_amax,
+                                        const c10::optional<at::Tensor>& w_t) {
   check_f32_cuda(gout_, "grad_output");
   const at::Tensor gout = nhwc(gout_);
   const int N = y.size(0), C = y.size(1), H = y.size(2), W = y.size(3);
@@ -756,7 +815,8 @@ std::vector<at::Tensor> conv_bn_act_bwd(const at::Tensor& gout_, const at::Tenso
       if (dx_addend.has_value() && dx_addend->defined()) dx.add_(*dx_addend);
     } else {
       // residual-branch gradient (dx_addend) is accumulated by the data-gradient GEMM's epilogue
-      dx = conv2d_dgrad(dy, w, {x.size(0), x.size(1), x.size(2), x.size(3)}, stride, pad, dx_addend, dya, w_amax);
+      dx = conv2d_dgrad(dy, w, {x.size(0), x.size(1), x.size(2), x.size(3)}, stride, pad, dx_addend, dya, w_amax,
+                        w_t);
     }
   }
   if (overlap) join_from(side);

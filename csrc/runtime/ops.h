@@ -15,7 +15,8 @@ std::vector<at::Tensor> conv2d_fwd(const at::Tensor& x, const at::Tensor& w, con
 at::Tensor conv2d_dgrad(const at::Tensor& dy, const at::Tensor& w, std::vector<int64_t> in_shape, int64_t stride,
                         int64_t pad, const c10::optional<at::Tensor>& addend,
                         const c10::optional<at::Tensor>& dy_amax = c10::nullopt,
-                        const c10::optional<at::Tensor>& w_amax = c10::nullopt);
+                        const c10::optional<at::Tensor>& w_amax = c10::nullopt,
+                        const c10::optional<at::Tensor>& w_t = c10::nullopt);
 at::Tensor conv2d_wgrad(const at::Tensor& dy, const at::Tensor& x, std::vector<int64_t> w_shape, int64_t stride,
                         int64_t pad, const c10::optional<at::Tensor>& out, bool accumulate,
                         const c10::optional<at::Tensor>& dy_amax = c10::nullopt,
@@ -34,6 +35,7 @@ std::vector<at::Tensor> conv_bn_act_fwd(const at::Tensor& x, const at::Tensor& w
                                         const c10::optional<at::Tensor>& x_amax = c10::nullopt,
                                         const c10::optional<at::Tensor>& w_amax = c10::nullopt);
 std::vector<at::Tensor> multi_amax(const std::vector<at::Tensor>& ts);
+std::vector<std::vector<at::Tensor>> weight_prep(const std::vector<at::Tensor>& ts, const std::vector<bool>& want_t);
 std::vector<at::Tensor> conv_bn_act_bwd(const at::Tensor& gout, const at::Tensor& x, const at::Tensor& w,
                                         const at::Tensor& y, const at::Tensor& stats, int64_t stride, int64_t pad,
                                         bool pool, bool relu, bool need_dx, bool has_bias,
@@ -44,7 +46,8 @@ std::vector<at::Tensor> conv_bn_act_bwd(const at::Tensor& gout, const at::Tensor
                                         const c10::optional<at::Tensor>& dbeta_out,
                                         const c10::optional<at::Tensor>& dx_addend,
                                         const c10::optional<at::Tensor>& x_amax = c10::nullopt,
-                                        const c10::optional<at::Tensor>& w_amax = c10::nullopt);
+                                        const c10::optional<at::Tensor>& w_amax = c10::nullopt,
+                                        const c10::optional<at::Tensor>& w_t = c10::nullopt);
 at::Tensor linear_fwd(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tensor>& b);
 std::vector<at::Tensor> linear_bwd(const at::Tensor& gy, const at::Tensor& x, const at::Tensor& w, bool need_dx,
                                    bool has_bias, const c10::optional<at::Tensor>& dw_out,

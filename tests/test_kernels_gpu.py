@@ -384,3 +384,52 @@ def test_torch_custom_ops_with_autograd():
     assert abs(torch.ops.cdp.cross_entropy(logits, tgt).item() - F.cross_entropy(logits, tgt).item()) < 1e-5
     yp, arg = torch.ops.cdp.max_pool2d(cl(torch.randn(2, 32, 8, 8, device="cuda")), 2, 2, 0)
     assert yp.shape == (2, 32, 4, 4) and arg.dtype == torch.uint8
+
+
+@pytest.mark.parametrize("N,Ci,H,W,Co,k,s,p", [CONV_CASES[i] for i in (4, 5, 7)])
+def test_split_k_conv_is_deterministic_and_exact_order(N, Ci, H, W, Co, k, s, p):
+    """Split-K shapes (in-kernel fixup: the last split of each tile sums the partial slabs in split
+    order): repeated launches are bitwise identical, BN partials included, and match fp64."""
+    torch.manual_seed(3)
+    x = torch.randn(N, Ci, H, W, device="cuda")
+    w = torch.randn(Co, Ci, k, k, device="cuda") * (1.0 / (Ci * k * k) ** 0.5)
+    b = torch.randn(Co, device="cuda")
+    outs = [C().conv2d_fwd(cl(x), cl(w), b, s, p, True) for _ in range(3)]
+    gy = torch.randn_like(outs[0][0])
+    dxs = [C().conv2d_dgrad(cl(gy), cl(w), list(x.shape), s, p) for _ in range(3)]
+    for o in outs[1:]:
+        assert torch.equal(o[0], outs[0][0]) and torch.equal(o[1], outs[0][1])
+    for d in dxs[1:]:
+        assert torch.equal(d, dxs[0])
+    ref = F.conv2d(x.double().cpu(), w.double().cpu(), b.double().cpu(), s, p)
+    assert rel_err(outs[0][0], ref) < 2e-5
+    xr = x.double().cpu().requires_grad_()
+    F.conv2d(xr, w.double().cpu(), None, s, p).backward(gy.double().cpu())
+    assert rel_err(dxs[0], xr.grad) < 2e-5
+
+
+def test_weight_prep_transposes_and_maxima():
+    """One launch for all conv weights: W^T [Ci, KH*KW*Co] where asked, and the |max| partials
+    (f16x2) whose max is each weight's |max|; dgrad with the prepared W^T equals dgrad without."""
+    torch.manual_seed(4)
+    ws = [cl(torch.randn(co, ci, k, k, device="cuda")) for co, ci, k in
+          [(64, 3, 3), (128, 64, 3), (512, 512, 3), (256, 64, 1), (10, 7, 3)]]
+    want = [False, True, True, True, True]
+    amax, wts = C().weight_prep(ws, want)
+    for w, wt, f in zip(ws, wts, want):
+        if not f:
+            continue
+        co, ci, kh, kw = w.shape
+        ref = w.permute(1, 2, 3, 0).reshape(ci, kh * kw * co)  # [ci][kh][kw][co]
+        assert torch.equal(wt, ref)
+    if C().get_conv_gemm() == "f16x2":
+        assert len(amax) == len(ws)
+        for w, a in zip(ws, amax):
+            assert a.max().item() == w.abs().max().item()
+    x = torch.randn(2, 128, 8, 8, device="cuda")
+    gy = torch.randn(2, 512, 8, 8, device="cuda")
+    w = ws[2]
+    a = C().conv2d_dgrad(cl(gy), w, [2, 512, 8, 8], 1, 1)
+    b = C().conv2d_dgrad(cl(gy), w, [2, 512, 8, 8], 1, 1, None, None, None, wts[2])
+    assert torch.equal(a, b)
+    del x
