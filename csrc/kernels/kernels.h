@@ -126,6 +126,16 @@ void slab_sum_launch(const float* slab, int S, long long n, float* dst, bool acc
 void slab_sum_strided_launch(const float* slab, int S, long long n_src, int src_cols, int dst_cols, float* dst,
                              bool accumulate, hipStream_t st);
 
+// stem.hip: 3x3 / stride 1 / pad 1 convs with Cin <= 4 and 64 outputs (exact fp32 MFMA)
+bool stem_ok(int Cin, int KH, int KW, int stride, int pad, int Co);
+void stem_fwd_launch(const float* x, const float* w, const float* bias, float* y, float* part, int N, int H, int W,
+                     int Cin, int Co, hipStream_t st);
+int stem_wgrad_blocks(int N, int H, int W);
+// dW partials [nblk][64][36] with the pool(2x2)/ReLU/BatchNorm(training) backward applied on the fly;
+// Co = 64, even H and W
+void stem_wgrad_launch(const float* y, const float* gout, const float* stats, const float* sums, const float* x,
+                       float* slab, int nblk, int N, int H, int W, int Cin, hipStream_t st);
+
 // bn.hip
 int bn_bwd_grid(int N, int H, int W, int C, bool pool);
 void bn_finalize_launch(const float* part, int nparts, int rpp, int M, int C, const float* gamma, const float* beta,

@@ -666,6 +666,52 @@ at::Tensor conv2d_wgrad_keep(const at::Tensor& dy_, const at::Tensor& x_, std::v
   return dw;
 }
 
+// ---------------------------------------------------------------- RGB stem (stem.hip)
+bool stem_enabled() {
+  static const bool on = [] {
+    const char* e = std::getenv("CDP_STEM");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
+// Training-mode conv + BN + act [+ pool] of a Cin <= 4 stem; same outputs as conv_bn_act_fwd with
+// x saved unpadded (xsave = x) and no f16x2 maxima for x / W (the stem kernels need none).
+std::vector<at::Tensor> stem_bn_act_fwd(const at::Tensor& x_, const at::Tensor& w_, const c10::optional<at::Tensor>& b,
+                                        const c10::optional<at::Tensor>& gamma, const c10::optional<at::Tensor>& beta,
+                                        const c10::optional<at::Tensor>& running_mean,
+                                        const c10::optional<at::Tensor>& running_var,
+                                        const c10::optional<at::Tensor>& num_batches_tracked, double momentum,
+                                        double eps, bool pool, bool relu) {
+  check_f32_cuda(x_, "x");
+  check_f32_cuda(w_, "weight");
+  const at::Tensor x = nhwc(x_), w = nhwc(w_);
+  const int N = x.size(0), Cin = x.size(1), H = x.size(2), W = x.size(3), Co = w.size(0);
+  TORCH_CHECK(w.size(1) == Cin, "stem weight in-channels mismatch");
+  auto opts = x.options();
+  hipStream_t st = cur_stream();
+  at::Tensor y = at::empty({N, Co, H, W}, opts.memory_format(at::MemoryFormat::ChannelsLast));
+  const long long M = (long long)N * H * W;
+  const int nparts = (int)((M + 255) / 256);
+  at::Tensor part = at::empty({nparts, Co, 2}, opts);
+  stem_fwd_launch(x.data_ptr<float>(), w.data_ptr<float>(), fptr(b), y.data_ptr<float>(), part.data_ptr<float>(), N,
+                  H, W, Cin, Co, st);
+  at::Tensor stats = at::empty({4, Co}, opts);
+  long long* nbt = nullptr;
+  if (num_batches_tracked.has_value() && num_batches_tracked->defined())
+    nbt = reinterpret_cast<long long*>(num_batches_tracked->data_ptr<int64_t>());
+  bn_finalize_launch(part.data_ptr<float>(), nparts, 256, (int)M, Co, fptr(gamma), fptr(beta),
+                     fptr_mut(running_mean), fptr_mut(running_var), nbt, (float)momentum, (float)eps,
+                     stats.data_ptr<float>(), st);
+  at::Tensor out = at::empty({N, Co, pool ? H / 2 : H, pool ? W / 2 : W},
+                             opts.memory_format(at::MemoryFormat::ChannelsLast));
+  at::Tensor out_amax;
+  if (f16x2_mode()) out_amax = at::empty({bn_act_grid(N, H, W, Co, pool)}, opts);
+  bn_act_fwd_launch(y.data_ptr<float>(), stats.data_ptr<float>(), nullptr, out.data_ptr<float>(), N, H, W, Co, pool,
+                    relu, st, out_amax.defined() ? out_amax.data_ptr<float>() : nullptr);
+  return {out, y, stats, x, out_amax, at::Tensor(), at::Tensor()};
+}
+
 // ---------------------------------------------------------------- fused block forward
 // out = [maxpool2](act(BN(conv3x3(x) + b) [+ residual])), training or eval BatchNorm.
 // Returns {out, y (conv output), stats [4, C] = (mean, invstd, scale, shift)}.
@@ -679,7 +725,13 @@ std::vector<at::Tensor> conv_bn_act_fwd(const at::Tensor& x, const at::Tensor& w
                                         const c10::optional<at::Tensor>& residual,
                                         const c10::optional<at::Tensor>& x_amax,
                                         const c10::optional<at::Tensor>& w_amax) {
-  // RGB stem: zero-pad 3 -> 4 channels so the float4 gather path runs (the padded input is what
+  // RGB stem (3x3 / stride 1 / pad 1, Cin <= 4, training BN): one exact-fp32 MFMA kernel reading
+  // the raw NHWC input, no channel padding, no operand scales (stem.hip)
+  if (stem_enabled() && stem_ok((int)x.size(1), (int)w.size(2), (int)w.size(3), stride, pad, (int)w.size(0)) &&
+      training && !(residual.has_value() && residual->defined()))
+    return stem_bn_act_fwd(x, w, b, gamma, beta, running_mean, running_var, num_batches_tracked, momentum, eps, pool,
+                           relu);
+  // other stems: zero-pad 3 -> 4 channels so the float4 gather path runs (the padded input is what
   // backward needs, so it is returned for saving)
   const bool padc = (x.size(1) % 4) != 0;
   const bool have_xa = x_amax.has_value() && x_amax->defined();
@@ -776,6 +828,24 @@ std::vector<at::Tensor> conv_bn_act_bwd(const at::Tensor& gout_, const at::Tenso
                        dgamma.data_ptr<float>(), false, st, ps, fused_db ? db.data_ptr<float>() : nullptr,
                        stats.data_ptr<float>() + 2 * C, (long long)N * H * W, dbmode);
   if (!training && dbmode != 2) sums.zero_();
+  // RGB stem without an input gradient (VGG layer 0): the weight-gradient kernel applies the
+  // BN / ReLU / pool backward on the fly, so dy is never materialised (stem.hip)
+  const int cin = (int)x.size(1);
+  if (stem_enabled() && !need_dx && training && pool && relu && !zout.defined() && fused_db && C == 64 &&
+      stem_ok(cin, (int)w.size(2), (int)w.size(3), stride, pad, C) && cin == (int)w.size(1) && (H % 2) == 0 &&
+      (W % 2) == 0) {
+    const at::Tensor xin = nhwc(x);
+    const int nb = stem_wgrad_blocks(N, H, W);
+    at::Tensor slab = at::empty({nb, C, 36}, opts);
+    stem_wgrad_launch(y.data_ptr<float>(), gout.data_ptr<float>(), stats.data_ptr<float>(), sums.data_ptr<float>(),
+                      xin.data_ptr<float>(), slab.data_ptr<float>(), nb, N, H, W, cin, st);
+    at::Tensor dw = dw_out.has_value() && dw_out->defined()
+                        ? *dw_out
+                        : at::empty({C, cin, w.size(2), w.size(3)}, opts.memory_format(at::MemoryFormat::ChannelsLast));
+    TORCH_CHECK(dw.is_contiguous(at::MemoryFormat::ChannelsLast), "stem dW slot must be channels_last");
+    slab_sum_strided_launch(slab.data_ptr<float>(), nb, (long long)C * 36, 4, cin, dw.data_ptr<float>(), false, st);
+    return {at::Tensor(), dw, db, dgamma, dbeta, at::Tensor()};
+  }
   at::Tensor dy = at::empty({N, C, H, W}, opts.memory_format(at::MemoryFormat::ChannelsLast));
   at::Tensor dbpart;
   const bool sep_db = has_bias && !fused_db;

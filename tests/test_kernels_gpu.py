@@ -135,6 +135,44 @@ def test_fused_block_matches_torch(N, Ci, H, W, Co, pool, training):
         assert int(bn.num_batches_tracked) == int(bn_r.num_batches_tracked) == 1
 
 
+@pytest.mark.parametrize("N,H,W,x_grad", [(8, 32, 32, False), (3, 10, 6, False), (4, 8, 8, True)])
+def test_rgb_stem_block_matches_torch(N, H, W, x_grad):
+    """VGG layer 0 (Cin = 3): exact-fp32 stem forward (stem_fwd_kernel) and, without an input
+    gradient, the weight gradient with the BN/ReLU/pool backward applied on the fly
+    (stem_wgrad_kernel) against fp64 torch."""
+    from cs744_distributed_data_parallel_amd.ops import functional as CF
+
+    torch.manual_seed(5)
+    conv = torch.nn.Conv2d(3, 64, 3, 1, 1).cuda()
+    bn = torch.nn.BatchNorm2d(64).cuda()
+    with torch.no_grad():
+        bn.weight.uniform_(0.5, 1.5)
+        bn.bias.uniform_(-0.5, 0.5)
+    conv_r = torch.nn.Conv2d(3, 64, 3, 1, 1).double()
+    bn_r = torch.nn.BatchNorm2d(64).double()
+    conv_r.load_state_dict(conv.state_dict())
+    bn_r.load_state_dict(bn.state_dict())
+    conv.weight.data = cl(conv.weight.data)
+    x = torch.randn(N, 3, H, W, device="cuda")
+    xn = cl(x).requires_grad_(x_grad)
+    out = CF.conv_bn_act(xn, conv, bn, relu=True, pool=True)
+    xr = x.double().cpu().requires_grad_(x_grad)
+    ref = F.max_pool2d(F.relu(bn_r(conv_r(xr))), 2, 2)
+    assert rel_err(out, ref) < 1e-5
+    g = torch.randn_like(out)
+    out.backward(g)
+    ref.backward(g.double().cpu())
+    if x_grad:
+        assert rel_err(xn.grad, xr.grad) < 5e-4
+    assert rel_err(conv.weight.grad, conv_r.weight.grad) < 5e-5
+    assert rel_err(bn.weight.grad, bn_r.weight.grad) < 5e-5
+    assert rel_err(bn.bias.grad, bn_r.bias.grad) < 5e-5
+    assert (conv.bias.grad.double().cpu() - conv_r.bias.grad).abs().max().item() < 1e-3 * (
+        conv_r.bias.grad.abs().max().item() + g.abs().mean().item())
+    assert rel_err(bn.running_mean, bn_r.running_mean) < 1e-5
+    assert rel_err(bn.running_var, bn_r.running_var) < 1e-5
+
+
 def test_residual_block_no_pool():
     from cs744_distributed_data_parallel_amd.ops import functional as CF
 
