@@ -336,7 +336,14 @@ struct WgradPlan {
 WgradPlan plan_wgrad(int Cout, int Kdim, long long M) {
   WgradPlan w;
   w.bm = Cout >= 128 ? 128 : 64;
-  w.bn = (Kdim % 128 == 0) ? 128 : 64;
+  // 128-wide k tiles also when Kdim is an odd multiple of 64 and >= 512 (e.g. 576 = 9 x 64: 4.5
+  // tiles, the last one half padding). Measured on VGG-11 layer 1 (B=256): 70.7 -> 61.9 us.
+  // CDP_WGRAD_BN=64 restores the exact 64-wide tiling.
+  static const int force_bn = [] {
+    const char* e = std::getenv("CDP_WGRAD_BN");
+    return e ? std::atoi(e) : 128;
+  }();
+  w.bn = (Kdim % 128 == 0 || (force_bn == 128 && Kdim >= 512)) ? 128 : 64;
   // 256x128 f16x2 tiles, 8 waves, one workgroup per CU (pipelined kernel only; CDP_WGRAD_BM=128
   // for the 128-wide tiles). Measured on MI355X, VGG-11 B=256: 156.0k -> 161.7k img/s (the x
   // gather and split are shared by four co waves instead of two)
