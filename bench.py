@@ -281,6 +281,10 @@ def rank_main(args) -> int:
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # native RCCL communicator unavailable on some rank -> all ranks agree to use torch's nccl (=RCCL)
+    # process group instead of failing the run (distributed._init_native_rccl); "comm" in the JSON
+    # says which one ran
+    os.environ.setdefault("CDP_RCCL_FALLBACK", "1")
     if os.environ.get("CDP_BENCH_FAIL_RANK") == str(rank):  # launcher test hook
         raise SystemExit(f"[bench] rank {rank}: CDP_BENCH_FAIL_RANK")
     if world != args.gpus:

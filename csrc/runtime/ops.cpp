@@ -258,8 +258,19 @@ int conv_blocks_per_cu(int bm, int bn) {
   return std::max(1, std::min(4, (160 * 1024) / (2 * (bm + bn) * 36 * 4)));
 }
 double conv_mfma_rate() {
+  static const double scale = [] {  // tuning knob for the split-K cost model (CDP_MFMA_RATE_SCALE)
+    const char* e = std::getenv("CDP_MFMA_RATE_SCALE");
+    return e ? std::atof(e) : 1.0;
+  }();
   const int m = conv_gemm_mode();
-  return m == 1 ? 250.0e12 : m == 2 ? 800.0e12 : m == 3 ? 450.0e12 : 120.0e12;
+  return scale * (m == 1 ? 250.0e12 : m == 2 ? 800.0e12 : m == 3 ? 450.0e12 : 120.0e12);
+}
+double slab_bw() {
+  static const double bw = [] {  // modelled split-K slab round-trip bandwidth (CDP_SLAB_BW, B/s)
+    const char* e = std::getenv("CDP_SLAB_BW");
+    return e ? std::atof(e) : 4.0e12;
+  }();
+  return bw;
 }
 int wgrad_blocks_per_cu(int bm, int bn) {
   // f16x2, two-stage pipeline (default, CDP_WGRAD_PIPE=0 for one stage): 2 stages x 2 planes x
@@ -287,7 +298,7 @@ int choose_splits(long long tiles, int ktiles, int slots, int min_kt, double flo
     const long long blocks = tiles * s;
     const long long waves = (blocks + slots - 1) / slots;
     const double eff = (double)blocks / (double)(waves * slots);
-    const double slab = s > 1 ? 2.0 * s * slab_bytes_per_split / 4.0e12 : 0.0;
+    const double slab = s > 1 ? 2.0 * s * slab_bytes_per_split / slab_bw() : 0.0;
     return flops / (rate * eff) + slab;
   };
   int best = 1;
