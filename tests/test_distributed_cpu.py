@@ -309,3 +309,37 @@ def test_bucket_allreduce_overlaps_backward(strategy):
             assert kinds[-1] == "f"
             ts = [t for _, _, t in log]
             assert ts == sorted(ts)
+
+
+# ----------------------------------------------------------------------------- resume agreement
+def _agreed_resume(rank, world, root, shared):
+    import os
+
+    from cs744_distributed_data_parallel_amd import distributed as dist
+    from cs744_distributed_data_parallel_amd.train import _agreed_checkpoint
+
+    d = root if shared else os.path.join(root, f"rank{rank}")
+    os.makedirs(d, exist_ok=True)
+    if rank == 0:  # only rank 0 writes checkpoints (utils/checkpoint.py)
+        for e in (1, 2):
+            with open(os.path.join(d, f"ckpt_{e}.pt"), "wb") as fh:
+                fh.write(b"x")
+    dist.barrier()
+    if not shared:  # this rank's filesystem shows only its own directory (no shared storage)
+        real = os.path.isfile
+        os.path.isfile = lambda q: q.startswith(d) and real(q)
+    try:
+        return ("ok", _agreed_checkpoint(d, world))
+    except RuntimeError as e:
+        return ("error", str(e))
+
+
+def test_resume_checkpoint_is_chosen_by_rank0_and_checked_on_every_rank(tmp_path):
+    """--resume: every rank loads the checkpoint rank 0 picked (shared dir), and a checkpoint that
+    some rank cannot read fails on every rank instead of silently diverging the replicas."""
+    ok = run_ranks(_agreed_resume, 2, (str(tmp_path / "shared"), True))
+    assert ok[0][0] == ok[1][0] == "ok"
+    assert ok[0][1] == ok[1][1] and ok[0][1].endswith("ckpt_2.pt")
+    bad = run_ranks(_agreed_resume, 2, (str(tmp_path / "private"), False))
+    assert bad[0][0] == bad[1][0] == "error", bad
+    assert "not readable on every rank" in bad[1][1]
