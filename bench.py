@@ -60,6 +60,9 @@ def parse(argv=None):
     p.add_argument("--dataset-size", type=int, default=50000)
     p.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
                    help="cpu = gloo smoke mode of the multi-process path (reference ops, tiny sizes)")
+    p.add_argument("--dist-backend", default="auto", choices=["auto", "gloo"],
+                   help="gloo: rehearse the multi-rank GPU path on ONE GPU (all ranks share cuda:0, gradients "
+                        "over gloo; not a performance mode)")
     return p.parse_args(argv)
 
 
@@ -306,9 +309,13 @@ def rank_main(args) -> int:
         if world > 1:
             dist.init_process_group("gloo", rank=rank, world_size=world)
     else:
+        if args.dist_backend == "gloo":
+            local = local % max(1, torch.cuda.device_count())
         torch.cuda.set_device(local)
         dev = torch.device("cuda", local)
-        if world > 1:
+        if world > 1 and args.dist_backend == "gloo":
+            dist.init_process_group("gloo", rank=rank, world_size=world)
+        elif world > 1:
             # collectives that stall longer than 5 minutes are aborted by the communicator's watchdog
             dist.init_process_group("rccl" if args.backend == "native" else "nccl", rank=rank, world_size=world,
                                     comm_timeout_s=300.0)
@@ -318,7 +325,7 @@ def rank_main(args) -> int:
                 cdp._native.lib().set_conv_gemm("bf16")
     ranks_seen = dist.ranks_seen() if world > 1 else 1
     comm_kind = ("rccl-native" if dist.native_communicator() is not None else
-                 ("gloo" if cpu else "torch-nccl")) if world > 1 else "none"
+                 ("gloo" if (cpu or args.dist_backend == "gloo") else "torch-nccl")) if world > 1 else "none"
 
     strong_lb = max(1, REF_GLOBAL_BATCH // world)
     main_lb = args.local_batch if args.scaling == "weak" else strong_lb
