@@ -316,6 +316,17 @@ def test_bench_self_launches_ranks_cpu():
     assert rec["exposed_comm_ms"] >= 0 and rec["value"] > 0
 
 
+@pytest.mark.parametrize("strategy", ["gather_scatter", "allreduce_blocking", "bucketed_overlap"])
+def test_bench_every_strategy_through_the_launcher_cpu(strategy):
+    """Parts 2a / 2b / bucketed overlap through the same self-launching bench path (ddp is the
+    default, covered above): each produces one record with both ranks seen."""
+    r = _bench(["--gpus", "2", "--device", "cpu", "--strategy", strategy, "--steps", "1", "--warmup", "1",
+                "--local-batch", "2", "--dataset-size", "16", "--no-extra"])
+    assert r.returncode == 0, r.stderr[-3000:]
+    rec = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    assert rec["ranks_seen"] == 2 and rec["config"]["strategy"] == strategy
+
+
 def test_bench_failing_rank_fails_the_launcher():
     r = _bench(["--gpus", "2", "--device", "cpu", "--steps", "1", "--warmup", "1", "--local-batch", "2",
                 "--dataset-size", "16", "--no-extra"], env_extra={"CDP_BENCH_FAIL_RANK": "1"})
