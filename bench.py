@@ -164,6 +164,7 @@ class _Run:
         self.nb = max(1, self.order.numel() // local_batch)
         self.static_idx = torch.empty(local_batch, dtype=torch.int64, device=dev)
         self.graph = None
+        self.break_capture = os.environ.get("CDP_BENCH_BREAK_CAPTURE") == "1"  # recovery test hook
 
     def _set_batch(self, i):
         s = (i % self.nb) * self.local_batch
@@ -187,6 +188,8 @@ class _Run:
         elif self.sync_grads and strategy == "gather_scatter":
             cdp.parallel.average_gradients_gather_scatter(self.model)
         self.opt.step()
+        if self.break_capture and self.torch.cuda.is_current_stream_capturing():
+            loss.item()  # test hook: a host read of a captured value invalidates the capture
         return loss
 
     def prepare(self, warmup, dbg):
@@ -199,7 +202,9 @@ class _Run:
         if cuda:
             torch.cuda.synchronize()
         dbg("eager warmup done")
-        if self.args.no_graph or not cuda:
+        # gloo executes its collectives on the host, which no stream capture survives (and a rank
+        # failing mid-capture would leave its peer blocked in the collective): eager steps
+        if self.args.no_graph or not cuda or self.args.dist_backend == "gloo":
             return
         try:
             s = torch.cuda.Stream()
@@ -210,8 +215,17 @@ class _Run:
             torch.cuda.current_stream().wait_stream(s)
             torch.cuda.synchronize()
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
-                self.body()
+            cs = torch.cuda.Stream()
+            cs.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(cs):
+                # thread-local capture mode: a failing rank's other threads (watchdog, autograd
+                # workers) cannot invalidate it, and ending it below always leaves capture mode
+                g.capture_begin(capture_error_mode="thread_local")
+                try:
+                    self.body()
+                finally:
+                    g.capture_end()
+            torch.cuda.current_stream().wait_stream(cs)
             torch.cuda.synchronize()
             for i in range(2):  # warm replays
                 self._set_batch(i)
@@ -220,9 +234,9 @@ class _Run:
             self.graph = g
             dbg("captured")
         except Exception as e:  # pragma: no cover - depends on the runtime
-            print(f"[bench] hipGraph capture failed ({e!r}); timing eager steps", file=sys.stderr)
+            print(f"[bench] hipGraph capture failed ({str(e)[:200]!r}); timing eager steps", file=sys.stderr)
             self.graph = None
-            torch.cuda.synchronize()
+            self._recover_from_failed_capture()
         if self.world > 1:
             # all ranks replay graphs or all run eager (a capture records collectives without running
             # them, so dropping every rank's graph after one rank's failure keeps the order matched)
@@ -237,6 +251,20 @@ class _Run:
                 print("[bench] another rank could not capture; all ranks time eager steps", file=sys.stderr)
                 self.graph.reset()
                 self.graph = None
+
+    def _recover_from_failed_capture(self):
+        """An invalidated capture leaves the thread's last HIP error set (the next launch would report
+        it) and may leave a reducer armed mid-backward: clear both so eager steps can run."""
+        torch = self.torch
+        if self.args.backend == "native":
+            self.cdp._native.lib().clear_hip_error()
+        for r in (getattr(self.model, "reducer", None), getattr(self.sync, "reducer", None)):
+            if isinstance(r, self.cdp.parallel.reducer.GradReducer):
+                r.disarm()
+        torch.cuda.synchronize()
+        if self.args.backend == "native":
+            self.cdp._native.lib().clear_hip_error()
+        self.opt.zero_grad()
 
     def time(self, steps, dist):
         torch = self.torch

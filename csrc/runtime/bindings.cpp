@@ -18,6 +18,8 @@ PYBIND11_MODULE(_C, m) {
         "select the conv GEMM engine: x3 (3-term bf16 split), f16x2 (scaled 2-term fp16 split), f32 (exact fp32 "
         "MFMA) or bf16 (bf16 operands, non-parity)");
   m.def("get_conv_gemm", &get_conv_gemm);
+  m.def("clear_hip_error", [] { return std::string(hipGetErrorName(hipGetLastError())); },
+        "reset the thread's last HIP error (e.g. after an invalidated stream capture) and return its name");
   m.def("conv2d_fwd", &conv2d_fwd, py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("stride"), py::arg("pad"),
         py::arg("want_stats") = false, py::arg("x_amax") = py::none(), py::arg("w_amax") = py::none());
   m.def("conv2d_dgrad", &conv2d_dgrad, py::arg("dy"), py::arg("w"), py::arg("in_shape"), py::arg("stride"),
