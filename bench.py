@@ -162,19 +162,14 @@ class _Run:
         self.model = model
         self.order = self.loader._order()
         self.nb = max(1, self.order.numel() // local_batch)
-        self.static_idx = torch.empty(local_batch, dtype=torch.int64, device=dev)
         self.graph = None
         self.break_capture = os.environ.get("CDP_BENCH_BREAK_CAPTURE") == "1"  # recovery test hook
-
-    def _set_batch(self, i):
-        s = (i % self.nb) * self.local_batch
-        self.static_idx.copy_(self.order[s:s + self.local_batch], non_blocking=True)
 
     def body(self):
         import contextlib
 
         cdp, strategy = self.cdp, self.args.strategy
-        x, y = self.loader.batch(self.static_idx, 0, self.local_batch)
+        x, y = self.loader.batch(self.order, 0, self.local_batch, nbatches=self.nb)
         self.opt.zero_grad()
         nosync = (not self.sync_grads and self.world > 1 and hasattr(self.model, "no_sync"))
         with (self.model.no_sync() if nosync else contextlib.nullcontext()):
@@ -197,7 +192,6 @@ class _Run:
         cuda = self.dev.type == "cuda"
         # eager warmup (includes the bucket rebuild in ready order after iteration 1)
         for i in range(max(3, warmup)):
-            self._set_batch(i)
             self.body()
         if cuda:
             torch.cuda.synchronize()
@@ -228,7 +222,6 @@ class _Run:
             torch.cuda.current_stream().wait_stream(cs)
             torch.cuda.synchronize()
             for i in range(2):  # warm replays
-                self._set_batch(i)
                 g.replay()
             torch.cuda.synchronize()
             self.graph = g
@@ -275,7 +268,6 @@ class _Run:
             torch.cuda.synchronize()
         t0 = time.perf_counter()
         for i in range(steps):
-            self._set_batch(i)
             if self.graph is not None:
                 self.graph.replay()
             else:

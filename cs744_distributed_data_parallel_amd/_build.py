@@ -22,7 +22,7 @@ ARCH = os.environ.get("CDP_OFFLOAD_ARCH", "gfx950")
 EXT_SUFFIX = sysconfig.get_config_var("EXT_SUFFIX") or ".so"
 OUTPUT = os.path.join(PKG_DIR, "_C" + EXT_SUFFIX)
 
-KERNELS = ["conv_igemm.hip", "conv_x3.hip", "wgrad.hip", "bn.hip", "misc.hip", "stem.hip"]
+KERNELS = ["conv_igemm.hip", "conv_x3.hip", "wgrad.hip", "bn.hip", "misc.hip", "stem.hip", "bwd_fuse.hip"]
 RUNTIME = ["ops.cpp", "rccl_comm.cpp", "reducer.cpp", "torch_ops.cpp", "bindings.cpp"]
 
 

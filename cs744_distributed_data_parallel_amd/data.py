@@ -167,17 +167,27 @@ class DeviceLoader:
     def dataset(self):
         return self.ds
 
-    def batch(self, idx: torch.Tensor, offset: int, bsz: int, out: Optional[torch.Tensor] = None):
-        """Produce one batch from ``idx[offset:offset+bsz]`` (graph-capturable on GPU)."""
+    def batch(self, idx: torch.Tensor, offset: int, bsz: int, out: Optional[torch.Tensor] = None,
+              nbatches: int = 0):
+        """Produce one batch from ``idx[offset:offset+bsz]`` (graph-capturable on GPU).
+
+        ``nbatches > 0``: the batch is ``idx[offset + (step % nbatches) * bsz :][:bsz]`` with ``step``
+        the loader's on-device step counter, so one captured hipGraph walks the whole order with no
+        per-step host work. The labels are gathered by the same kernel.
+        """
         pad = self.ds.pad if self.train else 0
         flip = self.train
         if self.dev.type == "cuda":
             C = _native.lib()
+            target = torch.empty(bsz, dtype=torch.int64, device=self.dev)
             data = C.augment(self.ds.images, idx, offset, bsz, self.ds.mean, self.ds.std, pad, flip, self._counter,
-                             self.seed, out)
+                             self.seed, out, nbatches, self.ds.labels, target)
             C.counter_inc(self._counter)
-            target = self.ds.labels.index_select(0, idx[offset : offset + bsz])
             return data, target
+        if nbatches > 0:
+            offset += (int(self._counter.item()) % nbatches) * bsz
+            if not pad:
+                self._counter += 1  # (the padded path advances it itself)
         return self._cpu_batch(idx[offset : offset + bsz], pad, flip)
 
     def _cpu_batch(self, sel, pad, flip):

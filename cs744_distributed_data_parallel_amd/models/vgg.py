@@ -80,9 +80,12 @@ class VGG(nn.Module):
             # (the first conv's input needs no gradient: no transpose)
             need = [k > 0 or x.requires_grad for k in range(len(self._plan))]
             wam, wts = CF.weight_prep([layers[ci].weight for ci, _, _ in self._plan], need)
+            last = len(self._plan) - 1
             for k, (ci, bi, pool) in enumerate(self._plan):
+                # each block's output feeds only the next block: its BN statistics reduction rides
+                # on that block's backward (CF.conv_bn_act bn_link)
                 x = CF.conv_bn_act(x, layers[ci], layers[bi], relu=True, pool=pool,
-                                   w_amax=wam[k] if wam is not None else None, w_t=wts[k])
+                                   w_amax=wam[k] if wam is not None else None, w_t=wts[k], bn_link=k < last)
             y = x.reshape(x.size(0), -1)
             return CF.linear(y, self.fc1.weight, self.fc1.bias)
         y = self.layers(x)

@@ -110,10 +110,34 @@ class GradSink:
         return GradSink()
 
 
+class _BNLink:
+    """Backward hand-off between two chained blocks (``bn_link``): block L's output feeds only block
+    L+1. Block L+1's backward, whose data-gradient reduction produces the gradient at block L's
+    output anyway, also reduces block L's BatchNorm statistics from it in the same launch
+    (csrc/kernels/bwd_fuse.hip) and leaves them in ``part``; block L's backward then skips its own
+    statistics pass. ``gptr`` pins the hand-off to that exact gradient tensor."""
+
+    __slots__ = ("y", "stats", "pool", "relu", "ps", "part", "gptr")
+
+    def __init__(self, y, stats, pool, relu, ps):
+        self.y, self.stats, self.pool, self.relu, self.ps = y, stats, pool, relu, ps
+        self.part, self.gptr = None, None
+
+
+LINK_HANDOFFS = [0]  # BN statistics reductions taken from the consumer block's backward (tests read it)
+
+
+def _get_link(t):
+    tag = getattr(t, "_cdp_bnlink", None)
+    if tag is None or tag[1] != t._version:
+        return None
+    return tag[0]
+
+
 class _ConvBNAct(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, b, gamma, beta, rm, rv, nbt, momentum, eps, training, stride, pad, pool, relu, residual,
-                res_sink=None, dx_sink=None, w_amax=None, w_t=None):
+                res_sink=None, dx_sink=None, w_amax=None, w_t=None, bn_link=False):
         C = _native.lib()
         out, y, stats, xsave, out_amax, x_amax, w_amax = C.conv_bn_act_fwd(
             x, w, b, gamma, beta, rm, rv, nbt, momentum, eps, training, stride, pad, pool, relu, residual, _get_amax(x),
@@ -127,6 +151,14 @@ class _ConvBNAct(torch.autograd.Function):
         zout = out if residual is not None else None
         ctx.save_for_backward(xsave, w, y, stats, zout)  # xsave: x, or x zero-padded to 4k channels
         _set_amax(out, out_amax)
+        # the producer of x handed over its BN (see _BNLink); this block is its only consumer
+        ctx.link_in = _get_link(x) if dx_sink is None else None
+        ctx.link_out = None
+        if bn_link and residual is None and _bwd_fuse_on():
+            odd_pool = pool and (y.shape[2] % 2 == 1 or y.shape[3] % 2 == 1)
+            ps = 3 if (b is not None and not odd_pool and training) else 2  # as conv_bn_act_bwd's
+            ctx.link_out = _BNLink(y, stats, pool, relu, ps)
+            out._cdp_bnlink = (ctx.link_out, out._version)
         return out
 
     @staticmethod
@@ -143,12 +175,26 @@ class _ConvBNAct(torch.autograd.Function):
                 park_dx = True
             else:
                 addend, dx_sink.grad = dx_sink.grad, None
-        dx, dw, db, dgamma, dbeta, dres = C.conv_bn_act_bwd(
+        part_in, lo = None, ctx.link_out
+        if lo is not None:
+            if lo.part is not None and lo.gptr == gout.data_ptr():
+                part_in = lo.part
+                LINK_HANDOFFS[0] += 1
+            lo.part = lo.gptr = None
+        li = ctx.link_in
+        prev = (None, None, False, False, 2)
+        if li is not None and nig[0] and not park_dx and addend is None:
+            prev = (li.y, li.stats, li.pool, li.relu, li.ps)
+        dx, dw, db, dgamma, dbeta, dres, prev_part = C.conv_bn_act_bwd(
             gout, x, w, y, stats, stride, pad, pool, relu, nig[0], has_bias, zout, training,
             _slot(wp, nig[1]), _slot(bp, nig[2] and has_bias), _slot(gp, nig[3]), _slot(betap, nig[4]), addend,
-            *ctx.amax, ctx.w_t,
+            *ctx.amax, ctx.w_t, part_in, *prev,
         )
         ctx.w_t = None
+        if li is not None:
+            li.part = prev_part if (prev_part is not None and dx is not None) else None
+            li.gptr = dx.data_ptr() if li.part is not None else None
+            ctx.link_in = None
         if park_dx:
             dx_sink.grad, dx = dx, None
         if has_res and res_sink is not None and nig[15]:
@@ -165,12 +211,18 @@ class _ConvBNAct(torch.autograd.Function):
             dbeta if ctx.needs_input_grad[4] else None,
             None, None, None, None, None, None, None, None, None, None,
             dres if has_res else None,
-            None, None, None, None,
+            None, None, None, None, None,
         )
 
 
+def _bwd_fuse_on() -> bool:
+    import os
+
+    return os.environ.get("CDP_BWD_FUSE", "1") != "0"
+
+
 def conv_bn_act(x, conv, bn, relu: bool = True, pool: bool = False, residual=None, res_sink=None, dx_sink=None,
-                w_amax=None, w_t=None):
+                w_amax=None, w_t=None, bn_link: bool = False):
     """``[maxpool2x2](act(bn(conv(x)) [+ residual]))`` for an ``nn.Conv2d`` / ``nn.BatchNorm2d`` pair.
 
     ``pool`` is the reference's ``MaxPool2d(kernel_size=2, stride=2)``; ``relu`` its
@@ -179,6 +231,8 @@ def conv_bn_act(x, conv, bn, relu: bool = True, pool: bool = False, residual=Non
     identity block into the data-gradient GEMM of the block's first conv instead of an autograd add.
     ``w_amax`` (f16x2 engine): ``conv.weight``'s entry of :func:`weight_amax`, else measured here.
     ``w_t``: ``conv.weight``'s W^T from :func:`weight_prep` (else backward transposes it).
+    ``bn_link``: the caller guarantees the result feeds exactly one op, the next ``conv_bn_act``
+    (a VGG chain); its backward then reduces this block's BN statistics for it (:class:`_BNLink`).
     """
     stride = conv.stride[0]
     pad = conv.padding[0]
@@ -206,6 +260,7 @@ def conv_bn_act(x, conv, bn, relu: bool = True, pool: bool = False, residual=Non
             dx_sink,
             w_amax if w_amax is not None else getattr(conv, "_cdp_wamax", None),
             w_t if w_t is not None else getattr(conv, "_cdp_wt", None),
+            bn_link,
         )
     y = F.conv2d(x, conv.weight, conv.bias, conv.stride, conv.padding)
     y = bn(y)

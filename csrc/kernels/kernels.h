@@ -136,6 +136,31 @@ int stem_wgrad_blocks(int N, int H, int W);
 void stem_wgrad_launch(const float* y, const float* gout, const float* stats, const float* sums, const float* x,
                        float* slab, int nblk, int N, int H, int W, int Cin, hipStream_t st);
 
+// bwd_fuse.hip: one launch that finishes a block's two gradient GEMMs' split-K slabs and starts the
+// previous block's BatchNorm backward (see the file header).
+struct BwdReduceArgs {
+  // job D: y[m][n] = sum_z d_slab[z][m][n] (+ d_addend), [d_M][d_Nout], d_Nout % 4 == 0
+  const float* d_slab;
+  float* d_y;
+  const float* d_addend;
+  int d_S, d_M, d_Nout;
+  // optional: BN-backward partials [ceil(d_M / rows_per_part)][d_Nout][bn_ps] of the BN whose
+  // (pooled) output d_y is the gradient of; bn_y = its saved conv output [N][bn_H][bn_W][d_Nout]
+  const float* bn_y;
+  const float* bn_stats;
+  float* bn_part;
+  int bn_H, bn_W, bn_pool, bn_relu, bn_ps;
+  // job W: w_dst[i] = sum_z w_slab[z][i] over w_n4 float4s
+  const float4* w_slab;
+  float4* w_dst;
+  int w_S;
+  long long w_n4;
+  // set by the launcher
+  int nbd, d_nbx, w_cb;
+};
+void bwd_reduce_launch(BwdReduceArgs a, hipStream_t st);
+int bwd_reduce_rows_per_part();
+
 // bn.hip
 int bn_bwd_grid(int N, int H, int W, int C, bool pool);
 void bn_finalize_launch(const float* part, int nparts, int rpp, int M, int C, const float* gamma, const float* beta,
@@ -165,9 +190,11 @@ void xent_bwd_launch(const float* logits, const long long* tgt, const float* gsc
 void sgd_launch(float* p, const float* g, float* buf, long long n, const float* lr_ptr, float lr, float momentum,
                 float dampening, float wd, float grad_scale, bool nesterov, bool first, bool maximize,
                 hipStream_t st);
+// nbatches > 0: batch offset idx_off + (counter % nbatches) * B; labels_out[b] = labels[idx[...]] when given
 void augment_launch(const unsigned char* imgs, const long long* idx, long long idx_off, int B, int H, int W, int C,
                     const float* mean, const float* inv_std, int pad, bool flip, const long long* counter,
-                    unsigned long long seed, float* out, hipStream_t st);
+                    unsigned long long seed, float* out, hipStream_t st, long long nbatches = 0,
+                    const long long* labels = nullptr, long long* labels_out = nullptr);
 void counter_inc_launch(long long* c, hipStream_t st);
 void wtrans_launch(const float* w, float* wt, int Co, int T, int Ci, hipStream_t st);
 // sub-filter transpose: wt[ci][a][b][co] = w[co][kh0 + 2a][kw0 + 2b][ci] (a < nkh, b < nkw)

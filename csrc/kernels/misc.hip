@@ -178,11 +178,17 @@ __global__ __launch_bounds__(256) void augment_kernel(const unsigned char* __res
                                                      int H, int W, int C, float m0, float m1, float m2, float is0,
                                                      float is1, float is2, int pad, int flip,
                                                      const long long* __restrict__ counter, unsigned long long seed,
-                                                     float* __restrict__ out) {
+                                                     float* __restrict__ out, long long nbatches,
+                                                     const long long* __restrict__ labels,
+                                                     long long* __restrict__ labels_out) {
   const int b = blockIdx.y;
   if (b >= B) return;
-  const long long src_i = idx ? idx[idx_off + b] : (idx_off + b);
   const unsigned long long ctr = counter ? (unsigned long long)counter[0] : 0ull;
+  // nbatches > 0: the batch offset into idx follows the step counter, so a replayed hipGraph walks
+  // the epoch order without a host-side index copy per step
+  const long long off = nbatches > 0 ? idx_off + (long long)(ctr % (unsigned long long)nbatches) * B : idx_off;
+  const long long src_i = idx ? idx[off + b] : (off + b);
+  if (labels_out && blockIdx.x == 0 && threadIdx.x == 0) labels_out[b] = labels[src_i];
   const unsigned long long r = splitmix64(seed ^ splitmix64(ctr * 0x100000001B3ull + (unsigned long long)b));
   const int span = 2 * pad + 1;
   const int oy = pad ? (int)(r % span) - pad : 0;
@@ -561,11 +567,13 @@ void sgd_launch(float* p, const float* g, float* buf, long long n, const float* 
 }
 void augment_launch(const unsigned char* imgs, const long long* idx, long long idx_off, int B, int H, int W, int C,
                     const float* mean, const float* inv_std, int pad, bool flip, const long long* counter,
-                    unsigned long long seed, float* out, hipStream_t st) {
+                    unsigned long long seed, float* out, hipStream_t st, long long nbatches,
+                    const long long* labels, long long* labels_out) {
   const int total = H * W * C;
   dim3 grid((total + 255) / 256, B);
   hipLaunchKernelGGL(augment_kernel, grid, dim3(256), 0, st, imgs, idx, idx_off, B, H, W, C, mean[0], mean[1],
-                     mean[2], inv_std[0], inv_std[1], inv_std[2], pad, flip ? 1 : 0, counter, seed, out);
+                     mean[2], inv_std[0], inv_std[1], inv_std[2], pad, flip ? 1 : 0, counter, seed, out, nbatches,
+                     labels, labels_out);
 }
 void counter_inc_launch(long long* c, hipStream_t st) {
   hipLaunchKernelGGL(counter_inc_kernel, dim3(1), dim3(1), 0, st, c);

@@ -39,7 +39,12 @@ PYBIND11_MODULE(_C, m) {
         py::arg("has_bias"), py::arg("zout") = py::none(), py::arg("training") = true, py::arg("dw_out") = py::none(),
         py::arg("db_out") = py::none(), py::arg("dgamma_out") = py::none(), py::arg("dbeta_out") = py::none(),
         py::arg("dx_addend") = py::none(), py::arg("x_amax") = py::none(), py::arg("w_amax") = py::none(),
-        py::arg("w_t") = py::none());
+        py::arg("w_t") = py::none(), py::arg("part_in") = py::none(), py::arg("prev_y") = py::none(),
+        py::arg("prev_stats") = py::none(), py::arg("prev_pool") = false, py::arg("prev_relu") = false,
+        py::arg("prev_ps") = 2,
+        "fused block backward; returns (dx, dw, db, dgamma, dbeta, dres, prev_part). prev_* describe the BN whose "
+        "output is x: its statistics reduction is then fused into this block's data-gradient reduction and returned "
+        "as prev_part (undefined when not fused), which that block's backward takes as part_in");
   m.def("weight_prep", &weight_prep, py::arg("weights"), py::arg("want_t"),
         "one launch per step: conv weights' |max| partials (f16x2; else empty) and W^T [Ci, KH*KW*Co] per weight "
         "with want_t (the data-gradient operand)");
@@ -49,7 +54,12 @@ PYBIND11_MODULE(_C, m) {
   m.def("xent_fwd", &xent_fwd, py::arg("logits"), py::arg("target"), py::arg("correct") = py::none());
   m.def("xent_bwd", &xent_bwd);
   m.def("sgd_step", &sgd_step);
-  m.def("augment", &augment);
+  m.def("augment", &augment, py::arg("images"), py::arg("indices"), py::arg("idx_offset"), py::arg("batch"),
+        py::arg("mean"), py::arg("std"), py::arg("pad"), py::arg("flip"), py::arg("counter"), py::arg("seed"),
+        py::arg("out") = py::none(), py::arg("nbatches") = 0, py::arg("labels") = py::none(),
+        py::arg("labels_out") = py::none(),
+        "gather + RandomCrop + flip + normalize one batch (NHWC fp32); nbatches > 0 takes the batch offset from "
+        "the step counter; labels_out receives the batch's labels");
   m.def("counter_inc", &counter_inc);
   m.def("stack_mean", &stack_mean);
   m.def("scale_", &scale_);

@@ -224,9 +224,33 @@ void conv_launch(const ConvGemmParams& p, int bm, int bn, bool dgrad, hipStream_
 // slabs) is 3-10x slower on MI355X -- cross-XCD visibility of the partials needs either a full L2
 // writeback/invalidate per workgroup or write-through stores, both far costlier than one extra
 // launch (docs/PERF.md).
+// Split-K reductions a block's backward defers into one bwd_reduce launch (bwd_fuse.hip): the
+// weight gradient's slab sum (w_*) and the data gradient's split-K reduction (d_*).
+struct DeferredReduce {
+  at::Tensor w_slab;
+  float* w_dst = nullptr;
+  int w_S = 0;
+  long long w_n = 0;
+  at::Tensor d_slab;
+  float* d_y = nullptr;
+  const float* d_addend = nullptr;
+  int d_S = 0, d_M = 0, d_Nout = 0;
+};
+
+bool bwd_fuse_enabled() {
+  static const bool on = [] {
+    const char* e = std::getenv("CDP_BWD_FUSE");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 // alloc_part(rows_per_part), when given, returns the BN partial buffer for that layout.
+// defer, when given, takes over a plain split-K reduction (no bias / BN partials / row scatter):
+// the GEMM is enqueued and the reduction left to the caller's bwd_reduce launch.
 int conv_gemm_splitk(ConvGemmParams p, const GemmPlan& g, bool dgrad, hipStream_t st, at::TensorOptions opts,
-                     std::vector<at::Tensor>& keep, const std::function<float*(int)>& alloc_part = nullptr) {
+                     std::vector<at::Tensor>& keep, const std::function<float*(int)>& alloc_part = nullptr,
+                     DeferredReduce* defer = nullptr) {
   p.splits = g.splits;
   if (g.splits == 1) {
     if (alloc_part) p.part = alloc_part(g.bm);
@@ -235,6 +259,18 @@ int conv_gemm_splitk(ConvGemmParams p, const GemmPlan& g, bool dgrad, hipStream_
   }
   at::Tensor slab = at::empty({g.splits, (long long)p.M, p.Nout}, opts);
   keep.push_back(slab);
+  if (defer && !alloc_part && !p.part && !p.bias && !p.rr.on && (p.Nout % 4) == 0) {
+    defer->d_slab = slab;
+    defer->d_y = p.y;
+    defer->d_addend = p.addend;
+    defer->d_S = g.splits;
+    defer->d_M = p.M;
+    defer->d_Nout = p.Nout;
+    p.y = slab.data_ptr<float>();
+    p.addend = nullptr;
+    conv_launch(p, g.bm, g.bn, dgrad, st);
+    return splitk_rows_per_part();
+  }
   float* y = p.y;
   const float* bias = p.bias;
   const float* addend = p.addend;
@@ -572,9 +608,10 @@ bool conv2d_dgrad_subpixel(const at::Tensor& dy, const at::Tensor& w, at::Tensor
 }
 
 // dX[N, C, H, W] from dY[N, Co, P, Q] and W[Co, C, KH, KW] (any stride / padding).
-at::Tensor conv2d_dgrad(const at::Tensor& dy_, const at::Tensor& w_, std::vector<int64_t> in_shape, int64_t stride,
-                        int64_t pad, const c10::optional<at::Tensor>& addend, const c10::optional<at::Tensor>& dy_amax,
-                        const c10::optional<at::Tensor>& w_amax, const c10::optional<at::Tensor>& w_t) {
+at::Tensor dgrad_impl(const at::Tensor& dy_, const at::Tensor& w_, std::vector<int64_t> in_shape, int64_t stride,
+                      int64_t pad, const c10::optional<at::Tensor>& addend, const c10::optional<at::Tensor>& dy_amax,
+                      const c10::optional<at::Tensor>& w_amax, const c10::optional<at::Tensor>& w_t,
+                      DeferredReduce* defer) {
   check_f32_cuda(dy_, "grad_output");
   check_f32_cuda(w_, "weight");
   const at::Tensor dy = nhwc(dy_);
@@ -621,8 +658,14 @@ at::Tensor conv2d_dgrad(const at::Tensor& dy_, const at::Tensor& w_, std::vector
   p.y = dx.data_ptr<float>();
   p.addend = addp;
   std::vector<at::Tensor> keep;
-  conv_gemm_splitk(p, g, true, st, opts, keep);
+  conv_gemm_splitk(p, g, true, st, opts, keep, nullptr, defer);
   return dx;
+}
+
+at::Tensor conv2d_dgrad(const at::Tensor& dy, const at::Tensor& w, std::vector<int64_t> in_shape, int64_t stride,
+                        int64_t pad, const c10::optional<at::Tensor>& addend, const c10::optional<at::Tensor>& dy_amax,
+                        const c10::optional<at::Tensor>& w_amax, const c10::optional<at::Tensor>& w_t) {
+  return dgrad_impl(dy, w, in_shape, stride, pad, addend, dy_amax, w_amax, w_t, nullptr);
 }
 
 // ---------------------------------------------------------------- conv weight gradient
@@ -635,10 +678,10 @@ at::Tensor conv2d_wgrad(const at::Tensor& dy_, const at::Tensor& x_, std::vector
 
 // keep_c >= 0: x carries zero-padded channels; only the first keep_c input channels of dW are
 // written (the strip is fused into the split-K slab reduction).
-at::Tensor conv2d_wgrad_keep(const at::Tensor& dy_, const at::Tensor& x_, std::vector<int64_t> w_shape,
-                             int64_t stride, int64_t pad, const c10::optional<at::Tensor>& out, bool accumulate,
-                             int64_t keep_c, const c10::optional<at::Tensor>& dy_amax,
-                             const c10::optional<at::Tensor>& x_amax) {
+at::Tensor wgrad_impl(const at::Tensor& dy_, const at::Tensor& x_, std::vector<int64_t> w_shape, int64_t stride,
+                      int64_t pad, const c10::optional<at::Tensor>& out, bool accumulate, int64_t keep_c,
+                      const c10::optional<at::Tensor>& dy_amax, const c10::optional<at::Tensor>& x_amax,
+                      DeferredReduce* defer) {
   check_f32_cuda(dy_, "grad_output");
   check_f32_cuda(x_, "input");
   const at::Tensor dy = nhwc(dy_);
@@ -678,10 +721,24 @@ at::Tensor conv2d_wgrad_keep(const at::Tensor& dy_, const at::Tensor& x_, std::v
     at::Tensor slab = at::empty({p.splits, Co, Kdim}, opts);
     p.out = slab.data_ptr<float>();
     wgrad_launch(p, wp.bm, wp.bn, x3_family() && x3_ok(p), st, split_planes());
-    slab_sum_strided_launch(slab.data_ptr<float>(), p.splits, (long long)Co * Kdim, C, Ckeep, dw.data_ptr<float>(),
-                            accumulate, st);
+    const long long n = (long long)Co * Kdim;
+    if (defer && !accumulate && Ckeep == C && (n % 4) == 0 &&
+        (reinterpret_cast<uintptr_t>(dw.data_ptr<float>()) & 15) == 0) {
+      defer->w_slab = slab;
+      defer->w_dst = dw.data_ptr<float>();
+      defer->w_S = p.splits;
+      defer->w_n = n;
+    } else {
+      slab_sum_strided_launch(slab.data_ptr<float>(), p.splits, n, C, Ckeep, dw.data_ptr<float>(), accumulate, st);
+    }
   }
   return dw;
+}
+
+at::Tensor conv2d_wgrad_keep(const at::Tensor& dy, const at::Tensor& x, std::vector<int64_t> w_shape, int64_t stride,
+                             int64_t pad, const c10::optional<at::Tensor>& out, bool accumulate, int64_t keep_c,
+                             const c10::optional<at::Tensor>& dy_amax, const c10::optional<at::Tensor>& x_amax) {
+  return wgrad_impl(dy, x, w_shape, stride, pad, out, accumulate, keep_c, dy_amax, x_amax, nullptr);
 }
 
 // ---------------------------------------------------------------- RGB stem (stem.hip)
@@ -812,7 +869,11 @@ std::vector<at::Tensor> conv_bn_act_bwd(const at::Tensor& gout_, const at::Tenso
                                         const c10::optional<at::Tensor>& dx_addend,
                                         const c10::optional<at::Tensor>& x_amax,
                                         const c10::optional<at::Tensor>& w_amax,
-                                        const c10::optional<at::Tensor>& w_t) {
+                                        const c10::optional<at::Tensor>& w_t,
+                                        const c10::optional<at::Tensor>& part_in,
+                                        const c10::optional<at::Tensor>& prev_y,
+                                        const c10::optional<at::Tensor>& prev_stats, bool prev_pool, bool prev_relu,
+                                        int64_t prev_ps) {
   check_f32_cuda(gout_, "grad_output");
   const at::Tensor gout = nhwc(gout_);
   const int N = y.size(0), C = y.size(1), H = y.size(2), W = y.size(3);
@@ -828,9 +889,20 @@ std::vector<at::Tensor> conv_bn_act_bwd(const at::Tensor& gout_, const at::Tenso
   const bool odd_pool = pool && ((H & 1) || (W & 1));
   const bool fused_db = has_bias && !odd_pool;
   const int ps = fused_db && training ? 3 : 2;
-  at::Tensor part = at::empty({nblk, C, ps}, opts);
-  bn_bwd_reduce_launch(y.data_ptr<float>(), gout.data_ptr<float>(), stats.data_ptr<float>(), part.data_ptr<float>(),
-                       nblk, N, H, W, C, pool, relu, zout.defined() ? zout.data_ptr<float>() : nullptr, st, ps == 3);
+  // the statistics reduction: from the consumer block's fused backward reduction when it made it
+  // (part_in, see prev_* below), else a launch of its own
+  at::Tensor part;
+  if (part_in.has_value() && part_in->defined()) {
+    part = *part_in;
+    TORCH_CHECK(part.dim() == 3 && part.size(1) == C && part.size(2) == ps && !zout.defined(),
+                "conv_bn_act_bwd: part_in must be [nparts, C, ", ps, "] (no residual)");
+  } else {
+    part = at::empty({nblk, C, ps}, opts);
+    bn_bwd_reduce_launch(y.data_ptr<float>(), gout.data_ptr<float>(), stats.data_ptr<float>(),
+                         part.data_ptr<float>(), nblk, N, H, W, C, pool, relu,
+                         zout.defined() ? zout.data_ptr<float>() : nullptr, st, ps == 3);
+  }
+  const int nparts = (int)part.size(0);
   at::Tensor sums = at::empty({2, C}, opts);
   // gradients go straight into the caller's slots (flat-arena views) when provided
   auto slot = [&](const c10::optional<at::Tensor>& o, std::initializer_list<int64_t> shape, bool cl) {
@@ -842,7 +914,7 @@ std::vector<at::Tensor> conv_bn_act_bwd(const at::Tensor& gout_, const at::Tenso
   if (has_bias) db = slot(db_out, {C}, false);
   // eval-mode BatchNorm is a fixed affine map: dy = scale * dz (no batch-statistics terms)
   const int dbmode = fused_db ? (training ? 1 : 2) : 0;
-  chan_finalize_launch(part.data_ptr<float>(), nblk, C, sums.data_ptr<float>(), dbeta.data_ptr<float>(),
+  chan_finalize_launch(part.data_ptr<float>(), nparts, C, sums.data_ptr<float>(), dbeta.data_ptr<float>(),
                        dgamma.data_ptr<float>(), false, st, ps, fused_db ? db.data_ptr<float>() : nullptr,
                        stats.data_ptr<float>() + 2 * C, (long long)N * H * W, dbmode);
   if (!training && dbmode != 2) sums.zero_();
@@ -862,7 +934,7 @@ std::vector<at::Tensor> conv_bn_act_bwd(const at::Tensor& gout_, const at::Tenso
                         : at::empty({C, cin, w.size(2), w.size(3)}, opts.memory_format(at::MemoryFormat::ChannelsLast));
     TORCH_CHECK(dw.is_contiguous(at::MemoryFormat::ChannelsLast), "stem dW slot must be channels_last");
     slab_sum_strided_launch(slab.data_ptr<float>(), nb, (long long)C * 36, 4, cin, dw.data_ptr<float>(), false, st);
-    return {at::Tensor(), dw, db, dgamma, dbeta, at::Tensor()};
+    return {at::Tensor(), dw, db, dgamma, dbeta, at::Tensor(), at::Tensor()};
   }
   at::Tensor dy = at::empty({N, C, H, W}, opts.memory_format(at::MemoryFormat::ChannelsLast));
   at::Tensor dbpart;
@@ -886,12 +958,16 @@ std::vector<at::Tensor> conv_bn_act_bwd(const at::Tensor& gout_, const at::Tenso
   // stream (fork/join by events, so it is also a parallel branch under hipGraph capture).
   at::Tensor dx, dw;
   const bool overlap = need_dx && conc_enabled();
+  // both GEMMs' split-K reductions (and, given prev_*, the previous block's BN statistics
+  // reduction) in one bwd_reduce launch after the two GEMMs (bwd_fuse.hip)
+  DeferredReduce dr;
+  DeferredReduce* defer = (bwd_fuse_enabled() && !overlap && !padc) ? &dr : nullptr;
   c10::hip::HIPStream side = overlap ? side_stream() : c10::hip::getCurrentHIPStream();
   if (overlap) fork_to(side);
   {
     c10::hip::HIPStreamGuard guard(side);
-    dw = conv2d_wgrad_keep(dy, x, {w.size(0), x.size(1), w.size(2), w.size(3)}, stride, pad, dw_out, false,
-                           padc ? w.size(1) : -1, dya, x_amax);
+    dw = wgrad_impl(dy, x, {w.size(0), x.size(1), w.size(2), w.size(3)}, stride, pad, dw_out, false,
+                    padc ? w.size(1) : -1, dya, x_amax, defer);
   }
   if (overlap && !(dw_out.has_value() && dw_out->defined()))  // allocated on the side stream, consumed on main
     c10::hip::HIPCachingAllocator::recordStream(dw.storage().data_ptr(), c10::hip::getCurrentHIPStream());
@@ -903,12 +979,52 @@ std::vector<at::Tensor> conv_bn_act_bwd(const at::Tensor& gout_, const at::Tenso
       if (dx_addend.has_value() && dx_addend->defined()) dx.add_(*dx_addend);
     } else {
       // residual-branch gradient (dx_addend) is accumulated by the data-gradient GEMM's epilogue
-      dx = conv2d_dgrad(dy, w, {x.size(0), x.size(1), x.size(2), x.size(3)}, stride, pad, dx_addend, dya, w_amax,
-                        w_t);
+      dx = dgrad_impl(dy, w, {x.size(0), x.size(1), x.size(2), x.size(3)}, stride, pad, dx_addend, dya, w_amax, w_t,
+                      defer);
     }
   }
+  at::Tensor prev_part;
+  if (dr.w_slab.defined() || dr.d_slab.defined()) {
+    BwdReduceArgs a{};
+    if (dr.d_slab.defined()) {
+      a.d_slab = dr.d_slab.data_ptr<float>();
+      a.d_y = dr.d_y;
+      a.d_addend = dr.d_addend;
+      a.d_S = dr.d_S;
+      a.d_M = dr.d_M;
+      a.d_Nout = dr.d_Nout;
+      // the previous block's BN statistics reduction over this dX (its gradient at the BN output)
+      if (prev_y.has_value() && prev_y->defined() && prev_stats.has_value() && prev_stats->defined() &&
+          !(dx_addend.has_value() && dx_addend->defined())) {
+        const at::Tensor py = nhwc(*prev_y);
+        const int pH = py.size(2), pW = py.size(3);
+        TORCH_CHECK(py.size(0) == x.size(0) && py.size(1) == x.size(1) &&
+                        (prev_pool ? (pH / 2 == x.size(2) && pW / 2 == x.size(3))
+                                   : (pH == x.size(2) && pW == x.size(3))) &&
+                        (prev_ps == 2 || prev_ps == 3) && prev_stats->numel() == 4 * py.size(1),
+                    "conv_bn_act_bwd: prev_y / prev_stats do not describe the BN that produced x");
+        prev_part = at::empty({(dr.d_M + bwd_reduce_rows_per_part() - 1) / bwd_reduce_rows_per_part(), x.size(1),
+                               prev_ps}, opts);
+        a.bn_y = py.data_ptr<float>();
+        a.bn_stats = prev_stats->data_ptr<float>();
+        a.bn_part = prev_part.data_ptr<float>();
+        a.bn_H = pH;
+        a.bn_W = pW;
+        a.bn_pool = prev_pool ? 1 : 0;
+        a.bn_relu = prev_relu ? 1 : 0;
+        a.bn_ps = (int)prev_ps;
+      }
+    }
+    if (dr.w_slab.defined()) {
+      a.w_slab = reinterpret_cast<const float4*>(dr.w_slab.data_ptr<float>());
+      a.w_dst = reinterpret_cast<float4*>(dr.w_dst);
+      a.w_S = dr.w_S;
+      a.w_n4 = dr.w_n / 4;
+    }
+    bwd_reduce_launch(a, st);
+  }
   if (overlap) join_from(side);
-  return {dx, dw, db, dgamma, dbeta, dres};
+  return {dx, dw, db, dgamma, dbeta, dres, prev_part};
 }
 
 // ---------------------------------------------------------------- linear
@@ -1044,7 +1160,9 @@ void sgd_step(at::Tensor p, const at::Tensor& g, c10::optional<at::Tensor> buf, 
 // ---------------------------------------------------------------- data augmentation
 at::Tensor augment(const at::Tensor& images, const c10::optional<at::Tensor>& indices, int64_t idx_offset, int64_t batch,
                    std::vector<double> mean, std::vector<double> std_, int64_t pad, bool flip,
-                   const c10::optional<at::Tensor>& counter, int64_t seed, c10::optional<at::Tensor> out) {
+                   const c10::optional<at::Tensor>& counter, int64_t seed, c10::optional<at::Tensor> out,
+                   int64_t nbatches, const c10::optional<at::Tensor>& labels,
+                   const c10::optional<at::Tensor>& labels_out) {
   TORCH_CHECK(images.is_cuda() && images.scalar_type() == at::kByte && images.dim() == 4,
               "images must be uint8 [N, H, W, C] on the GPU");
   const int H = images.size(1), W = images.size(2), C = images.size(3);
@@ -1061,8 +1179,18 @@ at::Tensor augment(const at::Tensor& images, const c10::optional<at::Tensor>& in
   if (indices.has_value() && indices->defined()) ip = reinterpret_cast<const long long*>(indices->data_ptr<int64_t>());
   const long long* cp = nullptr;
   if (counter.has_value() && counter->defined()) cp = reinterpret_cast<const long long*>(counter->data_ptr<int64_t>());
+  TORCH_CHECK(nbatches == 0 || cp, "counter-driven batch offsets need the counter");
+  const long long* lp = nullptr;
+  long long* lo = nullptr;
+  if (labels_out.has_value() && labels_out->defined()) {
+    TORCH_CHECK(labels.has_value() && labels->defined() && labels->scalar_type() == at::kLong &&
+                    labels_out->scalar_type() == at::kLong && labels_out->numel() >= batch,
+                "labels / labels_out must be int64, labels_out holding the batch");
+    lp = reinterpret_cast<const long long*>(labels->data_ptr<int64_t>());
+    lo = reinterpret_cast<long long*>(labels_out->data_ptr<int64_t>());
+  }
   augment_launch(images.data_ptr<uint8_t>(), ip, idx_offset, (int)batch, H, W, C, m, is, (int)pad, flip, cp,
-                 (unsigned long long)seed, o.data_ptr<float>(), cur_stream());
+                 (unsigned long long)seed, o.data_ptr<float>(), cur_stream(), nbatches, lp, lo);
   return o;
 }
 

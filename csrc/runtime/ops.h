@@ -47,7 +47,11 @@ std::vector<at::Tensor> conv_bn_act_bwd(const at::Tensor& gout, const at::Tensor
                                         const c10::optional<at::Tensor>& dx_addend,
                                         const c10::optional<at::Tensor>& x_amax = c10::nullopt,
                                         const c10::optional<at::Tensor>& w_amax = c10::nullopt,
-                                        const c10::optional<at::Tensor>& w_t = c10::nullopt);
+                                        const c10::optional<at::Tensor>& w_t = c10::nullopt,
+                                        const c10::optional<at::Tensor>& part_in = c10::nullopt,
+                                        const c10::optional<at::Tensor>& prev_y = c10::nullopt,
+                                        const c10::optional<at::Tensor>& prev_stats = c10::nullopt,
+                                        bool prev_pool = false, bool prev_relu = false, int64_t prev_ps = 2);
 at::Tensor linear_fwd(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tensor>& b);
 std::vector<at::Tensor> linear_bwd(const at::Tensor& gy, const at::Tensor& x, const at::Tensor& w, bool need_dx,
                                    bool has_bias, const c10::optional<at::Tensor>& dw_out,
@@ -59,7 +63,9 @@ void sgd_step(at::Tensor p, const at::Tensor& g, c10::optional<at::Tensor> buf, 
               bool maximize);
 at::Tensor augment(const at::Tensor& images, const c10::optional<at::Tensor>& indices, int64_t idx_offset, int64_t batch,
                    std::vector<double> mean, std::vector<double> std_, int64_t pad, bool flip,
-                   const c10::optional<at::Tensor>& counter, int64_t seed, c10::optional<at::Tensor> out);
+                   const c10::optional<at::Tensor>& counter, int64_t seed, c10::optional<at::Tensor> out,
+                   int64_t nbatches = 0, const c10::optional<at::Tensor>& labels = c10::nullopt,
+                   const c10::optional<at::Tensor>& labels_out = c10::nullopt);
 void counter_inc(at::Tensor c);
 void stack_mean(const std::vector<at::Tensor>& srcs, at::Tensor dst);
 void scale_(at::Tensor x, double a);

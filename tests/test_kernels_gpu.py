@@ -276,6 +276,40 @@ def test_augment_normalize_and_determinism():
     assert a.shape == (16, 3, 32, 32) and a.is_contiguous(memory_format=torch.channels_last)
 
 
+def test_augment_counter_driven_batches_in_graph():
+    """nbatches > 0: one captured graph walks the epoch order by the on-device step counter, and the
+    fused label gather matches labels[idx]."""
+    from cs744_distributed_data_parallel_amd.data import DeviceLoader, synthetic_cifar10
+
+    ds = synthetic_cifar10(64, device="cuda")
+    ld = DeviceLoader(ds, 16, train=False)
+    order = torch.randperm(64, generator=torch.Generator().manual_seed(1)).cuda()
+    xs = torch.empty(16, 3, 32, 32, device="cuda").contiguous(memory_format=torch.channels_last)
+    ys = torch.empty(16, dtype=torch.int64, device="cuda")
+
+    def body():
+        x, y = ld.batch(order, 0, 16, out=xs, nbatches=4)
+        ys.copy_(y)
+
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        body()  # step 0
+    torch.cuda.current_stream().wait_stream(s)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        body()  # captured (not run): the first replay reads counter 1, each replay advances it
+    mean = torch.tensor(ds.mean, device="cuda").view(1, 3, 1, 1)
+    std = torch.tensor(ds.std, device="cuda").view(1, 3, 1, 1)
+    for step in range(1, 7):
+        g.replay()
+        torch.cuda.synchronize()
+        sel = order[(step % 4) * 16:(step % 4) * 16 + 16]
+        ref = (ds.images[sel].permute(0, 3, 1, 2).float() / 255.0 - mean) / std
+        assert torch.allclose(xs, ref, atol=1e-5), step
+        assert torch.equal(ys, ds.labels[sel]), step
+
+
 def test_pooling_ops():
     from cs744_distributed_data_parallel_amd.ops import functional as CF
 

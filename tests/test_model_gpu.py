@@ -64,6 +64,45 @@ def test_vgg11_training_steps_match_reference(monkeypatch):
     assert e_nat < max(3 * e_t32, 1e-4), (e_nat, e_t32)
 
 
+def test_vgg11_bn_link_backward_matches_unlinked(monkeypatch):
+    """The chained backward (block L+1's data-gradient reduction also reduces block L's BN
+    statistics, bwd_fuse.hip) gives the gradients of the unchained one, and is really taken."""
+    import cs744_distributed_data_parallel_amd as cdp
+    from cs744_distributed_data_parallel_amd.ops import functional as CF
+
+    torch.manual_seed(0)
+    model = cdp.VGG11().cuda()
+    x = torch.randn(64, 3, 32, 32, device="cuda").contiguous(memory_format=torch.channels_last)
+    t = torch.randint(0, 10, (64,), device="cuda")
+    crit = cdp.CrossEntropyLoss()
+
+    def grads():
+        model.zero_grad(set_to_none=True)
+        crit(model(x), t).backward()
+        torch.cuda.synchronize()
+        return [p.grad.detach().clone() for p in model.parameters()]
+
+    n0 = CF.LINK_HANDOFFS[0]
+    g_link = grads()
+    assert CF.LINK_HANDOFFS[0] - n0 >= 5  # VGG-11: 7 chained blocks, most with split-K dgrads
+    monkeypatch.setenv("CDP_BWD_FUSE", "0")  # no hand-off: every block reduces its own statistics
+    n1 = CF.LINK_HANDOFFS[0]
+    g_ref = grads()
+    assert CF.LINK_HANDOFFS[0] == n1
+    named = dict(zip([n for n, _ in model.named_parameters()], zip(g_link, g_ref)))
+    for name, (a, b) in named.items():
+        conv_bias = name.startswith("layers.") and name.endswith(".bias") and \
+            isinstance(model.layers[int(name.split(".")[1])], torch.nn.Conv2d)
+        if conv_bias:
+            # a conv bias right before training-mode BN has zero gradient analytically: both are
+            # rounding noise, bounded against the BN shift's gradient
+            beta = named[name.split(".")[0] + "." + str(int(name.split(".")[1]) + 1) + ".bias"][1]
+            assert (a - b).norm() <= 1e-5 * beta.norm(), name
+            continue
+        err = ((a - b).norm() / b.norm().clamp_min(1e-30)).item()
+        assert err < 1e-5, (name, err)
+
+
 def test_vgg11_eval_matches_reference():
     import cs744_distributed_data_parallel_amd as cdp
 
