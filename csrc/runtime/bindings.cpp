@@ -31,7 +31,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("conv_bn_act_fwd", &conv_bn_act_fwd, py::arg("x"), py::arg("w"), py::arg("b"), py::arg("gamma"),
         py::arg("beta"), py::arg("running_mean"), py::arg("running_var"), py::arg("num_batches_tracked"),
         py::arg("momentum"), py::arg("eps"), py::arg("training"), py::arg("stride"), py::arg("pad"), py::arg("pool"),
-        py::arg("relu"), py::arg("residual"), py::arg("x_amax") = py::none(), py::arg("w_amax") = py::none());
+        py::arg("relu"), py::arg("residual"), py::arg("x_amax") = py::none(), py::arg("w_amax") = py::none(),
+        py::arg("stem_recompute") = false);
   m.def("multi_amax", &multi_amax, py::arg("tensors"),
         "f16x2 engine: partial |max| values of many tensors in one launch (empty list for other engines)");
   m.def("conv_bn_act_bwd", &conv_bn_act_bwd, py::arg("gout"), py::arg("x"), py::arg("w"), py::arg("y"),
@@ -41,7 +42,7 @@ PYBIND11_MODULE(_C, m) {
         py::arg("dx_addend") = py::none(), py::arg("x_amax") = py::none(), py::arg("w_amax") = py::none(),
         py::arg("w_t") = py::none(), py::arg("part_in") = py::none(), py::arg("prev_y") = py::none(),
         py::arg("prev_stats") = py::none(), py::arg("prev_pool") = false, py::arg("prev_relu") = false,
-        py::arg("prev_ps") = 2,
+        py::arg("prev_ps") = 2, py::arg("bias") = py::none(),
         "fused block backward; returns (dx, dw, db, dgamma, dbeta, dres, prev_part). prev_* describe the BN whose "
         "output is x: its statistics reduction is then fused into this block's data-gradient reduction and returned "
         "as prev_part (undefined when not fused), which that block's backward takes as part_in");

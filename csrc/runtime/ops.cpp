@@ -757,7 +757,7 @@ std::vector<at::Tensor> stem_bn_act_fwd(const at::Tensor& x_, const at::Tensor& 
                                         const c10::optional<at::Tensor>& running_mean,
                                         const c10::optional<at::Tensor>& running_var,
                                         const c10::optional<at::Tensor>& num_batches_tracked, double momentum,
-                                        double eps, bool pool, bool relu) {
+                                        double eps, bool pool, bool relu, bool recompute) {
   check_f32_cuda(x_, "x");
   check_f32_cuda(w_, "weight");
   const at::Tensor x = nhwc(x_), w = nhwc(w_);
@@ -765,12 +765,14 @@ std::vector<at::Tensor> stem_bn_act_fwd(const at::Tensor& x_, const at::Tensor& 
   TORCH_CHECK(w.size(1) == Cin, "stem weight in-channels mismatch");
   auto opts = x.options();
   hipStream_t st = cur_stream();
-  at::Tensor y = at::empty({N, Co, H, W}, opts.memory_format(at::MemoryFormat::ChannelsLast));
+  // recompute mode: y is never stored; the activation pass and the backward rebuild it from x
+  const bool rc = recompute && pool && relu && stem_recompute_ok(N, H, W);
+  at::Tensor y = rc ? at::Tensor() : at::empty({N, Co, H, W}, opts.memory_format(at::MemoryFormat::ChannelsLast));
   const long long M = (long long)N * H * W;
   const int nparts = (int)((M + 255) / 256);
   at::Tensor part = at::empty({nparts, Co, 2}, opts);
-  stem_fwd_launch(x.data_ptr<float>(), w.data_ptr<float>(), fptr(b), y.data_ptr<float>(), part.data_ptr<float>(), N,
-                  H, W, Cin, Co, st);
+  stem_fwd_launch(x.data_ptr<float>(), w.data_ptr<float>(), fptr(b), rc ? nullptr : y.data_ptr<float>(),
+                  part.data_ptr<float>(), N, H, W, Cin, Co, st);
   at::Tensor stats = at::empty({4, Co}, opts);
   long long* nbt = nullptr;
   if (num_batches_tracked.has_value() && num_batches_tracked->defined())
@@ -781,9 +783,17 @@ std::vector<at::Tensor> stem_bn_act_fwd(const at::Tensor& x_, const at::Tensor& 
   at::Tensor out = at::empty({N, Co, pool ? H / 2 : H, pool ? W / 2 : W},
                              opts.memory_format(at::MemoryFormat::ChannelsLast));
   at::Tensor out_amax;
-  if (f16x2_mode()) out_amax = at::empty({bn_act_grid(N, H, W, Co, pool)}, opts);
-  bn_act_fwd_launch(y.data_ptr<float>(), stats.data_ptr<float>(), nullptr, out.data_ptr<float>(), N, H, W, Co, pool,
-                    relu, st, out_amax.defined() ? out_amax.data_ptr<float>() : nullptr);
+  if (rc) {
+    if (f16x2_mode()) out_amax = at::empty({M / 256}, opts);
+    stem_act_launch(x.data_ptr<float>(), w.data_ptr<float>(), fptr(b), stats.data_ptr<float>(), out.data_ptr<float>(),
+                    out_amax.defined() ? out_amax.data_ptr<float>() : nullptr, N, H, W, Cin, st);
+    // y's shape without storage (stride 0): conv_bn_act_bwd takes this as "recompute from x"
+    y = at::empty({1}, opts).expand({N, Co, H, W});
+  } else {
+    if (f16x2_mode()) out_amax = at::empty({bn_act_grid(N, H, W, Co, pool)}, opts);
+    bn_act_fwd_launch(y.data_ptr<float>(), stats.data_ptr<float>(), nullptr, out.data_ptr<float>(), N, H, W, Co, pool,
+                      relu, st, out_amax.defined() ? out_amax.data_ptr<float>() : nullptr);
+  }
   return {out, y, stats, x, out_amax, at::Tensor(), at::Tensor()};
 }
 
@@ -799,13 +809,14 @@ std::vector<at::Tensor> conv_bn_act_fwd(const at::Tensor& x, const at::Tensor& w
                                         double eps, bool training, int64_t stride, int64_t pad, bool pool, bool relu,
                                         const c10::optional<at::Tensor>& residual,
                                         const c10::optional<at::Tensor>& x_amax,
-                                        const c10::optional<at::Tensor>& w_amax) {
+                                        const c10::optional<at::Tensor>& w_amax, bool stem_recompute) {
   // RGB stem (3x3 / stride 1 / pad 1, Cin <= 4, training BN): one exact-fp32 MFMA kernel reading
-  // the raw NHWC input, no channel padding, no operand scales (stem.hip)
+  // the raw NHWC input, no channel padding, no operand scales (stem.hip); stem_recompute (the
+  // caller needs no input gradient): y is rebuilt from x instead of stored
   if (stem_enabled() && stem_ok((int)x.size(1), (int)w.size(2), (int)w.size(3), stride, pad, (int)w.size(0)) &&
       training && !(residual.has_value() && residual->defined()))
     return stem_bn_act_fwd(x, w, b, gamma, beta, running_mean, running_var, num_batches_tracked, momentum, eps, pool,
-                           relu);
+                           relu, stem_recompute);
   // other stems: zero-pad 3 -> 4 channels so the float4 gather path runs (the padded input is what
   // backward needs, so it is returned for saving)
   const bool padc = (x.size(1) % 4) != 0;
@@ -873,12 +884,48 @@ std::vector<at::Tensor> conv_bn_act_bwd(const at::Tensor& gout_, const at::Tenso
                                         const c10::optional<at::Tensor>& part_in,
                                         const c10::optional<at::Tensor>& prev_y,
                                         const c10::optional<at::Tensor>& prev_stats, bool prev_pool, bool prev_relu,
-                                        int64_t prev_ps) {
+                                        int64_t prev_ps, const c10::optional<at::Tensor>& bias) {
   check_f32_cuda(gout_, "grad_output");
   const at::Tensor gout = nhwc(gout_);
   const int N = y.size(0), C = y.size(1), H = y.size(2), W = y.size(3);
   auto opts = y.options();
   hipStream_t st = cur_stream();
+  auto slot = [&](const c10::optional<at::Tensor>& o, std::initializer_list<int64_t> shape, bool cl) {
+    if (o.has_value() && o->defined()) return *o;
+    return cl ? at::empty(shape, opts.memory_format(at::MemoryFormat::ChannelsLast)) : at::empty(shape, opts);
+  };
+  if (y.dim() == 4 && y.stride(0) == 0) {
+    // RGB stem in recompute mode (stem_bn_act_fwd): y is rebuilt from x by the statistics pass and
+    // by the weight-gradient pass; no input gradient
+    const at::Tensor xin = nhwc(x), win = nhwc(w);
+    const int cin = (int)xin.size(1);
+    TORCH_CHECK(!need_dx && training && pool && relu && !(zout_.has_value() && zout_->defined()) && C == 64 &&
+                    stem_ok(cin, (int)w.size(2), (int)w.size(3), stride, pad, C) && stem_recompute_ok(N, H, W) &&
+                    !(part_in.has_value() && part_in->defined()) && (has_bias == (bias.has_value() && bias->defined())),
+                "conv_bn_act_bwd: recompute-mode stem backward with an unsupported configuration");
+    const float* bp = has_bias ? bias->data_ptr<float>() : nullptr;
+    const int ps = has_bias ? 3 : 2;
+    const int nparts = stem_bnstat_parts(N, H, W);
+    at::Tensor part = at::empty({nparts, C, ps}, opts);
+    stem_bnstat_launch(xin.data_ptr<float>(), win.data_ptr<float>(), bp, gout.data_ptr<float>(),
+                       stats.data_ptr<float>(), part.data_ptr<float>(), ps, N, H, W, cin, st);
+    at::Tensor sums = at::empty({2, C}, opts);
+    at::Tensor dgamma = slot(dgamma_out, {C}, false), dbeta = slot(dbeta_out, {C}, false);
+    at::Tensor db;
+    if (has_bias) db = slot(db_out, {C}, false);
+    chan_finalize_launch(part.data_ptr<float>(), nparts, C, sums.data_ptr<float>(), dbeta.data_ptr<float>(),
+                         dgamma.data_ptr<float>(), false, st, ps, has_bias ? db.data_ptr<float>() : nullptr,
+                         stats.data_ptr<float>() + 2 * C, (long long)N * H * W, has_bias ? 1 : 0);
+    const int nb = stem_wgrad_rc_blocks(N, H, W);
+    at::Tensor slab = at::empty({nb, C, 36}, opts);
+    stem_wgrad_rc_launch(xin.data_ptr<float>(), win.data_ptr<float>(), bp, gout.data_ptr<float>(),
+                         stats.data_ptr<float>(), sums.data_ptr<float>(), slab.data_ptr<float>(), nb, N, H, W, cin,
+                         st);
+    at::Tensor dw = slot(dw_out, {C, cin, w.size(2), w.size(3)}, true);
+    TORCH_CHECK(dw.is_contiguous(at::MemoryFormat::ChannelsLast), "stem dW slot must be channels_last");
+    slab_sum_strided_launch(slab.data_ptr<float>(), nb, (long long)C * 36, 4, cin, dw.data_ptr<float>(), false, st);
+    return {at::Tensor(), dw, db, dgamma, dbeta, at::Tensor(), at::Tensor()};
+  }
   at::Tensor zout;
   if (zout_.has_value() && zout_->defined()) zout = nhwc(*zout_);
   const int nblk = bn_bwd_grid(N, H, W, C, pool);
@@ -905,10 +952,6 @@ std::vector<at::Tensor> conv_bn_act_bwd(const at::Tensor& gout_, const at::Tenso
   const int nparts = (int)part.size(0);
   at::Tensor sums = at::empty({2, C}, opts);
   // gradients go straight into the caller's slots (flat-arena views) when provided
-  auto slot = [&](const c10::optional<at::Tensor>& o, std::initializer_list<int64_t> shape, bool cl) {
-    if (o.has_value() && o->defined()) return *o;
-    return cl ? at::empty(shape, opts.memory_format(at::MemoryFormat::ChannelsLast)) : at::empty(shape, opts);
-  };
   at::Tensor dgamma = slot(dgamma_out, {C}, false), dbeta = slot(dbeta_out, {C}, false);
   at::Tensor db;
   if (has_bias) db = slot(db_out, {C}, false);

@@ -33,7 +33,8 @@ std::vector<at::Tensor> conv_bn_act_fwd(const at::Tensor& x, const at::Tensor& w
                                         double eps, bool training, int64_t stride, int64_t pad, bool pool, bool relu,
                                         const c10::optional<at::Tensor>& residual,
                                         const c10::optional<at::Tensor>& x_amax = c10::nullopt,
-                                        const c10::optional<at::Tensor>& w_amax = c10::nullopt);
+                                        const c10::optional<at::Tensor>& w_amax = c10::nullopt,
+                                        bool stem_recompute = false);
 std::vector<at::Tensor> multi_amax(const std::vector<at::Tensor>& ts);
 std::vector<std::vector<at::Tensor>> weight_prep(const std::vector<at::Tensor>& ts, const std::vector<bool>& want_t);
 std::vector<at::Tensor> conv_bn_act_bwd(const at::Tensor& gout, const at::Tensor& x, const at::Tensor& w,
@@ -51,7 +52,8 @@ std::vector<at::Tensor> conv_bn_act_bwd(const at::Tensor& gout, const at::Tensor
                                         const c10::optional<at::Tensor>& part_in = c10::nullopt,
                                         const c10::optional<at::Tensor>& prev_y = c10::nullopt,
                                         const c10::optional<at::Tensor>& prev_stats = c10::nullopt,
-                                        bool prev_pool = false, bool prev_relu = false, int64_t prev_ps = 2);
+                                        bool prev_pool = false, bool prev_relu = false, int64_t prev_ps = 2,
+                                        const c10::optional<at::Tensor>& bias = c10::nullopt);
 at::Tensor linear_fwd(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tensor>& b);
 std::vector<at::Tensor> linear_bwd(const at::Tensor& gy, const at::Tensor& x, const at::Tensor& w, bool need_dx,
                                    bool has_bias, const c10::optional<at::Tensor>& dw_out,

@@ -103,6 +103,41 @@ def test_vgg11_bn_link_backward_matches_unlinked(monkeypatch):
         assert err < 1e-5, (name, err)
 
 
+def test_vgg11_stem_recompute_matches_stored(monkeypatch):
+    """Recompute-mode stem (layer 0's conv output rebuilt from x in the activation pass and both
+    backward passes, never stored): the forward is bitwise the stored path's, the layer-0 gradients
+    agree to reduction-order rounding, every other gradient is bitwise equal."""
+    import cs744_distributed_data_parallel_amd as cdp
+
+    torch.manual_seed(0)
+    model = cdp.VGG11().cuda()
+    x = torch.randn(64, 3, 32, 32, device="cuda").contiguous(memory_format=torch.channels_last)
+    t = torch.randint(0, 10, (64,), device="cuda")
+    crit = cdp.CrossEntropyLoss()
+
+    def run():
+        model.zero_grad(set_to_none=True)
+        loss = crit(model(x), t)
+        loss.backward()
+        torch.cuda.synchronize()
+        return loss.detach().clone(), [p.grad.detach().clone() for p in model.parameters()]
+
+    monkeypatch.setenv("CDP_STEM_RECOMPUTE", "1")
+    l_rc, g_rc = run()
+    monkeypatch.setenv("CDP_STEM_RECOMPUTE", "0")
+    l_st, g_st = run()
+    assert torch.equal(l_rc, l_st)
+    for (name, _), a, b in zip(model.named_parameters(), g_rc, g_st):
+        if name.startswith("layers.0.") or name.startswith("layers.1."):
+            if name == "layers.0.bias":  # analytically zero before training-mode BN: rounding noise
+                assert (a - b).norm() <= 1e-5 * g_st[3].norm()
+                continue
+            err = ((a - b).norm() / b.norm()).item()
+            assert err < 1e-5, (name, err)
+        else:
+            assert torch.equal(a, b), name
+
+
 def test_vgg11_eval_matches_reference():
     import cs744_distributed_data_parallel_amd as cdp
 
