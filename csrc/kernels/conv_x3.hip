@@ -154,11 +154,13 @@ conv_x3_kernel(ConvGemmParams p) {
     b_off[i] = n < p.Nout ? (unsigned)(mul24(n, p.Kdim) + kq) << ES : kOOB;
   }
 
-  // f16x2: power-of-two operand scales from the producers' partial maxima (wave-uniform)
+  // f16x2: power-of-two operand scales from the producers' partial maxima (wave-uniform); the
+  // partial loads go out first and are waited for after the first tiles' loads are issued
   float sa = 1.f, sb = 1.f;
+  float amx_a[NP == 2 ? kAmaxK : 1], amx_b[NP == 2 ? kAmaxK : 1];
   if constexpr (NP == 2) {
-    sa = amax_scale(p.amax_a, p.amax_na);
-    sb = amax_scale(p.amax_b, p.amax_nb);
+    amax_issue(p.amax_a, p.amax_na, amx_a);
+    amax_issue(p.amax_b, p.amax_nb, amx_b);
   }
 
   // byte offset of A row i at filter tap (kh, kw), channel offset c (relative to kq); OOB if padded
@@ -463,6 +465,10 @@ conv_x3_kernel(ConvGemmParams p) {
   if (kt_begin < kt_end) {
     load_tile(kt_begin, va0, vb0, true);
     load_tile(kt_begin + 1, va1, vb1, kt_begin + 1 < kt_end);
+    if constexpr (NP == 2) {
+      sa = amax_finish(p.amax_a, p.amax_na, amx_a);
+      sb = amax_finish(p.amax_b, p.amax_nb, amx_b);
+    }
     store_tile(va0, vb0, smem);
     __syncthreads();
     int kt = kt_begin;
@@ -479,6 +485,9 @@ conv_x3_kernel(ConvGemmParams p) {
       __syncthreads();
     }
     if (kt < kt_end) compute(smem);  // odd tile count: the last tile sits in stage 0
+  } else if constexpr (NP == 2) {  // no K-tiles: the (zero) accumulators still get unscaled
+    sa = amax_finish(p.amax_a, p.amax_na, amx_a);
+    sb = amax_finish(p.amax_b, p.amax_nb, amx_b);
   }
 
   if constexpr (NP == 2) {  // undo the operand scales (exact: powers of two)

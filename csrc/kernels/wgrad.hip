@@ -284,11 +284,18 @@ __global__ __launch_bounds__(wg_threads<BM>(), BM >= 256 ? 1 : 2) void wgrad_x3_
   for (int i = 0; i < RPT_A; ++i)
     a_off[i] = co < p.Cout ? (unsigned)(mul24(a_mq * RPT_A + i, p.Cout) + co) * 4u : kOOB;
   const __amdgpu_buffer_rsrc_t xr = make_rsrc(p.x, (unsigned)p.N * (unsigned)HWC * 4u);
-  float sa = 1.f, sb = 1.f;  // f16x2 operand scales (dY, x)
+  float sa = 1.f, sb = 1.f;  // f16x2 operand scales (dY, x): partial loads first, waited for after
+  float amx_a[NP == 2 ? kAmaxK : 1], amx_b[NP == 2 ? kAmaxK : 1];  // the first tiles' loads are issued
   if constexpr (NP == 2) {
-    sa = amax_scale(p.amax_dy, p.amax_ndy);
-    sb = amax_scale(p.amax_x, p.amax_nx);
+    amax_issue(p.amax_dy, p.amax_ndy, amx_a);
+    amax_issue(p.amax_x, p.amax_nx, amx_b);
   }
+  auto finish_scales = [&]() {
+    if constexpr (NP == 2) {
+      sa = amax_finish(p.amax_dy, p.amax_ndy, amx_a);
+      sb = amax_finish(p.amax_x, p.amax_nx, amx_b);
+    }
+  };
 
   float4 ra[RPT_A], rb[RPT_B], ra1[RPT_A], rb1[RPT_B];
   // valid == false (FAST only): zero-size / out-of-range buffers, so the loads return zeros without
@@ -432,6 +439,7 @@ __global__ __launch_bounds__(wg_threads<BM>(), BM >= 256 ? 1 : 2) void wgrad_x3_
       static_assert(!PIPE || FAST, "the pipelined kernel issues branch-free FAST loads");
       load_tile(kt_begin, ra, rb);
       load_tile(kt_begin + 1, ra1, rb1, kt_begin + 1 < kt_end);
+      finish_scales();
       store_tile(ra, rb, smem);
       __syncthreads();
       int kt = kt_begin;
@@ -446,9 +454,12 @@ __global__ __launch_bounds__(wg_threads<BM>(), BM >= 256 ? 1 : 2) void wgrad_x3_
         __syncthreads();
       }
       if (kt < kt_end) compute(smem);
+    } else {
+      finish_scales();
     }
   } else if (kt_begin < kt_end) {
     load_tile(kt_begin, ra, rb);
+    finish_scales();
     store_tile(ra, rb, smem);
     __syncthreads();
     for (int kt = kt_begin; kt < kt_end; ++kt) {

@@ -67,16 +67,48 @@ __device__ __forceinline__ void split_pair_h(float x, float y, float s, unsigned
 // Power-of-two operand scale from a producer's partial |max| values part[0..n): maps the max to
 // [2^14, 2^15). Every lane of the calling wave gets the same value (no LDS, no barrier). A zero,
 // inf or NaN max gives 1 (zeros stay zeros; non-finite inputs propagate as in fp32).
-__device__ __forceinline__ float amax_scale(const float* __restrict__ part, int n) {
+// The partials are read 32 independent buffer loads per lane at a time (2048 per round trip; past n
+// they read 0, neutral for |max|): a one-load-per-iteration loop waited a full memory latency per
+// 128 partials in every wave, ~16 round trips at the start of each GEMM fed by a 2048-block producer.
+// Split in two so a kernel can issue the first 2048 (amax_issue), then its first operand tiles, and
+// only then wait (amax_finish): the scale's round trip overlaps the tile loads.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t amax_rsrc(const float* part, int n) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(part), (short)0, n * 4, 0x00020000);
+}
+constexpr int kAmaxK = 32;  // loads per lane per round trip
+__device__ __forceinline__ void amax_issue(const float* __restrict__ part, int n, float (&v)[kAmaxK]) {
+  const int lane = threadIdx.x & 63;
+  const __amdgpu_buffer_rsrc_t r = amax_rsrc(part, n);
+#pragma unroll
+  for (int k = 0; k < kAmaxK; ++k) v[k] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, (64 * k + lane) * 4, 0, 0));
+}
+__device__ __forceinline__ float amax_finish(const float* __restrict__ part, int n, const float (&v0)[kAmaxK]) {
   const int lane = threadIdx.x & 63;
   float m = 0.f;
-  for (int i = lane; i < n; i += 64) m = fmaxf(m, part[i]);
+#pragma unroll
+  for (int k = 0; k < kAmaxK; ++k) m = fmaxf(m, v0[k]);
+  if (n > 64 * kAmaxK) {
+    const __amdgpu_buffer_rsrc_t r = amax_rsrc(part, n);
+    for (int base = 64 * kAmaxK; base < n; base += 64 * 16) {
+      float v[16];
+#pragma unroll
+      for (int k = 0; k < 16; ++k)
+        v[k] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, (base + 64 * k + lane) * 4, 0, 0));
+#pragma unroll
+      for (int k = 0; k < 16; ++k) m = fmaxf(m, v[k]);
+    }
+  }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
   if (!(m > 0.f) || !(m < 3.0e38f)) return 1.f;
   int e;
   (void)frexpf(m, &e);  // m < 2^e
   return ldexpf(1.f, max(-100, min(100, 15 - e)));
+}
+__device__ __forceinline__ float amax_scale(const float* __restrict__ part, int n) {
+  float v[kAmaxK];
+  amax_issue(part, n, v);
+  return amax_finish(part, n, v);
 }
 
 // Raw buffer resource over [base, base + bytes): loads past `bytes` return 0 (hardware range
