@@ -15,6 +15,7 @@
 // All element kernels move float4 along C (C % 4 == 0).
 #include "common.h"
 #include "kernels.h"
+#include "x3_common.h"
 
 namespace cdp {
 namespace {
@@ -28,18 +29,44 @@ __global__ __launch_bounds__(256) void bn_finalize_kernel(const float* __restric
   __shared__ double red[4];
   const int c = blockIdx.x;
   const int tid = threadIdx.x;
-  double s = 0.0;
-  for (int b = tid; b < nparts; b += 256) {
-    const int cnt = min(rpp, M - b * rpp);
-    s += (double)cnt * (double)part[((long long)b * C + c) * 2];
+  // this thread's partials (b = tid + 256 k) are loaded in one batch and kept in registers for
+  // both passes: one memory round trip instead of one per partial and pass (nparts <= 2048; more
+  // fall back to a second, looped batch)
+  // (buffer loads: the partials past nparts read 0 with no branch around the loads)
+  constexpr int KB = 8;
+  float pm[KB], pq[KB];
+  const __amdgpu_buffer_rsrc_t pr = make_rsrc(part, (unsigned)nparts * (unsigned)C * 8u);
+#pragma unroll
+  for (int k = 0; k < KB; ++k) {
+    const int b = tid + 256 * k;
+    const unsigned o = b < nparts ? (unsigned)(b * C + c) * 8u : kOOB;
+    const auto v = __builtin_amdgcn_raw_buffer_load_b64(pr, (int)o, 0, 0);
+    pm[k] = __uint_as_float(v[0]);
+    pq[k] = __uint_as_float(v[1]);
   }
+  double s = 0.0;
+#pragma unroll
+  for (int k = 0; k < KB; ++k) {
+    const int b = tid + 256 * k;
+    if (b < nparts) s += (double)min(rpp, M - b * rpp) * (double)pm[k];
+  }
+  for (int b = tid + 256 * KB; b < nparts; b += 256)
+    s += (double)min(rpp, M - b * rpp) * (double)part[((long long)b * C + c) * 2];
   s = wave_sum_d(s);
   if ((tid & 63) == 0) red[tid >> 6] = s;
   __syncthreads();
   const double mean = (red[0] + red[1] + red[2] + red[3]) / (double)M;
   __syncthreads();
   double q = 0.0;
-  for (int b = tid; b < nparts; b += 256) {
+#pragma unroll
+  for (int k = 0; k < KB; ++k) {
+    const int b = tid + 256 * k;
+    if (b < nparts) {
+      const double d = (double)pm[k] - mean;
+      q += (double)pq[k] + (double)min(rpp, M - b * rpp) * d * d;
+    }
+  }
+  for (int b = tid + 256 * KB; b < nparts; b += 256) {
     const int cnt = min(rpp, M - b * rpp);
     const double d = (double)part[((long long)b * C + c) * 2] - mean;
     q += (double)part[((long long)b * C + c) * 2 + 1] + (double)cnt * d * d;
@@ -289,7 +316,26 @@ __global__ __launch_bounds__(256) void chan_finalize_kernel(const float* __restr
   __shared__ double r0[4], r1[4], r2[4];
   const int c = blockIdx.x;
   double s0 = 0.0, s1 = 0.0, s2 = 0.0;
-  for (int b = threadIdx.x; b < nparts; b += 256) {
+  // all of this thread's partials in one batch of loads (nparts <= 1024), then the sums; the
+  // summation order per thread is unchanged (b ascending), so results are as before
+  constexpr int KB = 4;
+  float v0[KB], v1[KB], v2[KB];
+  const __amdgpu_buffer_rsrc_t pr = make_rsrc(part, (unsigned)nparts * (unsigned)C * (unsigned)PS * 4u);
+#pragma unroll
+  for (int k = 0; k < KB; ++k) {
+    const int b = threadIdx.x + 256 * k;
+    const unsigned o = b < nparts ? (unsigned)((b * C + c) * PS) * 4u : kOOB;
+    v0[k] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(pr, (int)o, 0, 0));
+    v1[k] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(pr, (int)(o + 4u), 0, 0));
+    v2[k] = PS == 3 ? __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(pr, (int)(o + 8u), 0, 0)) : 0.f;
+  }
+#pragma unroll
+  for (int k = 0; k < KB; ++k) {
+    s0 += (double)v0[k];
+    s1 += (double)v1[k];
+    s2 += (double)v2[k];
+  }
+  for (int b = threadIdx.x + 256 * KB; b < nparts; b += 256) {
     const float* q = part + ((long long)b * C + c) * PS;
     s0 += (double)q[0];
     s1 += (double)q[1];
@@ -461,11 +507,13 @@ int bn_bwd_grid(int N, int H, int W, int C, bool pool) {
   const int ppb = 256 / lanes_c;
   const long long npix = (long long)N * (pool ? (H / 2) * (W / 2) : H * W);
   long long b = (npix + ppb - 1) / ppb;
-  // keep >= ~8 pixels per thread lane for reduction efficiency, <= 1024 partial rows
-  // but never fewer workgroups than CUs while there are rows for them: the deep VGG layers
-  // (2x2 / 4x4 maps) otherwise ran 16-128 workgroups, latency-bound at ~11 us per kernel
+  // ~2 pixels per thread lane, <= 1024 partial rows (one batch of loads in chan_finalize), and
+  // never fewer workgroups than CUs while there are rows for them. Every pixel a lane handles is
+  // one dependent memory round trip (the loop is not software-pipelined): at ~8 per lane the
+  // small deep-layer passes were latency-bound (deep VGG layers otherwise ran 16-128 workgroups,
+  // ~11 us per kernel)
   const long long rows = b;
-  b = (b + 7) / 8;
+  b = (b + 1) / 2;
   if (b < 256) b = rows < 256 ? rows : 256;
   if (b > 1024) b = 1024;
   if (b < 1) b = 1;

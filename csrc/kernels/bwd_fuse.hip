@@ -70,23 +70,39 @@ __global__ __launch_bounds__(256) void bwd_reduce_kernel(BwdReduceArgs a) {
     const int y0 = by * RBD;
     const long long plane = (long long)a.d_M * C;
     float4 g[RBD / 16];
+    // both rows' slab loads in batches of 8 splits (one round trip per batch); out-of-range rows /
+    // splits load a valid address and are masked to zero
+#pragma unroll
+    for (int i = 0; i < RBD / 16; ++i) g[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    const bool any = nok && y0 + rl < a.d_M;
+    for (int z0 = 0; any && z0 < a.d_S; z0 += 8) {
+      float4 t[RBD / 16][8];
+#pragma unroll
+      for (int i = 0; i < RBD / 16; ++i) {
+        const int m = y0 + rl + 16 * i;
+        const float* src = a.d_slab + (long long)(m < a.d_M ? m : y0 + rl) * C + n;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) t[i][k] = ld4(src + (long long)(z0 + k < a.d_S ? z0 + k : 0) * plane);
+      }
+#pragma unroll
+      for (int i = 0; i < RBD / 16; ++i)
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+          if (z0 + k >= a.d_S) t[i][k] = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+      for (int i = 0; i < RBD / 16; ++i) {
+        float4& s = g[i];
+        s.x += ((t[i][0].x + t[i][1].x) + (t[i][2].x + t[i][3].x)) + ((t[i][4].x + t[i][5].x) + (t[i][6].x + t[i][7].x));
+        s.y += ((t[i][0].y + t[i][1].y) + (t[i][2].y + t[i][3].y)) + ((t[i][4].y + t[i][5].y) + (t[i][6].y + t[i][7].y));
+        s.z += ((t[i][0].z + t[i][1].z) + (t[i][2].z + t[i][3].z)) + ((t[i][4].z + t[i][5].z) + (t[i][6].z + t[i][7].z));
+        s.w += ((t[i][0].w + t[i][1].w) + (t[i][2].w + t[i][3].w)) + ((t[i][4].w + t[i][5].w) + (t[i][6].w + t[i][7].w));
+      }
+    }
 #pragma unroll
     for (int i = 0; i < RBD / 16; ++i) {
       const int m = y0 + rl + 16 * i;
-      float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+      float4 s = g[i];
       if (m < a.d_M && nok) {
-        const float* src = a.d_slab + (long long)m * C + n;
-        int z = 0;
-        for (; z + 3 < a.d_S; z += 4) {
-          const float4 p = ld4(src + z * plane), q = ld4(src + (z + 1) * plane);
-          const float4 r = ld4(src + (z + 2) * plane), t = ld4(src + (z + 3) * plane);
-          s.x += (p.x + q.x) + (r.x + t.x); s.y += (p.y + q.y) + (r.y + t.y);
-          s.z += (p.z + q.z) + (r.z + t.z); s.w += (p.w + q.w) + (r.w + t.w);
-        }
-        for (; z < a.d_S; ++z) {
-          const float4 p = ld4(src + z * plane);
-          s.x += p.x; s.y += p.y; s.z += p.z; s.w += p.w;
-        }
         const long long o = (long long)m * C + n;
         if (a.d_addend) {
           const float4 ad = ld4(a.d_addend + o);

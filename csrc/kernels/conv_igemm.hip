@@ -310,23 +310,40 @@ __global__ __launch_bounds__(256) void splitk_reduce4_kernel(const float* __rest
   const float4 bv = (bias && nok) ? ld4(bias + n) : f4zero();
   const long long plane = (long long)M * Nout;
   float4 v[RB / 16];
+  // all rows' slab loads in batches of 8 splits (one memory round trip per batch, not one per 4
+  // splits and row): out-of-range rows / splits load a valid address and are masked to zero
+  float4 acc[RB / 16];
+#pragma unroll
+  for (int i = 0; i < RB / 16; ++i) acc[i] = f4zero();
+  const bool any = nok && y0 + rl < M;
+  for (int z0 = 0; any && z0 < S; z0 += 8) {
+    float4 t[RB / 16][8];
+#pragma unroll
+    for (int i = 0; i < RB / 16; ++i) {
+      const int m = y0 + rl + 16 * i;
+      const float* src = slab + (long long)(m < M ? m : y0 + rl) * Nout + n;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) t[i][k] = ld4(src + (long long)(z0 + k < S ? z0 + k : 0) * plane);
+    }
+#pragma unroll
+    for (int i = 0; i < RB / 16; ++i)
+#pragma unroll
+      for (int k = 0; k < 8; ++k)
+        if (z0 + k >= S) t[i][k] = f4zero();
+#pragma unroll
+    for (int i = 0; i < RB / 16; ++i) {
+      float4& a = acc[i];
+      a.x += ((t[i][0].x + t[i][1].x) + (t[i][2].x + t[i][3].x)) + ((t[i][4].x + t[i][5].x) + (t[i][6].x + t[i][7].x));
+      a.y += ((t[i][0].y + t[i][1].y) + (t[i][2].y + t[i][3].y)) + ((t[i][4].y + t[i][5].y) + (t[i][6].y + t[i][7].y));
+      a.z += ((t[i][0].z + t[i][1].z) + (t[i][2].z + t[i][3].z)) + ((t[i][4].z + t[i][5].z) + (t[i][6].z + t[i][7].z));
+      a.w += ((t[i][0].w + t[i][1].w) + (t[i][2].w + t[i][3].w)) + ((t[i][4].w + t[i][5].w) + (t[i][6].w + t[i][7].w));
+    }
+  }
 #pragma unroll
   for (int i = 0; i < RB / 16; ++i) {
     const int m = y0 + rl + 16 * i;
-    float4 s = f4zero();
+    float4 s = acc[i];
     if (m < M && nok) {
-      const float* src = slab + (long long)m * Nout + n;
-      int z = 0;
-      for (; z + 3 < S; z += 4) {
-        const float4 a = ld4(src + z * plane), b = ld4(src + (z + 1) * plane);
-        const float4 c = ld4(src + (z + 2) * plane), d = ld4(src + (z + 3) * plane);
-        s.x += (a.x + b.x) + (c.x + d.x); s.y += (a.y + b.y) + (c.y + d.y);
-        s.z += (a.z + b.z) + (c.z + d.z); s.w += (a.w + b.w) + (c.w + d.w);
-      }
-      for (; z < S; ++z) {
-        const float4 a = ld4(src + z * plane);
-        s.x += a.x; s.y += a.y; s.z += a.z; s.w += a.w;
-      }
       s.x += bv.x; s.y += bv.y; s.z += bv.z; s.w += bv.w;
       const long long o = remap_row(rr, m) * Nout + n;
       if (addend) {
