@@ -21,6 +21,11 @@ template <int BM>
 constexpr int waves_m() { return BM >= 256 ? 4 : 2; }
 
 template <int BM, int BN>
+__device__ __forceinline__ void conv_tile_stats(const ConvGemmParams& p,
+                                                const f32x16 (&acc)[BM / waves_m<BM>() / 32][BN / 64], float* red,
+                                                int m0, int n0, int tm_idx);
+
+template <int BM, int BN>
 __device__ __forceinline__ void conv_epilogue(const ConvGemmParams& p,
                                               f32x16 (&acc)[BM / waves_m<BM>() / 32][BN / 64], float* red, int m0,
                                               int n0, int tm_idx, int split) {
@@ -76,6 +81,14 @@ __device__ __forceinline__ void conv_epilogue(const ConvGemmParams& p,
     const int n = n0 + wn * (BN / 2) + b * 32 + l32;
     bias_v[b] = (p.bias && n < p.Nout) ? p.bias[n] : 0.f;
   }
+#pragma unroll
+  for (int a = 0; a < TM; ++a)
+#pragma unroll
+    for (int b = 0; b < TN; ++b)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[a][b][r] += bias_v[b];
+  // the output stores go last: a barrier behind them (the statistics' ones) would make every wave
+  // wait for its stores to reach memory first
   auto out_store = [&](auto pred) {
 #pragma unroll
     for (int a = 0; a < TM; ++a)
@@ -85,16 +98,28 @@ __device__ __forceinline__ void conv_epilogue(const ConvGemmParams& p,
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int m = m0 + wm * (BM / WM) + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
-          const float v = acc[a][b][r] + bias_v[b];
-          acc[a][b][r] = v;
-          if (!decltype(pred)::value || (m < p.M && n < p.Nout)) p.y[remap_row(p.rr, m) * p.Nout + n] = v;
+          if (!decltype(pred)::value || (m < p.M && n < p.Nout)) p.y[remap_row(p.rr, m) * p.Nout + n] = acc[a][b][r];
         }
       }
   };
+  if (p.part) conv_tile_stats<BM, BN>(p, acc, red, m0, n0, tm_idx);
   if (full) out_store(std::false_type{});
   else out_store(std::true_type{});
-  if (!p.part) return;
+}
 
+// BN partials (mean, M2) of the tile's columns over its valid rows -> p.part[tm_idx]
+template <int BM, int BN>
+__device__ __forceinline__ void conv_tile_stats(const ConvGemmParams& p,
+                                                const f32x16 (&acc)[BM / waves_m<BM>() / 32][BN / 64], float* red,
+                                                int m0, int n0, int tm_idx) {
+  constexpr int WM = waves_m<BM>();
+  constexpr int TM = BM / WM / 32, TN = BN / 64;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wid = tid >> 6;
+  const int wm = wid >> 1, wn = wid & 1;
+  const int l32 = lane & 31;
+  const int hh = lane >> 5;
   __syncthreads();  // `red` aliases the operand LDS
   const int cnt = min(BM, p.M - m0);
   float colsum[TN];
