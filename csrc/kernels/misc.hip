@@ -197,17 +197,20 @@ __global__ __launch_bounds__(256) void augment_kernel(const unsigned char* __res
   const unsigned char* src = imgs + src_i * (long long)H * W * C;
   const float mean[3] = {m0, m1, m2};
   const float istd[3] = {is0, is1, is2};
-  const int total = H * W * C;
-  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < total; e += gridDim.x * blockDim.x) {
-    const int c = e % C;
-    const int w = (e / C) % W;
-    const int h = e / (C * W);
+  const int npix = H * W;
+  float* dst = out + (long long)b * npix * C;
+  // one thread per output pixel, all its channels (one index decode per pixel, not per element)
+  for (int px = blockIdx.x * blockDim.x + threadIdx.x; px < npix; px += gridDim.x * blockDim.x) {
+    const int h = px / W, w = px - (px / W) * W;
     const int ww = fl ? (W - 1 - w) : w;  // flip applied after the crop (torchvision order)
     const int sh = h + oy, sw = ww + ox;
-    float v = 0.f;
-    if ((unsigned)sh < (unsigned)H && (unsigned)sw < (unsigned)W) v = (float)src[(sh * W + sw) * C + c] * (1.f / 255.f);
-    const int ci = c < 3 ? c : 2;
-    out[(long long)b * total + e] = (v - mean[ci]) * istd[ci];
+    const bool in = (unsigned)sh < (unsigned)H && (unsigned)sw < (unsigned)W;
+    const unsigned char* sp = src + (long long)(in ? sh * W + sw : 0) * C;
+    for (int c = 0; c < C; ++c) {
+      const float v = in ? (float)sp[c] * (1.f / 255.f) : 0.f;
+      const int ci = c < 3 ? c : 2;
+      dst[(long long)px * C + c] = (v - mean[ci]) * istd[ci];
+    }
   }
 }
 
@@ -236,8 +239,12 @@ __global__ __launch_bounds__(256) void wtrans_kernel(const float* __restrict__ w
 // One launch for all conv weights of a step (replaces a transpose launch per layer plus the
 // |max| pass): block (segment, co32, ci32) walks the T taps of its 32x32 (co, ci) block, keeps the
 // block's |max| (one partial per block) and, when asked, writes the tile transposed through LDS.
+// Taps go in groups of TG: all of a group's loads are issued before any is used (branch-free: out
+// of range elements read 0 through the buffer range check), so a 3x3 filter costs one memory round
+// trip per block instead of nine.
 __global__ __launch_bounds__(256) void weight_prep_kernel(WeightPrepArgs a, float* __restrict__ part) {
-  __shared__ float tile[32][33];
+  constexpr int TG = 9;
+  __shared__ float tile[TG][32][33];
   __shared__ float red[4];
   const int b = blockIdx.x;
   int seg = 0;
@@ -249,21 +256,37 @@ __global__ __launch_bounds__(256) void weight_prep_kernel(WeightPrepArgs a, floa
   const int nci = (Ci + 31) / 32;
   const int co0 = (local / nci) * 32, ci0 = (local % nci) * 32;
   const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 32 x 8
+  const __amdgpu_buffer_rsrc_t wr = make_rsrc(w, (unsigned)((long long)Co * T * Ci * 4));
   float m = 0.f;
-  for (int tap = 0; tap < T; ++tap) {
+  for (int t0 = 0; t0 < T; t0 += TG) {
+    float v[TG][4];
 #pragma unroll
-    for (int j = ty; j < 32; j += 8) {
-      const int co = co0 + j, ci = ci0 + tx;
-      const float v = (co < Co && ci < Ci) ? w[((long long)co * T + tap) * Ci + ci] : 0.f;
-      m = fmaxf(m, fabsf(v));
-      tile[j][tx] = v;
-    }
+    for (int g = 0; g < TG; ++g)
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) {
+        const int co = co0 + ty + 8 * jj, ci = ci0 + tx, tap = t0 + g;
+        const unsigned o = (co < Co && ci < Ci && tap < T) ? (unsigned)(((co * T + tap) * Ci + ci) * 4) : kOOB;
+        v[g][jj] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(wr, (int)o, 0, 0));
+      }
+#pragma unroll
+    for (int g = 0; g < TG; ++g)
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) m = fmaxf(m, fabsf(v[g][jj]));
     if (wt) {
+#pragma unroll
+      for (int g = 0; g < TG; ++g)
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) tile[g][ty + 8 * jj][tx] = v[g][jj];
       __syncthreads();
 #pragma unroll
-      for (int j = ty; j < 32; j += 8) {
-        const int ci = ci0 + j, co = co0 + tx;
-        if (ci < Ci && co < Co) wt[((long long)ci * T + tap) * Co + co] = tile[tx][j];
+      for (int g = 0; g < TG; ++g) {
+        const int tap = t0 + g;
+        if (tap >= T) break;
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) {
+          const int ci = ci0 + ty + 8 * jj, co = co0 + tx;
+          if (ci < Ci && co < Co) wt[((long long)ci * T + tap) * Co + co] = tile[g][tx][ty + 8 * jj];
+        }
       }
       __syncthreads();
     }
@@ -569,8 +592,7 @@ void augment_launch(const unsigned char* imgs, const long long* idx, long long i
                     const float* mean, const float* inv_std, int pad, bool flip, const long long* counter,
                     unsigned long long seed, float* out, hipStream_t st, long long nbatches,
                     const long long* labels, long long* labels_out) {
-  const int total = H * W * C;
-  dim3 grid((total + 255) / 256, B);
+  dim3 grid((H * W + 255) / 256, B);
   hipLaunchKernelGGL(augment_kernel, grid, dim3(256), 0, st, imgs, idx, idx_off, B, H, W, C, mean[0], mean[1],
                      mean[2], inv_std[0], inv_std[1], inv_std[2], pad, flip ? 1 : 0, counter, seed, out, nbatches,
                      labels, labels_out);
