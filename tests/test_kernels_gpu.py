@@ -485,8 +485,8 @@ def test_weight_prep_transposes_and_maxima():
     (f16x2) whose max is each weight's |max|; dgrad with the prepared W^T equals dgrad without."""
     torch.manual_seed(4)
     ws = [cl(torch.randn(co, ci, k, k, device="cuda")) for co, ci, k in
-          [(64, 3, 3), (128, 64, 3), (512, 512, 3), (256, 64, 1), (10, 7, 3)]]
-    want = [False, True, True, True, True]
+          [(64, 3, 3), (128, 64, 3), (512, 512, 3), (256, 64, 1), (10, 7, 3), (64, 3, 7), (40, 36, 5)]]
+    want = [False, True, True, True, True, True, True]  # 7x7 / 5x5: taps past one 9-tap load batch
     amax, wts = C().weight_prep(ws, want)
     for w, wt, f in zip(ws, wts, want):
         if not f:
