@@ -13,6 +13,8 @@
 //   bn_bwd_apply: dy = scale*(dz - mean(dz) - xhat*mean(dz*xhat)), plus partial sum(dy) for the
 //   conv bias gradient.
 // All element kernels move float4 along C (C % 4 == 0).
+#include <algorithm>
+
 #include "common.h"
 #include "kernels.h"
 #include "x3_common.h"
@@ -124,6 +126,126 @@ __device__ __forceinline__ float4 affine_act(float4 y, float4 sc, float4 sh, boo
     z.w = fmaxf(z.w, 0.f);
   }
   return z;
+}
+
+// Finalize + apply in one launch for layers with few statistics partials (nparts <= 128, the
+// deep VGG layers): block = 64 channels x one chunk of output rows. Every block merges its 64
+// channels' partials itself (fp64, the formulas of bn_finalize_kernel); the chunk-0 blocks publish
+// stats and the running statistics; then the block applies [pool2](relu(y*scale + shift)) to its
+// rows. Saves a dependent launch per layer; the redundant merge reads <= 64 KB per block from L2.
+constexpr int FIN_MAXP = 128;
+__global__ __launch_bounds__(256) void bn_fin_act_kernel(const float* __restrict__ part, int nparts, int rpp, int M,
+                                                         int C, const float* __restrict__ gamma,
+                                                         const float* __restrict__ beta, float* running_mean,
+                                                         float* running_var, long long* nbt, float momentum,
+                                                         float eps, float* __restrict__ stats,
+                                                         const float* __restrict__ y, float* __restrict__ out, int N,
+                                                         int H, int W, int pool, int relu, int chunks,
+                                                         float* __restrict__ amax_part) {
+  __shared__ double red[4][64];
+  __shared__ float s_sc[64], s_sh[64];
+  const int ngroups = C >> 6;
+  const int cg = blockIdx.x % ngroups, chunk = blockIdx.x / ngroups;
+  const int tid = threadIdx.x;
+  const int ch = tid & 63, q = tid >> 6;
+  const int c = cg * 64 + ch;
+  // phase 1: thread (ch, q) merges partials b = q + 4k -- one batch of buffer loads
+  constexpr int KP = FIN_MAXP / 4;
+  float pm[KP], pq[KP];
+  const __amdgpu_buffer_rsrc_t pr = make_rsrc(part, (unsigned)nparts * (unsigned)C * 8u);
+#pragma unroll
+  for (int k = 0; k < KP; ++k) {
+    const int b = q + 4 * k;
+    const unsigned o = b < nparts ? (unsigned)(b * C + c) * 8u : kOOB;
+    const auto v = __builtin_amdgcn_raw_buffer_load_b64(pr, (int)o, 0, 0);
+    pm[k] = __uint_as_float(v[0]);
+    pq[k] = __uint_as_float(v[1]);
+  }
+  double sm = 0.0;
+#pragma unroll
+  for (int k = 0; k < KP; ++k) {
+    const int b = q + 4 * k;
+    if (b < nparts) sm += (double)min(rpp, M - b * rpp) * (double)pm[k];
+  }
+  red[q][ch] = sm;
+  __syncthreads();
+  const double mean = (red[0][ch] + red[1][ch] + red[2][ch] + red[3][ch]) / (double)M;
+  __syncthreads();
+  double sq = 0.0;
+#pragma unroll
+  for (int k = 0; k < KP; ++k) {
+    const int b = q + 4 * k;
+    if (b < nparts) {
+      const double d = (double)pm[k] - mean;
+      sq += (double)pq[k] + (double)min(rpp, M - b * rpp) * d * d;
+    }
+  }
+  red[q][ch] = sq;
+  __syncthreads();
+  if (q == 0) {
+    const double m2 = red[0][ch] + red[1][ch] + red[2][ch] + red[3][ch];
+    const double var = m2 / (double)M;
+    const float invstd = (float)(1.0 / sqrt(var + (double)eps));
+    const float g = gamma ? gamma[c] : 1.f;
+    const float bb = beta ? beta[c] : 0.f;
+    const float scale = g * invstd;
+    const float shift = bb - (float)mean * scale;
+    s_sc[ch] = scale;
+    s_sh[ch] = shift;
+    if (chunk == 0) {
+      stats[c] = (float)mean;
+      stats[C + c] = invstd;
+      stats[2 * C + c] = scale;
+      stats[3 * C + c] = shift;
+      if (running_mean) {
+        float f = momentum;
+        if (f < 0.f) f = 1.f / (float)(nbt[0] + 1);  // momentum=None: cumulative average
+        const double unb = M > 1 ? m2 / (double)(M - 1) : var;
+        running_mean[c] = (1.f - f) * running_mean[c] + f * (float)mean;
+        running_var[c] = (1.f - f) * running_var[c] + f * (float)unb;
+      }
+      if (c == 0 && nbt) nbt[0] += 1;
+    }
+  }
+  __syncthreads();
+  // phase 2: this chunk's output rows, 16 channel quads x 16 row lanes
+  const int cq = tid & 15, rl = tid >> 4;
+  const int n0 = cg * 64 + 4 * cq;
+  const float4 sc = make_float4(s_sc[4 * cq], s_sc[4 * cq + 1], s_sc[4 * cq + 2], s_sc[4 * cq + 3]);
+  const float4 sh = make_float4(s_sh[4 * cq], s_sh[4 * cq + 1], s_sh[4 * cq + 2], s_sh[4 * cq + 3]);
+  const int Ho = pool ? H / 2 : H, Wo = pool ? W / 2 : W;
+  const long long rows = (long long)N * Ho * Wo;
+  const long long per = (rows + chunks - 1) / chunks;
+  const long long r0 = (long long)chunk * per, r1 = min(rows, r0 + per);
+  float am = 0.f;
+  for (long long r = r0 + rl; r < r1; r += 16) {
+    float4 z;
+    if (!pool) {
+      z = affine_act(ld4(y + r * C + n0), sc, sh, relu);
+    } else {
+      const int wo = (int)(r % Wo);
+      const long long t = r / Wo;
+      const int ho = (int)(t % Ho);
+      const int n = (int)(t / Ho);
+      const float* base = y + (((long long)n * H + 2 * ho) * W + 2 * wo) * C + n0;
+      const float4 z0 = affine_act(ld4(base), sc, sh, relu), z1 = affine_act(ld4(base + C), sc, sh, relu);
+      const float4 z2 = affine_act(ld4(base + (long long)W * C), sc, sh, relu);
+      const float4 z3 = affine_act(ld4(base + (long long)W * C + C), sc, sh, relu);
+      z.x = fmaxf(fmaxf(z0.x, z1.x), fmaxf(z2.x, z3.x));
+      z.y = fmaxf(fmaxf(z0.y, z1.y), fmaxf(z2.y, z3.y));
+      z.z = fmaxf(fmaxf(z0.z, z1.z), fmaxf(z2.z, z3.z));
+      z.w = fmaxf(fmaxf(z0.w, z1.w), fmaxf(z2.w, z3.w));
+    }
+    st4(out + r * C + n0, z);
+    am = fmaxf(am, fmaxf(fmaxf(fabsf(z.x), fabsf(z.y)), fmaxf(fabsf(z.z), fabsf(z.w))));
+  }
+  if (amax_part) {
+    __shared__ float ared[4];
+    am = wave_max(am);
+    if ((tid & 63) == 0) ared[tid >> 6] = am;
+    __syncthreads();
+    if (tid == 0) amax_part[blockIdx.x] = fmaxf(fmaxf(ared[0], ared[1]), fmaxf(ared[2], ared[3]));
+  }
 }
 
 // ------------------------------------------------------------------ forward apply
@@ -531,6 +653,26 @@ void bn_eval_stats_launch(int C, const float* gamma, const float* beta, const fl
                           float* stats, hipStream_t st) {
   hipLaunchKernelGGL(bn_eval_stats_kernel, dim3((C + 255) / 256), dim3(256), 0, st, C, gamma, beta, rm, rv, eps,
                      stats);
+}
+
+bool bn_fin_act_ok(int nparts, int C, bool residual) { return !residual && nparts <= FIN_MAXP && (C % 64) == 0; }
+
+int bn_fin_act_grid(int N, int H, int W, int C, bool pool) {
+  const long long rows = (long long)N * (pool ? (H / 2) * (W / 2) : H * W);
+  const int ngroups = C / 64;
+  long long chunks = std::max<long long>(1, std::min<long long>((rows + 31) / 32, 512 / ngroups));
+  return (int)(chunks * ngroups);
+}
+
+void bn_fin_act_launch(const float* part, int nparts, int rpp, int C, const float* gamma, const float* beta,
+                       float* running_mean, float* running_var, long long* nbt, float momentum, float eps,
+                       float* stats, const float* y, float* out, int N, int H, int W, bool pool, bool relu,
+                       float* amax_part, hipStream_t st) {
+  const int grid = bn_fin_act_grid(N, H, W, C, pool);
+  const int M = N * H * W;
+  hipLaunchKernelGGL(bn_fin_act_kernel, dim3(grid), dim3(256), 0, st, part, nparts, rpp, M, C, gamma, beta,
+                     running_mean, running_var, nbt, momentum, eps, stats, y, out, N, H, W, pool ? 1 : 0,
+                     relu ? 1 : 0, grid / (C / 64), amax_part);
 }
 
 int bn_act_grid(int N, int H, int W, int C, bool pool) {

@@ -179,6 +179,14 @@ void bn_finalize_launch(const float* part, int nparts, int rpp, int M, int C, co
                         float* stats, hipStream_t st);
 void bn_eval_stats_launch(int C, const float* gamma, const float* beta, const float* rm, const float* rv, float eps,
                           float* stats, hipStream_t st);
+// finalize + apply in one launch (training, no residual, nparts <= 128, C % 64 == 0); amax_part
+// (optional) gets bn_fin_act_grid entries
+bool bn_fin_act_ok(int nparts, int C, bool residual);
+int bn_fin_act_grid(int N, int H, int W, int C, bool pool);
+void bn_fin_act_launch(const float* part, int nparts, int rpp, int C, const float* gamma, const float* beta,
+                       float* running_mean, float* running_var, long long* nbt, float momentum, float eps,
+                       float* stats, const float* y, float* out, int N, int H, int W, bool pool, bool relu,
+                       float* amax_part, hipStream_t st);
 // amax_part (optional, bn_act_grid entries): per-block |max| of the written output
 int bn_act_grid(int N, int H, int W, int C, bool pool);
 void bn_act_fwd_launch(const float* y, const float* stats, const float* res, float* out, int N, int H, int W, int C,

@@ -836,34 +836,51 @@ std::vector<at::Tensor> conv_bn_act_fwd(const at::Tensor& x, const at::Tensor& w
   auto opts = y.options();
   at::Tensor stats = at::empty({4, C}, opts);
   hipStream_t st = cur_stream();
+  const bool has_res = residual.has_value() && residual->defined();
+  // few statistics partials (the deep layers): finalize and apply in one launch (bn_fin_act_kernel)
+  static const bool fin_act_on = [] {
+    const char* e = std::getenv("CDP_BN_FIN_ACT");
+    return !(e && e[0] == '0');
+  }();
+  bool fused_fin = false;
+  int nparts = 0, rpp = 0;
+  long long* nbt = nullptr;
   if (training) {
-    const int nparts = r[1].size(0);
-    const int rpp = r[2].item<int>();
-    long long* nbt = nullptr;
+    nparts = r[1].size(0);
+    rpp = r[2].item<int>();
     if (num_batches_tracked.has_value() && num_batches_tracked->defined()) {
       TORCH_CHECK(num_batches_tracked->scalar_type() == at::kLong, "num_batches_tracked must be int64");
       nbt = reinterpret_cast<long long*>(num_batches_tracked->data_ptr<int64_t>());
     }
-    bn_finalize_launch(r[1].data_ptr<float>(), nparts, rpp, N * H * W, C, fptr(gamma), fptr(beta),
-                       fptr_mut(running_mean), fptr_mut(running_var), nbt, (float)momentum, (float)eps,
-                       stats.data_ptr<float>(), st);
+    fused_fin = fin_act_on && bn_fin_act_ok(nparts, C, has_res);
+    if (!fused_fin)
+      bn_finalize_launch(r[1].data_ptr<float>(), nparts, rpp, N * H * W, C, fptr(gamma), fptr(beta),
+                         fptr_mut(running_mean), fptr_mut(running_var), nbt, (float)momentum, (float)eps,
+                         stats.data_ptr<float>(), st);
   } else {
     TORCH_CHECK(running_mean.has_value() && running_var.has_value(), "eval BatchNorm needs running stats");
     bn_eval_stats_launch(C, fptr(gamma), fptr(beta), running_mean->data_ptr<float>(), running_var->data_ptr<float>(),
                          (float)eps, stats.data_ptr<float>(), st);
   }
   at::Tensor res;
-  if (residual.has_value() && residual->defined()) {
+  if (has_res) {
     TORCH_CHECK(!pool, "residual + pool not supported");
     res = nhwc(*residual);
   }
   at::Tensor out = at::empty({N, C, pool ? H / 2 : H, pool ? W / 2 : W},
                              opts.memory_format(at::MemoryFormat::ChannelsLast));
   at::Tensor out_amax;  // the output's |max| partials: the next conv's operand scale (f16x2)
-  if (f16x2_mode()) out_amax = at::empty({bn_act_grid(N, H, W, C, pool)}, opts);
-  bn_act_fwd_launch(y.data_ptr<float>(), stats.data_ptr<float>(), res.defined() ? res.data_ptr<float>() : nullptr,
-                    out.data_ptr<float>(), N, H, W, C, pool, relu, st,
-                    out_amax.defined() ? out_amax.data_ptr<float>() : nullptr);
+  if (f16x2_mode())
+    out_amax = at::empty({fused_fin ? bn_fin_act_grid(N, H, W, C, pool) : bn_act_grid(N, H, W, C, pool)}, opts);
+  if (fused_fin)
+    bn_fin_act_launch(r[1].data_ptr<float>(), nparts, rpp, C, fptr(gamma), fptr(beta), fptr_mut(running_mean),
+                      fptr_mut(running_var), nbt, (float)momentum, (float)eps, stats.data_ptr<float>(),
+                      y.data_ptr<float>(), out.data_ptr<float>(), N, H, W, pool, relu,
+                      out_amax.defined() ? out_amax.data_ptr<float>() : nullptr, st);
+  else
+    bn_act_fwd_launch(y.data_ptr<float>(), stats.data_ptr<float>(), res.defined() ? res.data_ptr<float>() : nullptr,
+                      out.data_ptr<float>(), N, H, W, C, pool, relu, st,
+                      out_amax.defined() ? out_amax.data_ptr<float>() : nullptr);
   return {out, y, stats, xin, out_amax, xa, wa};
 }
 
