@@ -150,16 +150,22 @@ __global__ __launch_bounds__(256) void bn_fin_act_kernel(const float* __restrict
   const int ch = tid & 63, q = tid >> 6;
   const int c = cg * 64 + ch;
   // phase 1: thread (ch, q) merges partials b = q + 4k -- one batch of buffer loads
+  // (only the batches of 8 loads that hold partials are issued: kp = ceil(nparts / 4) rounded up to 8)
   constexpr int KP = FIN_MAXP / 4;
+  const int kp = (((nparts + 3) >> 2) + 7) & ~7;
   float pm[KP], pq[KP];
   const __amdgpu_buffer_rsrc_t pr = make_rsrc(part, (unsigned)nparts * (unsigned)C * 8u);
 #pragma unroll
-  for (int k = 0; k < KP; ++k) {
-    const int b = q + 4 * k;
-    const unsigned o = b < nparts ? (unsigned)(b * C + c) * 8u : kOOB;
-    const auto v = __builtin_amdgcn_raw_buffer_load_b64(pr, (int)o, 0, 0);
-    pm[k] = __uint_as_float(v[0]);
-    pq[k] = __uint_as_float(v[1]);
+  for (int k0 = 0; k0 < KP; k0 += 8) {
+    if (k0 >= kp) break;
+#pragma unroll
+    for (int k = k0; k < k0 + 8; ++k) {
+      const int b = q + 4 * k;
+      const unsigned o = b < nparts ? (unsigned)(b * C + c) * 8u : kOOB;
+      const auto v = __builtin_amdgcn_raw_buffer_load_b64(pr, (int)o, 0, 0);
+      pm[k] = __uint_as_float(v[0]);
+      pq[k] = __uint_as_float(v[1]);
+    }
   }
   double sm = 0.0;
 #pragma unroll
@@ -614,6 +620,138 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const float* __restri
   }
 }
 
+// Backward twin of bn_fin_act_kernel for layers with few statistics partials (nparts <= 128: the
+// deep VGG layers, whose partials come from the consumer block's bwd_reduce_kernel): block = 64
+// channels x one chunk of output rows. Every block merges its channels' partials itself (fp64, as
+// chan_finalize_kernel); the chunk-0 blocks publish dgamma, dbeta and the conv-bias gradient; then
+// the block writes dy = scale*(dz - sum(dz)/M - xhat*sum(dz*xhat)/M) for its rows, with the
+// pool / ReLU routing recomputed from y. Training mode only (no residual, even map under pooling).
+__global__ __launch_bounds__(256) void bn_bwd_fin_apply_kernel(
+    const float* __restrict__ part, int nparts, int PS, const float* __restrict__ y,
+    const float* __restrict__ gout, const float* __restrict__ stats, float* __restrict__ dy, float* gbeta,
+    float* ggamma, float* gdb, int N, int H, int W, int C, int pool, int relu, int chunks,
+    float* __restrict__ amax_part) {
+  __shared__ double red[3][4][64];
+  __shared__ float s_k1[64], s_k2[64];
+  const int ngroups = C >> 6;
+  const int cg = blockIdx.x % ngroups, chunk = blockIdx.x / ngroups;
+  const int tid = threadIdx.x;
+  const int ch = tid & 63, q = tid >> 6;
+  const int c = cg * 64 + ch;
+  const long long Mtot = (long long)N * H * W;
+  // phase 1: thread (ch, q) sums partials b = q + 4k (one batch of buffer loads, ascending b)
+  // batches of 8 partials per thread (one round trip for nparts <= 32), only as many as there are
+  constexpr int KB = 8;
+  const __amdgpu_buffer_rsrc_t pr = make_rsrc(part, (unsigned)nparts * (unsigned)C * (unsigned)PS * 4u);
+  double s0 = 0.0, s1 = 0.0, s2 = 0.0;
+  for (int k0 = 0; 4 * k0 < nparts; k0 += KB) {
+    float v0[KB], v1[KB], v2[KB];
+#pragma unroll
+    for (int k = 0; k < KB; ++k) {
+      const int b = q + 4 * (k0 + k);
+      const unsigned o = b < nparts ? (unsigned)((b * C + c) * PS) * 4u : kOOB;
+      v0[k] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(pr, (int)o, 0, 0));
+      v1[k] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(pr, (int)(o + 4u), 0, 0));
+      v2[k] = PS == 3 ? __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(pr, (int)(o + 8u), 0, 0)) : 0.f;
+    }
+#pragma unroll
+    for (int k = 0; k < KB; ++k) {
+      s0 += (double)v0[k];
+      s1 += (double)v1[k];
+      s2 += (double)v2[k];
+    }
+  }
+  red[0][q][ch] = s0;
+  red[1][q][ch] = s1;
+  red[2][q][ch] = s2;
+  __syncthreads();
+  if (q == 0) {
+    const double d0 = (red[0][0][ch] + red[0][1][ch]) + (red[0][2][ch] + red[0][3][ch]);
+    const double d1 = (red[1][0][ch] + red[1][1][ch]) + (red[1][2][ch] + red[1][3][ch]);
+    const double d2 = (red[2][0][ch] + red[2][1][ch]) + (red[2][2][ch] + red[2][3][ch]);
+    const float t0 = (float)d0, t1 = (float)d1;
+    const float invM = 1.f / (float)Mtot;
+    s_k1[ch] = t0 * invM;
+    s_k2[ch] = t1 * invM;
+    if (chunk == 0) {
+      if (gbeta) gbeta[c] = t0;
+      if (ggamma) ggamma[c] = t1;
+      if (gdb) gdb[c] = (float)(-(double)stats[2 * C + c] * d2 * d1 * (1.0 / (double)Mtot));
+    }
+  }
+  __syncthreads();
+  // phase 2: this chunk's rows (pooled windows or pixels), 16 channel quads x 16 row lanes
+  const int cq = tid & 15, rl = tid >> 4;
+  const int n0 = cg * 64 + 4 * cq;
+  const float4 sc = ld4(stats + 2 * C + n0), sh = ld4(stats + 3 * C + n0);
+  const float4 mu = ld4(stats + n0), is = ld4(stats + C + n0);
+  const float4 k1 = make_float4(s_k1[4 * cq], s_k1[4 * cq + 1], s_k1[4 * cq + 2], s_k1[4 * cq + 3]);
+  const float4 k2 = make_float4(s_k2[4 * cq], s_k2[4 * cq + 1], s_k2[4 * cq + 2], s_k2[4 * cq + 3]);
+  const int Ho = pool ? H / 2 : H, Wo = pool ? W / 2 : W;
+  const long long rows = (long long)N * Ho * Wo;
+  const long long per = (rows + chunks - 1) / chunks;
+  const long long r0 = (long long)chunk * per, r1 = min(rows, r0 + per);
+  float am = 0.f;
+  auto emit = [&](long long off, float4 yv, float4 dz) {
+    float4 o;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float xh = (F4GET(yv, e) - F4GET(mu, e)) * F4GET(is, e);
+      const float v = F4GET(sc, e) * (F4GET(dz, e) - F4GET(k1, e) - xh * F4GET(k2, e));
+      if (e == 0) o.x = v;
+      if (e == 1) o.y = v;
+      if (e == 2) o.z = v;
+      if (e == 3) o.w = v;
+    }
+    st4(dy + off, o);
+    am = fmaxf(am, fmaxf(fmaxf(fabsf(o.x), fabsf(o.y)), fmaxf(fabsf(o.z), fabsf(o.w))));
+  };
+  for (long long r = r0 + rl; r < r1; r += 16) {
+    const float4 g = ld4(gout + r * C + n0);
+    if (!pool) {
+      const float4 yv = ld4(y + r * C + n0);
+      const float4 z = affine_act(yv, sc, sh, relu);
+      float4 dz;
+      dz.x = (!relu || z.x > 0.f) ? g.x : 0.f;
+      dz.y = (!relu || z.y > 0.f) ? g.y : 0.f;
+      dz.z = (!relu || z.z > 0.f) ? g.z : 0.f;
+      dz.w = (!relu || z.w > 0.f) ? g.w : 0.f;
+      emit(r * C + n0, yv, dz);
+    } else {
+      const int wo = (int)(r % Wo);
+      const long long t = r / Wo;
+      const int ho = (int)(t % Ho);
+      const int n = (int)(t / Ho);
+      const long long o0 = (((long long)n * H + 2 * ho) * W + 2 * wo) * C + n0;
+      const long long o1 = o0 + C, o2 = o0 + (long long)W * C, o3 = o2 + C;
+      const float4 y0 = ld4(y + o0), y1 = ld4(y + o1), y2 = ld4(y + o2), y3 = ld4(y + o3);
+      const float4 z0 = affine_act(y0, sc, sh, relu), z1 = affine_act(y1, sc, sh, relu),
+                   z2 = affine_act(y2, sc, sh, relu), z3 = affine_act(y3, sc, sh, relu);
+      float4 d0, d1, d2, d3;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float a, b, cc, d;
+        pool_relu_grad(F4GET(z0, e), F4GET(z1, e), F4GET(z2, e), F4GET(z3, e), F4GET(g, e), relu, a, b, cc, d);
+        if (e == 0) { d0.x = a; d1.x = b; d2.x = cc; d3.x = d; }
+        if (e == 1) { d0.y = a; d1.y = b; d2.y = cc; d3.y = d; }
+        if (e == 2) { d0.z = a; d1.z = b; d2.z = cc; d3.z = d; }
+        if (e == 3) { d0.w = a; d1.w = b; d2.w = cc; d3.w = d; }
+      }
+      emit(o0, y0, d0);
+      emit(o1, y1, d1);
+      emit(o2, y2, d2);
+      emit(o3, y3, d3);
+    }
+  }
+  if (amax_part) {
+    __shared__ float ared[4];
+    am = wave_max(am);
+    if ((tid & 63) == 0) ared[tid >> 6] = am;
+    __syncthreads();
+    if (tid == 0) amax_part[blockIdx.x] = fmaxf(fmaxf(ared[0], ared[1]), fmaxf(ared[2], ared[3]));
+  }
+}
+
 int act_grid(long long work_items) {
   long long b = (work_items + 255) / 256;
   if (b > 2048) b = 2048;
@@ -673,6 +811,18 @@ void bn_fin_act_launch(const float* part, int nparts, int rpp, int C, const floa
   hipLaunchKernelGGL(bn_fin_act_kernel, dim3(grid), dim3(256), 0, st, part, nparts, rpp, M, C, gamma, beta,
                      running_mean, running_var, nbt, momentum, eps, stats, y, out, N, H, W, pool ? 1 : 0,
                      relu ? 1 : 0, grid / (C / 64), amax_part);
+}
+
+bool bn_bwd_fin_apply_ok(int nparts, int C, int H, int W, bool pool) {
+  return nparts <= FIN_MAXP && (C % 64) == 0 && !(pool && ((H & 1) || (W & 1)));
+}
+
+void bn_bwd_fin_apply_launch(const float* part, int nparts, int ps, const float* y, const float* gout,
+                             const float* stats, float* dy, float* gbeta, float* ggamma, float* gdb, int N, int H,
+                             int W, int C, bool pool, bool relu, float* amax_part, hipStream_t st) {
+  const int grid = bn_fin_act_grid(N, H, W, C, pool);
+  hipLaunchKernelGGL(bn_bwd_fin_apply_kernel, dim3(grid), dim3(256), 0, st, part, nparts, ps, y, gout, stats, dy,
+                     gbeta, ggamma, gdb, N, H, W, C, pool ? 1 : 0, relu ? 1 : 0, grid / (C / 64), amax_part);
 }
 
 int bn_act_grid(int N, int H, int W, int C, bool pool) {

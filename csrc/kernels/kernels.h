@@ -187,6 +187,13 @@ void bn_fin_act_launch(const float* part, int nparts, int rpp, int C, const floa
                        float* running_mean, float* running_var, long long* nbt, float momentum, float eps,
                        float* stats, const float* y, float* out, int N, int H, int W, bool pool, bool relu,
                        float* amax_part, hipStream_t st);
+// backward twin (training, no residual, nparts <= 128, C % 64 == 0, even map under pooling):
+// finalize the statistics partials (dbeta, dgamma, conv-bias gradient when gdb) and write dy in one
+// launch; amax_part (optional) gets bn_fin_act_grid entries
+bool bn_bwd_fin_apply_ok(int nparts, int C, int H, int W, bool pool);
+void bn_bwd_fin_apply_launch(const float* part, int nparts, int ps, const float* y, const float* gout,
+                             const float* stats, float* dy, float* gbeta, float* ggamma, float* gdb, int N, int H,
+                             int W, int C, bool pool, bool relu, float* amax_part, hipStream_t st);
 // amax_part (optional, bn_act_grid entries): per-block |max| of the written output
 int bn_act_grid(int N, int H, int W, int C, bool pool);
 void bn_act_fwd_launch(const float* y, const float* stats, const float* res, float* out, int N, int H, int W, int C,

@@ -800,6 +800,18 @@ std::vector<at::Tensor> stem_bn_act_fwd(const at::Tensor& x_, const at::Tensor& 
 // ---------------------------------------------------------------- fused block forward
 // out = [maxpool2](act(BN(conv3x3(x) + b) [+ residual])), training or eval BatchNorm.
 // Returns {out, y (conv output), stats [4, C] = (mean, invstd, scale, shift)}.
+// One-launch BN finalize + apply for the layers with few statistics partials: forward
+// bn_fin_act (default; CDP_BN_FIN_ACT=0 selects finalize-then-apply) and backward bn_bwd_fin_apply
+// (opt-in, CDP_BN_BWD_FIN=1). Same-box A/B on MI355X, VGG-11 B=256 hipGraph step, 3 runs each:
+// forward 1.422 vs 1.429 ms (neutral), backward 1.426 vs 1.439 ms (fused 0.9 % slower: every block
+// repeats the partial merge before its first dy store, which costs more than the dispatch it
+// saves). Read per call so a test can compare both paths in one process.
+static bool bn_fin_enabled(bool bwd = false) {
+  const char* e = std::getenv(bwd ? "CDP_BN_BWD_FIN" : "CDP_BN_FIN_ACT");
+  if (bwd) return e && e[0] == '1';
+  return !(e && e[0] == '0');
+}
+
 std::vector<at::Tensor> conv_bn_act_fwd(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tensor>& b,
                                         const c10::optional<at::Tensor>& gamma,
                                         const c10::optional<at::Tensor>& beta,
@@ -838,10 +850,6 @@ std::vector<at::Tensor> conv_bn_act_fwd(const at::Tensor& x, const at::Tensor& w
   hipStream_t st = cur_stream();
   const bool has_res = residual.has_value() && residual->defined();
   // few statistics partials (the deep layers): finalize and apply in one launch (bn_fin_act_kernel)
-  static const bool fin_act_on = [] {
-    const char* e = std::getenv("CDP_BN_FIN_ACT");
-    return !(e && e[0] == '0');
-  }();
   bool fused_fin = false;
   int nparts = 0, rpp = 0;
   long long* nbt = nullptr;
@@ -852,7 +860,7 @@ std::vector<at::Tensor> conv_bn_act_fwd(const at::Tensor& x, const at::Tensor& w
       TORCH_CHECK(num_batches_tracked->scalar_type() == at::kLong, "num_batches_tracked must be int64");
       nbt = reinterpret_cast<long long*>(num_batches_tracked->data_ptr<int64_t>());
     }
-    fused_fin = fin_act_on && bn_fin_act_ok(nparts, C, has_res);
+    fused_fin = bn_fin_enabled() && bn_fin_act_ok(nparts, C, has_res);
     if (!fused_fin)
       bn_finalize_launch(r[1].data_ptr<float>(), nparts, rpp, N * H * W, C, fptr(gamma), fptr(beta),
                          fptr_mut(running_mean), fptr_mut(running_var), nbt, (float)momentum, (float)eps,
@@ -974,16 +982,21 @@ std::vector<at::Tensor> conv_bn_act_bwd(const at::Tensor& gout_, const at::Tenso
   if (has_bias) db = slot(db_out, {C}, false);
   // eval-mode BatchNorm is a fixed affine map: dy = scale * dz (no batch-statistics terms)
   const int dbmode = fused_db ? (training ? 1 : 2) : 0;
-  chan_finalize_launch(part.data_ptr<float>(), nparts, C, sums.data_ptr<float>(), dbeta.data_ptr<float>(),
-                       dgamma.data_ptr<float>(), false, st, ps, fused_db ? db.data_ptr<float>() : nullptr,
-                       stats.data_ptr<float>() + 2 * C, (long long)N * H * W, dbmode);
-  if (!training && dbmode != 2) sums.zero_();
   // RGB stem without an input gradient (VGG layer 0): the weight-gradient kernel applies the
   // BN / ReLU / pool backward on the fly, so dy is never materialised (stem.hip)
   const int cin = (int)x.size(1);
-  if (stem_enabled() && !need_dx && training && pool && relu && !zout.defined() && fused_db && C == 64 &&
-      stem_ok(cin, (int)w.size(2), (int)w.size(3), stride, pad, C) && cin == (int)w.size(1) && (H % 2) == 0 &&
-      (W % 2) == 0) {
+  const bool stem_path = stem_enabled() && !need_dx && training && pool && relu && !zout.defined() && fused_db &&
+                         C == 64 && stem_ok(cin, (int)w.size(2), (int)w.size(3), stride, pad, C) &&
+                         cin == (int)w.size(1) && (H % 2) == 0 && (W % 2) == 0;
+  // few statistics partials (the deep layers): finalize and apply in one launch (bn_bwd_fin_apply_kernel)
+  const bool fused_fin = bn_fin_enabled(true) && training && !stem_path && !zout.defined() && (!has_bias || fused_db) &&
+                         bn_bwd_fin_apply_ok(nparts, C, H, W, pool);
+  if (!fused_fin)
+    chan_finalize_launch(part.data_ptr<float>(), nparts, C, sums.data_ptr<float>(), dbeta.data_ptr<float>(),
+                         dgamma.data_ptr<float>(), false, st, ps, fused_db ? db.data_ptr<float>() : nullptr,
+                         stats.data_ptr<float>() + 2 * C, (long long)N * H * W, dbmode);
+  if (!training && dbmode != 2) sums.zero_();
+  if (stem_path) {
     const at::Tensor xin = nhwc(x);
     const int nb = stem_wgrad_blocks(N, H, W);
     at::Tensor slab = at::empty({nb, C, 36}, opts);
@@ -1003,12 +1016,18 @@ std::vector<at::Tensor> conv_bn_act_bwd(const at::Tensor& gout_, const at::Tenso
   at::Tensor dres;
   if (zout.defined()) dres = at::empty({N, C, H, W}, opts.memory_format(at::MemoryFormat::ChannelsLast));
   at::Tensor dy_amax;  // dy's |max| partials: operand scale of both gradient GEMMs (f16x2)
-  if (f16x2_mode()) dy_amax = at::empty({nblk}, opts);
-  bn_bwd_apply_launch(y.data_ptr<float>(), gout.data_ptr<float>(), stats.data_ptr<float>(), sums.data_ptr<float>(),
-                      dy.data_ptr<float>(), sep_db ? dbpart.data_ptr<float>() : nullptr, nblk, N, H, W, C, pool,
-                      relu, zout.defined() ? zout.data_ptr<float>() : nullptr,
-                      dres.defined() ? dres.data_ptr<float>() : nullptr, st,
-                      dy_amax.defined() ? dy_amax.data_ptr<float>() : nullptr);
+  if (f16x2_mode()) dy_amax = at::empty({fused_fin ? bn_fin_act_grid(N, H, W, C, pool) : nblk}, opts);
+  if (fused_fin)
+    bn_bwd_fin_apply_launch(part.data_ptr<float>(), nparts, ps, y.data_ptr<float>(), gout.data_ptr<float>(),
+                            stats.data_ptr<float>(), dy.data_ptr<float>(), dbeta.data_ptr<float>(),
+                            dgamma.data_ptr<float>(), has_bias ? db.data_ptr<float>() : nullptr, N, H, W, C, pool,
+                            relu, dy_amax.defined() ? dy_amax.data_ptr<float>() : nullptr, st);
+  else
+    bn_bwd_apply_launch(y.data_ptr<float>(), gout.data_ptr<float>(), stats.data_ptr<float>(),
+                        sums.data_ptr<float>(), dy.data_ptr<float>(), sep_db ? dbpart.data_ptr<float>() : nullptr,
+                        nblk, N, H, W, C, pool, relu, zout.defined() ? zout.data_ptr<float>() : nullptr,
+                        dres.defined() ? dres.data_ptr<float>() : nullptr, st,
+                        dy_amax.defined() ? dy_amax.data_ptr<float>() : nullptr);
   const c10::optional<at::Tensor> dya = dy_amax.defined() ? c10::optional<at::Tensor>(dy_amax) : c10::nullopt;
   if (sep_db)
     chan_finalize_launch(dbpart.data_ptr<float>(), nblk, C, nullptr, db.data_ptr<float>(), nullptr, false, st);

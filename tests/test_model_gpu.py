@@ -103,6 +103,45 @@ def test_vgg11_bn_link_backward_matches_unlinked(monkeypatch):
         assert err < 1e-5, (name, err)
 
 
+def test_vgg11_bn_finalize_fusion_matches_two_launch_path(monkeypatch):
+    """One-launch BN finalize + apply (forward bn_fin_act_kernel, default; backward
+    bn_bwd_fin_apply_kernel, opt-in CDP_BN_BWD_FIN=1; both taken by the deep layers with <= 128
+    statistics partials) vs the finalize-then-apply launches: loss and every gradient agree to
+    the rounding of the reordered fp64 partial merges."""
+    import cs744_distributed_data_parallel_amd as cdp
+
+    torch.manual_seed(0)
+    model = cdp.VGG11().cuda()
+    x = torch.randn(64, 3, 32, 32, device="cuda").contiguous(memory_format=torch.channels_last)
+    t = torch.randint(0, 10, (64,), device="cuda")
+    crit = cdp.CrossEntropyLoss()
+
+    def run():
+        model.zero_grad(set_to_none=True)
+        loss = crit(model(x), t)
+        loss.backward()
+        torch.cuda.synchronize()
+        return loss.detach().clone(), [p.grad.detach().clone() for p in model.parameters()]
+
+    monkeypatch.setenv("CDP_BN_FIN_ACT", "1")
+    monkeypatch.setenv("CDP_BN_BWD_FIN", "1")
+    l_f, g_f = run()
+    monkeypatch.setenv("CDP_BN_FIN_ACT", "0")
+    monkeypatch.setenv("CDP_BN_BWD_FIN", "0")
+    l_s, g_s = run()
+    assert abs(l_f.item() - l_s.item()) <= 1e-6 * abs(l_s.item())
+    named = dict(zip([n for n, _ in model.named_parameters()], zip(g_f, g_s)))
+    for name, (a, b) in named.items():
+        conv_bias = name.startswith("layers.") and name.endswith(".bias") and \
+            isinstance(model.layers[int(name.split(".")[1])], torch.nn.Conv2d)
+        if conv_bias:  # analytically zero before training-mode BN: rounding noise
+            beta = named[name.split(".")[0] + "." + str(int(name.split(".")[1]) + 1) + ".bias"][1]
+            assert (a - b).norm() <= 1e-5 * beta.norm(), name
+            continue
+        err = ((a - b).norm() / b.norm().clamp_min(1e-30)).item()
+        assert err < 1e-5, (name, err)
+
+
 def test_vgg11_stem_recompute_matches_stored(monkeypatch):
     """Recompute-mode stem (layer 0's conv output rebuilt from x in the activation pass and both
     backward passes, never stored): the forward is bitwise the stored path's, the layer-0 gradients
