@@ -134,6 +134,36 @@ __device__ __forceinline__ float4 affine_act(float4 y, float4 sc, float4 sh, boo
 // stats and the running statistics; then the block applies [pool2](relu(y*scale + shift)) to its
 // rows. Saves a dependent launch per layer; the redundant merge reads <= 64 KB per block from L2.
 constexpr int FIN_MAXP = 128;
+// A fused-finalize block's row r (pooled window or pixel) of y: the 2x2 window's four pixels (pool)
+// or the pixel in v[0], channels n0..n0+3.
+constexpr int kFinRPT = 4;  // rows per thread loaded before the statistics merge
+__device__ __forceinline__ long long fin_row_off(long long r, int pool, int H, int W, int Ho, int Wo, int C, int n0) {
+  if (!pool) return r * C + n0;
+  const int wo = (int)(r % Wo);
+  const long long t = r / Wo;
+  const int ho = (int)(t % Ho);
+  const int n = (int)(t / Ho);
+  return (((long long)n * H + 2 * ho) * W + 2 * wo) * C + n0;
+}
+__device__ __forceinline__ void fin_load_row(const float* __restrict__ y, float4 (&v)[4], long long r, int pool, int H,
+                                             int W, int Ho, int Wo, int C, int n0) {
+  const float* b = y + fin_row_off(r, pool, H, W, Ho, Wo, C, n0);
+  v[0] = ld4(b);
+  if (pool) {
+    v[1] = ld4(b + C);
+    v[2] = ld4(b + (long long)W * C);
+    v[3] = ld4(b + (long long)W * C + C);
+  }
+}
+// rows ra, ra + 16, ... (the first kFinRPT of this thread); rows past r1 load row 0 (unused)
+__device__ __forceinline__ void fin_prefetch(const float* __restrict__ y, float4 (&pv)[kFinRPT][4], long long ra,
+                                             long long r1, int pool, int H, int W, int Ho, int Wo, int C, int n0) {
+#pragma unroll
+  for (int i = 0; i < kFinRPT; ++i) {
+    const long long r = ra + 16 * i;
+    fin_load_row(y, pv[i], r < r1 ? r : 0, pool, H, W, Ho, Wo, C, n0);
+  }
+}
 __global__ __launch_bounds__(256) void bn_fin_act_kernel(const float* __restrict__ part, int nparts, int rpp, int M,
                                                          int C, const float* __restrict__ gamma,
                                                          const float* __restrict__ beta, float* running_mean,
@@ -149,6 +179,16 @@ __global__ __launch_bounds__(256) void bn_fin_act_kernel(const float* __restrict
   const int tid = threadIdx.x;
   const int ch = tid & 63, q = tid >> 6;
   const int c = cg * 64 + ch;
+  // phase-2 geometry, and this thread's first kFinRPT rows of y loaded before the merge: the y
+  // round trip overlaps the partials' instead of following it
+  const int cq = tid & 15, rl = tid >> 4;
+  const int n0 = cg * 64 + 4 * cq;
+  const int Ho = pool ? H / 2 : H, Wo = pool ? W / 2 : W;
+  const long long rows = (long long)N * Ho * Wo;
+  const long long per = (rows + chunks - 1) / chunks;
+  const long long r0 = (long long)chunk * per, r1 = min(rows, r0 + per);
+  float4 pv[kFinRPT][4];
+  fin_prefetch(y, pv, r0 + rl, r1, pool, H, W, Ho, Wo, C, n0);
   // phase 1: thread (ch, q) merges partials b = q + 4k -- one batch of buffer loads
   // (only the batches of 8 loads that hold partials are issued: kp = ceil(nparts / 4) rounded up to 8)
   constexpr int KP = FIN_MAXP / 4;
@@ -215,35 +255,29 @@ __global__ __launch_bounds__(256) void bn_fin_act_kernel(const float* __restrict
   }
   __syncthreads();
   // phase 2: this chunk's output rows, 16 channel quads x 16 row lanes
-  const int cq = tid & 15, rl = tid >> 4;
-  const int n0 = cg * 64 + 4 * cq;
   const float4 sc = make_float4(s_sc[4 * cq], s_sc[4 * cq + 1], s_sc[4 * cq + 2], s_sc[4 * cq + 3]);
   const float4 sh = make_float4(s_sh[4 * cq], s_sh[4 * cq + 1], s_sh[4 * cq + 2], s_sh[4 * cq + 3]);
-  const int Ho = pool ? H / 2 : H, Wo = pool ? W / 2 : W;
-  const long long rows = (long long)N * Ho * Wo;
-  const long long per = (rows + chunks - 1) / chunks;
-  const long long r0 = (long long)chunk * per, r1 = min(rows, r0 + per);
   float am = 0.f;
-  for (long long r = r0 + rl; r < r1; r += 16) {
-    float4 z;
-    if (!pool) {
-      z = affine_act(ld4(y + r * C + n0), sc, sh, relu);
-    } else {
-      const int wo = (int)(r % Wo);
-      const long long t = r / Wo;
-      const int ho = (int)(t % Ho);
-      const int n = (int)(t / Ho);
-      const float* base = y + (((long long)n * H + 2 * ho) * W + 2 * wo) * C + n0;
-      const float4 z0 = affine_act(ld4(base), sc, sh, relu), z1 = affine_act(ld4(base + C), sc, sh, relu);
-      const float4 z2 = affine_act(ld4(base + (long long)W * C), sc, sh, relu);
-      const float4 z3 = affine_act(ld4(base + (long long)W * C + C), sc, sh, relu);
-      z.x = fmaxf(fmaxf(z0.x, z1.x), fmaxf(z2.x, z3.x));
-      z.y = fmaxf(fmaxf(z0.y, z1.y), fmaxf(z2.y, z3.y));
-      z.z = fmaxf(fmaxf(z0.z, z1.z), fmaxf(z2.z, z3.z));
-      z.w = fmaxf(fmaxf(z0.w, z1.w), fmaxf(z2.w, z3.w));
+  auto emit = [&](long long r, const float4 (&v)[4]) {
+    float4 z = affine_act(v[0], sc, sh, relu);
+    if (pool) {
+      const float4 z1 = affine_act(v[1], sc, sh, relu), z2 = affine_act(v[2], sc, sh, relu),
+                   z3 = affine_act(v[3], sc, sh, relu);
+      z.x = fmaxf(fmaxf(z.x, z1.x), fmaxf(z2.x, z3.x));
+      z.y = fmaxf(fmaxf(z.y, z1.y), fmaxf(z2.y, z3.y));
+      z.z = fmaxf(fmaxf(z.z, z1.z), fmaxf(z2.z, z3.z));
+      z.w = fmaxf(fmaxf(z.w, z1.w), fmaxf(z2.w, z3.w));
     }
     st4(out + r * C + n0, z);
     am = fmaxf(am, fmaxf(fmaxf(fabsf(z.x), fabsf(z.y)), fmaxf(fabsf(z.z), fabsf(z.w))));
+  };
+#pragma unroll
+  for (int i = 0; i < kFinRPT; ++i)
+    if (r0 + rl + 16 * i < r1) emit(r0 + rl + 16 * i, pv[i]);
+  for (long long r = r0 + rl + 16 * kFinRPT; r < r1; r += 16) {
+    float4 v[4];
+    fin_load_row(y, v, r, pool, H, W, Ho, Wo, C, n0);
+    emit(r, v);
   }
   if (amax_part) {
     __shared__ float ared[4];
@@ -639,23 +673,45 @@ __global__ __launch_bounds__(256) void bn_bwd_fin_apply_kernel(
   const int ch = tid & 63, q = tid >> 6;
   const int c = cg * 64 + ch;
   const long long Mtot = (long long)N * H * W;
-  // phase 1: thread (ch, q) sums partials b = q + 4k (one batch of buffer loads, ascending b)
-  // batches of 8 partials per thread (one round trip for nparts <= 32), only as many as there are
-  constexpr int KB = 8;
-  const __amdgpu_buffer_rsrc_t pr = make_rsrc(part, (unsigned)nparts * (unsigned)C * (unsigned)PS * 4u);
-  double s0 = 0.0, s1 = 0.0, s2 = 0.0;
-  for (int k0 = 0; 4 * k0 < nparts; k0 += KB) {
-    float v0[KB], v1[KB], v2[KB];
+  // phase-2 geometry, and this thread's first kFinRPT rows of y and of gout loaded before the
+  // merge (their round trip overlaps the partials')
+  const int cq = tid & 15, rl = tid >> 4;
+  const int n0 = cg * 64 + 4 * cq;
+  const int Ho = pool ? H / 2 : H, Wo = pool ? W / 2 : W;
+  const long long rows = (long long)N * Ho * Wo;
+  const long long per = (rows + chunks - 1) / chunks;
+  const long long r0 = (long long)chunk * per, r1 = min(rows, r0 + per);
+  float4 pv[kFinRPT][4], pg[kFinRPT];
+  fin_prefetch(y, pv, r0 + rl, r1, pool, H, W, Ho, Wo, C, n0);
 #pragma unroll
-    for (int k = 0; k < KB; ++k) {
-      const int b = q + 4 * (k0 + k);
+  for (int i = 0; i < kFinRPT; ++i) {
+    const long long r = r0 + rl + 16 * i;
+    pg[i] = ld4(gout + (r < r1 ? r : 0) * C + n0);
+  }
+  // phase 1: thread (ch, q) sums partials b = q + 4k (one batch of buffer loads, ascending b)
+  // all of this thread's partials in one round trip (issued in groups of 8 up to kp = ceil(nparts /
+  // 4) rounded up to 8; a group loop that summed before loading the next took one round trip per
+  // group: 4 for nparts = 128)
+  constexpr int KP = FIN_MAXP / 4;
+  const int kp = (((nparts + 3) >> 2) + 7) & ~7;
+  const __amdgpu_buffer_rsrc_t pr = make_rsrc(part, (unsigned)nparts * (unsigned)C * (unsigned)PS * 4u);
+  float v0[KP], v1[KP], v2[KP];
+#pragma unroll
+  for (int k0 = 0; k0 < KP; k0 += 8) {
+    if (k0 >= kp) break;
+#pragma unroll
+    for (int k = k0; k < k0 + 8; ++k) {
+      const int b = q + 4 * k;
       const unsigned o = b < nparts ? (unsigned)((b * C + c) * PS) * 4u : kOOB;
       v0[k] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(pr, (int)o, 0, 0));
       v1[k] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(pr, (int)(o + 4u), 0, 0));
       v2[k] = PS == 3 ? __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(pr, (int)(o + 8u), 0, 0)) : 0.f;
     }
+  }
+  double s0 = 0.0, s1 = 0.0, s2 = 0.0;
 #pragma unroll
-    for (int k = 0; k < KB; ++k) {
+  for (int k = 0; k < KP; ++k) {
+    if (q + 4 * k < nparts) {
       s0 += (double)v0[k];
       s1 += (double)v1[k];
       s2 += (double)v2[k];
@@ -681,16 +737,10 @@ __global__ __launch_bounds__(256) void bn_bwd_fin_apply_kernel(
   }
   __syncthreads();
   // phase 2: this chunk's rows (pooled windows or pixels), 16 channel quads x 16 row lanes
-  const int cq = tid & 15, rl = tid >> 4;
-  const int n0 = cg * 64 + 4 * cq;
   const float4 sc = ld4(stats + 2 * C + n0), sh = ld4(stats + 3 * C + n0);
   const float4 mu = ld4(stats + n0), is = ld4(stats + C + n0);
   const float4 k1 = make_float4(s_k1[4 * cq], s_k1[4 * cq + 1], s_k1[4 * cq + 2], s_k1[4 * cq + 3]);
   const float4 k2 = make_float4(s_k2[4 * cq], s_k2[4 * cq + 1], s_k2[4 * cq + 2], s_k2[4 * cq + 3]);
-  const int Ho = pool ? H / 2 : H, Wo = pool ? W / 2 : W;
-  const long long rows = (long long)N * Ho * Wo;
-  const long long per = (rows + chunks - 1) / chunks;
-  const long long r0 = (long long)chunk * per, r1 = min(rows, r0 + per);
   float am = 0.f;
   auto emit = [&](long long off, float4 yv, float4 dz) {
     float4 o;
@@ -706,10 +756,9 @@ __global__ __launch_bounds__(256) void bn_bwd_fin_apply_kernel(
     st4(dy + off, o);
     am = fmaxf(am, fmaxf(fmaxf(fabsf(o.x), fabsf(o.y)), fmaxf(fabsf(o.z), fabsf(o.w))));
   };
-  for (long long r = r0 + rl; r < r1; r += 16) {
-    const float4 g = ld4(gout + r * C + n0);
+  auto row = [&](long long r, const float4 (&v)[4], float4 g) {
     if (!pool) {
-      const float4 yv = ld4(y + r * C + n0);
+      const float4 yv = v[0];
       const float4 z = affine_act(yv, sc, sh, relu);
       float4 dz;
       dz.x = (!relu || z.x > 0.f) ? g.x : 0.f;
@@ -718,13 +767,9 @@ __global__ __launch_bounds__(256) void bn_bwd_fin_apply_kernel(
       dz.w = (!relu || z.w > 0.f) ? g.w : 0.f;
       emit(r * C + n0, yv, dz);
     } else {
-      const int wo = (int)(r % Wo);
-      const long long t = r / Wo;
-      const int ho = (int)(t % Ho);
-      const int n = (int)(t / Ho);
-      const long long o0 = (((long long)n * H + 2 * ho) * W + 2 * wo) * C + n0;
+      const long long o0 = fin_row_off(r, pool, H, W, Ho, Wo, C, n0);
       const long long o1 = o0 + C, o2 = o0 + (long long)W * C, o3 = o2 + C;
-      const float4 y0 = ld4(y + o0), y1 = ld4(y + o1), y2 = ld4(y + o2), y3 = ld4(y + o3);
+      const float4 y0 = v[0], y1 = v[1], y2 = v[2], y3 = v[3];
       const float4 z0 = affine_act(y0, sc, sh, relu), z1 = affine_act(y1, sc, sh, relu),
                    z2 = affine_act(y2, sc, sh, relu), z3 = affine_act(y3, sc, sh, relu);
       float4 d0, d1, d2, d3;
@@ -742,6 +787,14 @@ __global__ __launch_bounds__(256) void bn_bwd_fin_apply_kernel(
       emit(o2, y2, d2);
       emit(o3, y3, d3);
     }
+  };
+#pragma unroll
+  for (int i = 0; i < kFinRPT; ++i)
+    if (r0 + rl + 16 * i < r1) row(r0 + rl + 16 * i, pv[i], pg[i]);
+  for (long long r = r0 + rl + 16 * kFinRPT; r < r1; r += 16) {
+    float4 v[4];
+    fin_load_row(y, v, r, pool, H, W, Ho, Wo, C, n0);
+    row(r, v, ld4(gout + r * C + n0));
   }
   if (amax_part) {
     __shared__ float ared[4];
@@ -798,7 +851,8 @@ bool bn_fin_act_ok(int nparts, int C, bool residual) { return !residual && npart
 int bn_fin_act_grid(int N, int H, int W, int C, bool pool) {
   const long long rows = (long long)N * (pool ? (H / 2) * (W / 2) : H * W);
   const int ngroups = C / 64;
-  long long chunks = std::max<long long>(1, std::min<long long>((rows + 31) / 32, 512 / ngroups));
+  // >= 16 rows per chunk (one per row lane), <= 512 blocks (each repeats the partial merge)
+  long long chunks = std::max<long long>(1, std::min<long long>((rows + 15) / 16, 512 / ngroups));
   return (int)(chunks * ngroups);
 }
 

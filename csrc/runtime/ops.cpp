@@ -802,10 +802,11 @@ std::vector<at::Tensor> stem_bn_act_fwd(const at::Tensor& x_, const at::Tensor& 
 // Returns {out, y (conv output), stats [4, C] = (mean, invstd, scale, shift)}.
 // One-launch BN finalize + apply for the layers with few statistics partials: forward
 // bn_fin_act (default; CDP_BN_FIN_ACT=0 selects finalize-then-apply) and backward bn_bwd_fin_apply
-// (opt-in, CDP_BN_BWD_FIN=1). Same-box A/B on MI355X, VGG-11 B=256 hipGraph step, 3 runs each:
-// forward 1.422 vs 1.429 ms (neutral), backward 1.426 vs 1.439 ms (fused 0.9 % slower: every block
-// repeats the partial merge before its first dy store, which costs more than the dispatch it
-// saves). Read per call so a test can compare both paths in one process.
+// (opt-in, CDP_BN_BWD_FIN=1). Both load their first rows of y (and gout) before merging the
+// partials, so the two round trips overlap. Same-box A/B on MI355X, VGG-11 B=256 hipGraph step:
+// forward 1.399 vs 1.407 ms (fused 0.6 % faster, two boxes agree); backward 1.409 vs 1.404 ms
+// (fused 0.35 % slower, within noise, so it stays opt-in). Read per call so a test can compare
+// both paths in one process.
 static bool bn_fin_enabled(bool bwd = false) {
   const char* e = std::getenv(bwd ? "CDP_BN_BWD_FIN" : "CDP_BN_FIN_ACT");
   if (bwd) return e && e[0] == '1';
