@@ -105,15 +105,15 @@ def test_vgg11_bn_link_backward_matches_unlinked(monkeypatch):
 
 def test_vgg11_bn_finalize_fusion_matches_two_launch_path(monkeypatch):
     """One-launch BN finalize + apply (forward bn_fin_act_kernel, default; backward
-    bn_bwd_fin_apply_kernel, opt-in CDP_BN_BWD_FIN=1; both taken by the deep layers with <= 128
-    statistics partials) vs the finalize-then-apply launches: loss and every gradient agree to
-    the rounding of the reordered fp64 partial merges."""
+    bn_bwd_fin_apply_kernel, opt-in CDP_BN_BWD_FIN=1; both taken by the layers with few statistics
+    partials) vs the finalize-then-apply launches: loss and every gradient agree to
+    the rounding of the reordered fp64 partial merges (B=256: the fused layers are 4-7)."""
     import cs744_distributed_data_parallel_amd as cdp
 
     torch.manual_seed(0)
     model = cdp.VGG11().cuda()
-    x = torch.randn(64, 3, 32, 32, device="cuda").contiguous(memory_format=torch.channels_last)
-    t = torch.randint(0, 10, (64,), device="cuda")
+    x = torch.randn(256, 3, 32, 32, device="cuda").contiguous(memory_format=torch.channels_last)
+    t = torch.randint(0, 10, (256,), device="cuda")
     crit = cdp.CrossEntropyLoss()
 
     def run():
