@@ -146,9 +146,7 @@ class DeviceLoader:
         self.ds, self.batch_size, self.sampler, self.shuffle = dataset, batch_size, sampler, shuffle
         self.train, self.drop_last, self.seed = train, drop_last, seed
         self.dev = dataset.images.device
-        # [step, arrivals]: on the GPU the augment kernel's last workgroup advances the step itself
-        # (no increment launch per batch); element 0 is the step everywhere
-        self._counter = torch.zeros(2, dtype=torch.int64, device=self.dev)
+        self._counter = torch.zeros(1, dtype=torch.int64, device=self.dev)
         self._epoch = 0
 
     def _order(self) -> torch.Tensor:
@@ -184,18 +182,19 @@ class DeviceLoader:
             target = torch.empty(bsz, dtype=torch.int64, device=self.dev)
             data = C.augment(self.ds.images, idx, offset, bsz, self.ds.mean, self.ds.std, pad, flip, self._counter,
                              self.seed, out, nbatches, self.ds.labels, target)
+            C.counter_inc(self._counter)
             return data, target
         if nbatches > 0:
-            offset += (int(self._counter[0].item()) % nbatches) * bsz
+            offset += (int(self._counter.item()) % nbatches) * bsz
             if not pad:
-                self._counter[0] += 1  # (the padded path advances it itself)
+                self._counter += 1  # (the padded path advances it itself)
         return self._cpu_batch(idx[offset : offset + bsz], pad, flip)
 
     def _cpu_batch(self, sel, pad, flip):
         imgs = self.ds.images.index_select(0, sel).permute(0, 3, 1, 2).float().div_(255.0)  # NCHW
         if pad:
-            g = torch.Generator().manual_seed(self.seed * 1000003 + int(self._counter[0].item()))
-            self._counter[0] += 1
+            g = torch.Generator().manual_seed(self.seed * 1000003 + int(self._counter.item()))
+            self._counter += 1
             B, C, H, W = imgs.shape
             padded = torch.nn.functional.pad(imgs, (pad, pad, pad, pad))
             out = torch.empty_like(imgs)

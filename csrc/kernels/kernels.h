@@ -218,9 +218,9 @@ void sgd_launch(float* p, const float* g, float* buf, long long n, const float* 
                 hipStream_t st);
 // nbatches > 0: batch offset idx_off + (counter % nbatches) * B; labels_out[b] = labels[idx[...]] when given
 void augment_launch(const unsigned char* imgs, const long long* idx, long long idx_off, int B, int H, int W, int C,
-                    const float* mean, const float* inv_std, int pad, bool flip, long long* counter,
+                    const float* mean, const float* inv_std, int pad, bool flip, const long long* counter,
                     unsigned long long seed, float* out, hipStream_t st, long long nbatches = 0,
-                    const long long* labels = nullptr, long long* labels_out = nullptr, bool advance = false);
+                    const long long* labels = nullptr, long long* labels_out = nullptr);
 void counter_inc_launch(long long* c, hipStream_t st);
 void wtrans_launch(const float* w, float* wt, int Co, int T, int Ci, hipStream_t st);
 // sub-filter transpose: wt[ci][a][b][co] = w[co][kh0 + 2a][kw0 + 2b][ci] (a < nkh, b < nkw)

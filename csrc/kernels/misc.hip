@@ -177,11 +177,12 @@ __global__ __launch_bounds__(256) void augment_kernel(const unsigned char* __res
                                                      const long long* __restrict__ idx, long long idx_off, int B,
                                                      int H, int W, int C, float m0, float m1, float m2, float is0,
                                                      float is1, float is2, int pad, int flip,
-                                                     long long* counter, unsigned long long seed,
+                                                     const long long* __restrict__ counter, unsigned long long seed,
                                                      float* __restrict__ out, long long nbatches,
                                                      const long long* __restrict__ labels,
-                                                     long long* __restrict__ labels_out, int advance) {
-  const int b = blockIdx.y;  // < B (grid.y == B)
+                                                     long long* __restrict__ labels_out) {
+  const int b = blockIdx.y;
+  if (b >= B) return;
   const unsigned long long ctr = counter ? (unsigned long long)counter[0] : 0ull;
   // nbatches > 0: the batch offset into idx follows the step counter, so a replayed hipGraph walks
   // the epoch order without a host-side index copy per step
@@ -209,20 +210,6 @@ __global__ __launch_bounds__(256) void augment_kernel(const unsigned char* __res
       const float v = in ? (float)sp[c] * (1.f / 255.f) : 0.f;
       const int ci = c < 3 ? c : 2;
       dst[(long long)px * C + c] = (v - mean[ci]) * istd[ci];
-    }
-  }
-  // advance (counter = {step, arrivals}): the last block to arrive moves the step counter on, so no
-  // separate increment launch follows. Every block arrives only after all its threads have read
-  // counter[0], so no block can see the new value; the arrival count is reset for the next launch.
-  if (advance) {
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      const unsigned total = gridDim.x * gridDim.y;
-      const unsigned prev = atomicAdd(reinterpret_cast<unsigned*>(counter + 1), 1u);
-      if (prev == total - 1) {
-        counter[1] = 0;
-        counter[0] = (long long)ctr + 1;
-      }
     }
   }
 }
@@ -602,13 +589,13 @@ void sgd_launch(float* p, const float* g, float* buf, long long n, const float* 
                      dampening, wd, grad_scale, flags);
 }
 void augment_launch(const unsigned char* imgs, const long long* idx, long long idx_off, int B, int H, int W, int C,
-                    const float* mean, const float* inv_std, int pad, bool flip, long long* counter,
+                    const float* mean, const float* inv_std, int pad, bool flip, const long long* counter,
                     unsigned long long seed, float* out, hipStream_t st, long long nbatches,
-                    const long long* labels, long long* labels_out, bool advance) {
+                    const long long* labels, long long* labels_out) {
   dim3 grid((H * W + 255) / 256, B);
   hipLaunchKernelGGL(augment_kernel, grid, dim3(256), 0, st, imgs, idx, idx_off, B, H, W, C, mean[0], mean[1],
                      mean[2], inv_std[0], inv_std[1], inv_std[2], pad, flip ? 1 : 0, counter, seed, out, nbatches,
-                     labels, labels_out, (advance && counter) ? 1 : 0);
+                     labels, labels_out);
 }
 void counter_inc_launch(long long* c, hipStream_t st) {
   hipLaunchKernelGGL(counter_inc_kernel, dim3(1), dim3(1), 0, st, c);

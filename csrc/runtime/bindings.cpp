@@ -60,8 +60,7 @@ PYBIND11_MODULE(_C, m) {
         py::arg("out") = py::none(), py::arg("nbatches") = 0, py::arg("labels") = py::none(),
         py::arg("labels_out") = py::none(),
         "gather + RandomCrop + flip + normalize one batch (NHWC fp32); nbatches > 0 takes the batch offset from "
-        "the step counter; labels_out receives the batch's labels; a 2-element counter [step, arrivals] is "
-        "advanced by the kernel itself");
+        "the step counter; labels_out receives the batch's labels");
   m.def("counter_inc", &counter_inc);
   m.def("stack_mean", &stack_mean);
   m.def("scale_", &scale_);

@@ -1260,15 +1260,8 @@ at::Tensor augment(const at::Tensor& images, const c10::optional<at::Tensor>& in
   }
   const long long* ip = nullptr;
   if (indices.has_value() && indices->defined()) ip = reinterpret_cast<const long long*>(indices->data_ptr<int64_t>());
-  // counter: [step] (the caller advances it) or [step, arrivals] (the kernel's last block advances it)
-  long long* cp = nullptr;
-  bool advance = false;
-  if (counter.has_value() && counter->defined()) {
-    TORCH_CHECK(counter->scalar_type() == at::kLong && counter->is_cuda() && counter->is_contiguous(),
-                "counter must be a contiguous int64 GPU tensor");
-    cp = reinterpret_cast<long long*>(counter->data_ptr<int64_t>());
-    advance = counter->numel() >= 2;
-  }
+  const long long* cp = nullptr;
+  if (counter.has_value() && counter->defined()) cp = reinterpret_cast<const long long*>(counter->data_ptr<int64_t>());
   TORCH_CHECK(nbatches == 0 || cp, "counter-driven batch offsets need the counter");
   const long long* lp = nullptr;
   long long* lo = nullptr;
@@ -1280,7 +1273,7 @@ at::Tensor augment(const at::Tensor& images, const c10::optional<at::Tensor>& in
     lo = reinterpret_cast<long long*>(labels_out->data_ptr<int64_t>());
   }
   augment_launch(images.data_ptr<uint8_t>(), ip, idx_offset, (int)batch, H, W, C, m, is, (int)pad, flip, cp,
-                 (unsigned long long)seed, o.data_ptr<float>(), cur_stream(), nbatches, lp, lo, advance);
+                 (unsigned long long)seed, o.data_ptr<float>(), cur_stream(), nbatches, lp, lo);
   return o;
 }
 
