@@ -75,7 +75,13 @@ def test_two_ranks_on_one_gpu_strategy_equivalence():
     for s, per_rank in outs.items():
         (f0, l0, _), (f1, l1, _) = per_rank
         np.testing.assert_allclose(f0, f1, rtol=0, atol=1e-6, err_msg=f"{s}: ranks diverged")
-        np.testing.assert_allclose(f0, ref_flat, rtol=1e-4, atol=2e-5, err_msg=f"{s} != allreduce_blocking")
+        # strategies average in different orders (per-tensor SUM then /W, bucketed ncclAvg-style,
+        # gather + stack_mean): 1-ulp gradient differences that 3 steps through ReLU masks and
+        # max-pool argmaxes can amplify in a handful of elements (seen: 1.1e-4 in 0.012 % of them),
+        # so the model-level check is a global relative L2 norm plus a loose elementwise bound
+        rel = float(np.linalg.norm(f0 - ref_flat) / np.linalg.norm(ref_flat))
+        assert rel < 1e-5, (s, rel)
+        np.testing.assert_allclose(f0, ref_flat, rtol=1e-3, atol=1e-3, err_msg=f"{s} != allreduce_blocking")
         np.testing.assert_allclose(l0, ref_losses, rtol=1e-4, err_msg=f"{s} losses")
     info = outs["ddp"][0][2]
     assert info["native_reducer"], info
