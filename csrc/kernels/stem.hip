@@ -104,13 +104,13 @@ __device__ __forceinline__ void stem_y_mfma(const float (&lo)[9][2], const float
         acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x2f32(hi[t][a], wl[32 * b + i][4 * t + 2 + h], acc[a][b], 0, 0, 0);
       }
 }
-// LDS barrier that does not wait for global loads or stores still in flight: workgroup-scope
-// fences restricted to LDS ("local") order the LDS accesses around the barrier for the compiler and
-// emit only s_waitcnt lgkmcnt(0) -- __syncthreads' fences would also drain vmcnt
+// LDS barrier that does not wait for global loads still in flight (lgkmcnt(0) only; vmcnt and
+// expcnt fields left at their maximum) -- __syncthreads' fence would drain them. (A variant built
+// from LDS-only workgroup fences around s_barrier made the two-rank strategy-equivalence test fail
+// in 2 of 3 runs -- results no longer deterministic -- and was reverted; this form passes 3 of 3.)
 __device__ __forceinline__ void lds_barrier() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_s_waitcnt(0xc07f);
   __builtin_amdgcn_s_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
 }
 
 // ---------------------------------------------------------------------------------- forward
