@@ -14,6 +14,7 @@
 //   conv bias gradient.
 // All element kernels move float4 along C (C % 4 == 0).
 #include <algorithm>
+#include <cstdlib>
 
 #include "common.h"
 #include "kernels.h"
@@ -155,15 +156,19 @@ __device__ __forceinline__ void fin_load_row(const float* __restrict__ y, float4
     v[3] = ld4(b + (long long)W * C + C);
   }
 }
-// rows ra, ra + 16, ... (the first kFinRPT of this thread); rows past r1 load row 0 (unused)
+// rows ra, ra + rs, ... (the first kFinRPT of this thread); rows past r1 load row 0 (unused)
 __device__ __forceinline__ void fin_prefetch(const float* __restrict__ y, float4 (&pv)[kFinRPT][4], long long ra,
-                                             long long r1, int pool, int H, int W, int Ho, int Wo, int C, int n0) {
+                                             long long r1, int pool, int H, int W, int Ho, int Wo, int C, int n0,
+                                             int rs = 16) {
 #pragma unroll
   for (int i = 0; i < kFinRPT; ++i) {
-    const long long r = ra + 16 * i;
+    const long long r = ra + rs * i;
     fin_load_row(y, pv[i], r < r1 ? r : 0, pool, H, W, Ho, Wo, C, n0);
   }
 }
+// CG channels per block: 64 (4 merge threads per channel) or 16 (16 merge threads per channel: a
+// quarter of the merge work per thread, 4x the blocks repeating it)
+template <int CG>
 __global__ __launch_bounds__(256) void bn_fin_act_kernel(const float* __restrict__ part, int nparts, int rpp, int M,
                                                          int C, const float* __restrict__ gamma,
                                                          const float* __restrict__ beta, float* running_mean,
@@ -172,27 +177,30 @@ __global__ __launch_bounds__(256) void bn_fin_act_kernel(const float* __restrict
                                                          const float* __restrict__ y, float* __restrict__ out, int N,
                                                          int H, int W, int pool, int relu, int chunks,
                                                          float* __restrict__ amax_part) {
-  __shared__ double red[4][64];
-  __shared__ float s_sc[64], s_sh[64];
-  const int ngroups = C >> 6;
+  constexpr int TQ = 256 / CG;  // merge threads per channel
+  constexpr int CQ = CG / 4;    // phase 2: channel quads x RL row lanes
+  constexpr int RL = 256 / CQ;
+  __shared__ double red[TQ][CG];
+  __shared__ float s_sc[CG], s_sh[CG];
+  const int ngroups = C / CG;
   const int cg = blockIdx.x % ngroups, chunk = blockIdx.x / ngroups;
   const int tid = threadIdx.x;
-  const int ch = tid & 63, q = tid >> 6;
-  const int c = cg * 64 + ch;
+  const int ch = tid % CG, q = tid / CG;
+  const int c = cg * CG + ch;
   // phase-2 geometry, and this thread's first kFinRPT rows of y loaded before the merge: the y
   // round trip overlaps the partials' instead of following it
-  const int cq = tid & 15, rl = tid >> 4;
-  const int n0 = cg * 64 + 4 * cq;
+  const int cq = tid % CQ, rl = tid / CQ;
+  const int n0 = cg * CG + 4 * cq;
   const int Ho = pool ? H / 2 : H, Wo = pool ? W / 2 : W;
   const long long rows = (long long)N * Ho * Wo;
   const long long per = (rows + chunks - 1) / chunks;
   const long long r0 = (long long)chunk * per, r1 = min(rows, r0 + per);
   float4 pv[kFinRPT][4];
-  fin_prefetch(y, pv, r0 + rl, r1, pool, H, W, Ho, Wo, C, n0);
-  // phase 1: thread (ch, q) merges partials b = q + 4k -- one batch of buffer loads
-  // (only the batches of 8 loads that hold partials are issued: kp = ceil(nparts / 4) rounded up to 8)
-  constexpr int KP = FIN_MAXP / 4;
-  const int kp = (((nparts + 3) >> 2) + 7) & ~7;
+  fin_prefetch(y, pv, r0 + rl, r1, pool, H, W, Ho, Wo, C, n0, RL);
+  // phase 1: thread (ch, q) merges partials b = q + TQ k -- one batch of buffer loads
+  // (only the batches of 8 loads that hold partials are issued: kp = ceil(nparts / TQ) rounded up to 8)
+  constexpr int KP = FIN_MAXP / TQ;
+  const int kp = (((nparts + TQ - 1) / TQ) + 7) & ~7;
   float pm[KP], pq[KP];
   const __amdgpu_buffer_rsrc_t pr = make_rsrc(part, (unsigned)nparts * (unsigned)C * 8u);
 #pragma unroll
@@ -200,7 +208,7 @@ __global__ __launch_bounds__(256) void bn_fin_act_kernel(const float* __restrict
     if (k0 >= kp) break;
 #pragma unroll
     for (int k = k0; k < k0 + 8; ++k) {
-      const int b = q + 4 * k;
+      const int b = q + TQ * k;
       const unsigned o = b < nparts ? (unsigned)(b * C + c) * 8u : kOOB;
       const auto v = __builtin_amdgcn_raw_buffer_load_b64(pr, (int)o, 0, 0);
       pm[k] = __uint_as_float(v[0]);
@@ -210,17 +218,20 @@ __global__ __launch_bounds__(256) void bn_fin_act_kernel(const float* __restrict
   double sm = 0.0;
 #pragma unroll
   for (int k = 0; k < KP; ++k) {
-    const int b = q + 4 * k;
+    const int b = q + TQ * k;
     if (b < nparts) sm += (double)min(rpp, M - b * rpp) * (double)pm[k];
   }
   red[q][ch] = sm;
   __syncthreads();
-  const double mean = (red[0][ch] + red[1][ch] + red[2][ch] + red[3][ch]) / (double)M;
+  double tot = 0.0;
+#pragma unroll
+  for (int t = 0; t < TQ; ++t) tot += red[t][ch];
+  const double mean = tot / (double)M;
   __syncthreads();
   double sq = 0.0;
 #pragma unroll
   for (int k = 0; k < KP; ++k) {
-    const int b = q + 4 * k;
+    const int b = q + TQ * k;
     if (b < nparts) {
       const double d = (double)pm[k] - mean;
       sq += (double)pq[k] + (double)min(rpp, M - b * rpp) * d * d;
@@ -229,7 +240,9 @@ __global__ __launch_bounds__(256) void bn_fin_act_kernel(const float* __restrict
   red[q][ch] = sq;
   __syncthreads();
   if (q == 0) {
-    const double m2 = red[0][ch] + red[1][ch] + red[2][ch] + red[3][ch];
+    double m2 = 0.0;
+#pragma unroll
+    for (int t = 0; t < TQ; ++t) m2 += red[t][ch];
     const double var = m2 / (double)M;
     const float invstd = (float)(1.0 / sqrt(var + (double)eps));
     const float g = gamma ? gamma[c] : 1.f;
@@ -273,8 +286,8 @@ __global__ __launch_bounds__(256) void bn_fin_act_kernel(const float* __restrict
   };
 #pragma unroll
   for (int i = 0; i < kFinRPT; ++i)
-    if (r0 + rl + 16 * i < r1) emit(r0 + rl + 16 * i, pv[i]);
-  for (long long r = r0 + rl + 16 * kFinRPT; r < r1; r += 16) {
+    if (r0 + rl + RL * i < r1) emit(r0 + rl + RL * i, pv[i]);
+  for (long long r = r0 + rl + RL * kFinRPT; r < r1; r += RL) {
     float4 v[4];
     fin_load_row(y, v, r, pool, H, W, Ho, Wo, C, n0);
     emit(r, v);
@@ -848,11 +861,22 @@ void bn_eval_stats_launch(int C, const float* gamma, const float* beta, const fl
 
 bool bn_fin_act_ok(int nparts, int C, bool residual) { return !residual && nparts <= FIN_MAXP && (C % 64) == 0; }
 
-int bn_fin_act_grid(int N, int H, int W, int C, bool pool) {
+// channels per fused-finalize block: 16 above CDP_FIN_CG16 partials (default 32), else 64
+static int fin_cg(int nparts) {
+  static const int t = [] {
+    const char* e = std::getenv("CDP_FIN_CG16");
+    return e ? std::atoi(e) : 32;
+  }();
+  return nparts > t ? 16 : 64;
+}
+
+int bn_fin_act_grid(int N, int H, int W, int C, bool pool, int nparts) {
   const long long rows = (long long)N * (pool ? (H / 2) * (W / 2) : H * W);
-  const int ngroups = C / 64;
-  // >= 16 rows per chunk (one per row lane), <= 512 blocks (each repeats the partial merge)
-  long long chunks = std::max<long long>(1, std::min<long long>((rows + 15) / 16, 512 / ngroups));
+  const int cg = nparts > 0 ? fin_cg(nparts) : 64;
+  const int ngroups = C / cg;
+  const int rl = 1024 / cg;  // row lanes per block
+  // >= one row per row lane, <= 512 blocks (each repeats the partial merge)
+  long long chunks = std::max<long long>(1, std::min<long long>((rows + rl - 1) / rl, 512 / ngroups));
   return (int)(chunks * ngroups);
 }
 
@@ -860,11 +884,12 @@ void bn_fin_act_launch(const float* part, int nparts, int rpp, int C, const floa
                        float* running_mean, float* running_var, long long* nbt, float momentum, float eps,
                        float* stats, const float* y, float* out, int N, int H, int W, bool pool, bool relu,
                        float* amax_part, hipStream_t st) {
-  const int grid = bn_fin_act_grid(N, H, W, C, pool);
+  const int grid = bn_fin_act_grid(N, H, W, C, pool, nparts);
   const int M = N * H * W;
-  hipLaunchKernelGGL(bn_fin_act_kernel, dim3(grid), dim3(256), 0, st, part, nparts, rpp, M, C, gamma, beta,
-                     running_mean, running_var, nbt, momentum, eps, stats, y, out, N, H, W, pool ? 1 : 0,
-                     relu ? 1 : 0, grid / (C / 64), amax_part);
+  const int cg = fin_cg(nparts);
+  hipLaunchKernelGGL(cg == 64 ? bn_fin_act_kernel<64> : bn_fin_act_kernel<16>, dim3(grid), dim3(256), 0, st, part,
+                     nparts, rpp, M, C, gamma, beta, running_mean, running_var, nbt, momentum, eps, stats, y, out, N,
+                     H, W, pool ? 1 : 0, relu ? 1 : 0, grid / (C / cg), amax_part);
 }
 
 bool bn_bwd_fin_apply_ok(int nparts, int C, int H, int W, bool pool) {

@@ -182,7 +182,7 @@ void bn_eval_stats_launch(int C, const float* gamma, const float* beta, const fl
 // finalize + apply in one launch (training, no residual, nparts <= 128, C % 64 == 0); amax_part
 // (optional) gets bn_fin_act_grid entries
 bool bn_fin_act_ok(int nparts, int C, bool residual);
-int bn_fin_act_grid(int N, int H, int W, int C, bool pool);
+int bn_fin_act_grid(int N, int H, int W, int C, bool pool, int nparts = 0);  // nparts 0: 64-channel blocks
 void bn_fin_act_launch(const float* part, int nparts, int rpp, int C, const float* gamma, const float* beta,
                        float* running_mean, float* running_var, long long* nbt, float momentum, float eps,
                        float* stats, const float* y, float* out, int N, int H, int W, bool pool, bool relu,

@@ -880,7 +880,8 @@ std::vector<at::Tensor> conv_bn_act_fwd(const at::Tensor& x, const at::Tensor& w
                              opts.memory_format(at::MemoryFormat::ChannelsLast));
   at::Tensor out_amax;  // the output's |max| partials: the next conv's operand scale (f16x2)
   if (f16x2_mode())
-    out_amax = at::empty({fused_fin ? bn_fin_act_grid(N, H, W, C, pool) : bn_act_grid(N, H, W, C, pool)}, opts);
+    out_amax = at::empty({fused_fin ? bn_fin_act_grid(N, H, W, C, pool, nparts) : bn_act_grid(N, H, W, C, pool)},
+                         opts);
   if (fused_fin)
     bn_fin_act_launch(r[1].data_ptr<float>(), nparts, rpp, C, fptr(gamma), fptr(beta), fptr_mut(running_mean),
                       fptr_mut(running_var), nbt, (float)momentum, (float)eps, stats.data_ptr<float>(),
