@@ -841,7 +841,12 @@ int bn_bwd_grid(int N, int H, int W, int C, bool pool) {
   const long long rows = b;
   b = (b + 1) / 2;
   if (b < 256) b = rows < 256 ? rows : 256;
-  if (b > 1024) b = 1024;
+  static const long long cap = [] {  // CDP_BN_BWD_MAXBLK: workgroup cap (partial rows), default 1024
+    const char* e = std::getenv("CDP_BN_BWD_MAXBLK");
+    const long long v = e ? std::atoll(e) : 1024;
+    return v < 256 ? 256 : v > 4096 ? 4096 : v;
+  }();
+  if (b > cap) b = cap;
   if (b < 1) b = 1;
   return (int)b;
 }
