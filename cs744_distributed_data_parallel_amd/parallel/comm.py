@@ -218,11 +218,22 @@ class TorchCommunicator(Communicator):
         w = tdist.reduce(t, dst, op=_TORCH_OPS[_norm_op(op)], group=self.group, async_op=async_op)
         return Work(torch_work=w) if async_op else None
 
+    def _gloo_device_fence(self, t):
+        # gloo on device tensors (the one-GPU multi-rank rehearsal): its host staging copies run on
+        # gloo's own streams; a device-wide sync around the blocking gather / scatter keeps the
+        # consumer kernels (stack_mean, SGD) from ever seeing a buffer before its copy lands
+        if t.is_cuda and tdist.get_backend(self.group) == "gloo":
+            torch.cuda.synchronize(t.device)
+
     def gather(self, t, gather_list=None, dst=0):
+        self._gloo_device_fence(t)
         tdist.gather(t, gather_list if self.rank == dst else None, dst=dst, group=self.group)
+        self._gloo_device_fence(t)
 
     def scatter(self, t, scatter_list=None, src=0):
+        self._gloo_device_fence(t)
         tdist.scatter(t, scatter_list if self.rank == src else None, src=src, group=self.group)
+        self._gloo_device_fence(t)
 
     def all_gather(self, out, t, async_op=False):
         w = tdist.all_gather_into_tensor(out, t, group=self.group, async_op=async_op)
