@@ -117,7 +117,7 @@ def launch(args) -> int:
 class _Run:
     """Builds model/optimizer/data for one (local batch, sync on/off) point and times it."""
 
-    def __init__(self, args, world, rank, dev, local_batch, sync_grads=True):
+    def __init__(self, args, world, rank, dev, local_batch, sync_grads=True, model_name=None):
         import torch
 
         import cs744_distributed_data_parallel_amd as cdp
@@ -132,7 +132,8 @@ class _Run:
         self.args, self.world, self.dev, self.local_batch = args, world, dev, local_batch
         self.sync_grads = sync_grads and world > 1
         cdp.utils.seed_everything(0)
-        self.imagenet = args.model.startswith("resnet")
+        model_name = model_name or args.model
+        self.imagenet = model_name.startswith("resnet")
         size = args.dataset_size if dev.type == "cuda" else min(args.dataset_size, 8 * local_batch)
         size = max(size, local_batch * world)  # at least one batch per rank
         if self.imagenet:  # BASELINE.json config #5: ResNet-50, ImageNet-shaped synthetic
@@ -144,7 +145,7 @@ class _Run:
         strategy = args.strategy
         self.sync = None
         if args.backend == "native":
-            model = cdp.get_model(args.model).to(dev)
+            model = cdp.get_model(model_name).to(dev)
             if world > 1 and strategy == "ddp":
                 model = cdp.DistributedDataParallel(model, bucket_cap_mb=args.bucket_cap_mb)
             if world > 1 and strategy == "bucketed_overlap":
@@ -153,7 +154,7 @@ class _Run:
             self.crit = cdp.CrossEntropyLoss()
         else:
             os.environ["CDP_FORCE_REFERENCE"] = "1"
-            model = cdp.get_model(args.model).to(dev).to(memory_format=torch.channels_last)
+            model = cdp.get_model(model_name).to(dev).to(memory_format=torch.channels_last)
             if world > 1:
                 model = torch.nn.parallel.DistributedDataParallel(
                     model, device_ids=[dev.index] if dev.type == "cuda" else None)
@@ -163,7 +164,12 @@ class _Run:
         self.order = self.loader._order()
         self.nb = max(1, self.order.numel() // local_batch)
         self.graph = None
-        self.break_capture = os.environ.get("CDP_BENCH_BREAK_CAPTURE") == "1"  # recovery test hook
+        self.graph_collectives = None  # native-communicator collectives recorded in the captured step
+        # test hooks: CDP_BENCH_BREAK_CAPTURE=1 (every rank) or =r (rank r only) invalidates the capture;
+        # CDP_BENCH_CORRUPT_RANK=r perturbs rank r's gradient after the sync (replicas then diverge)
+        bc = os.environ.get("CDP_BENCH_BREAK_CAPTURE")
+        self.break_capture = bc == "1" if world == 1 else bc in ("all", str(rank))
+        self.corrupt = os.environ.get("CDP_BENCH_CORRUPT_RANK") == str(rank) and world > 1
 
     def body(self):
         import contextlib
@@ -182,6 +188,8 @@ class _Run:
             cdp.parallel.average_gradients_allreduce(self.model)
         elif self.sync_grads and strategy == "gather_scatter":
             cdp.parallel.average_gradients_gather_scatter(self.model)
+        if self.corrupt:
+            next(self.model.parameters()).grad.narrow(0, 0, 1).add_(1e-3)
         self.opt.step()
         if self.break_capture and self.torch.cuda.is_current_stream_capturing():
             loss.item()  # test hook: a host read of a captured value invalidates the capture
@@ -200,6 +208,9 @@ class _Run:
         # failing mid-capture would leave its peer blocked in the collective): eager steps
         if self.args.no_graph or not cuda or self.args.dist_backend == "gloo":
             return
+        from cs744_distributed_data_parallel_amd import distributed as D
+
+        ok = True
         try:
             s = torch.cuda.Stream()
             s.wait_stream(torch.cuda.current_stream())
@@ -211,6 +222,7 @@ class _Run:
             g = torch.cuda.CUDAGraph()
             cs = torch.cuda.Stream()
             cs.wait_stream(torch.cuda.current_stream())
+            n0 = D.collective_counts()
             with torch.cuda.stream(cs):
                 # thread-local capture mode: a failing rank's other threads (watchdog, autograd
                 # workers) cannot invalidate it, and ending it below always leaves capture mode
@@ -221,29 +233,37 @@ class _Run:
                     g.capture_end()
             torch.cuda.current_stream().wait_stream(cs)
             torch.cuda.synchronize()
-            for i in range(2):  # warm replays
-                g.replay()
-            torch.cuda.synchronize()
+            n1 = D.collective_counts()
+            if n0 is not None and n1 is not None:
+                self.graph_collectives = n1["captured"] - n0["captured"]
             self.graph = g
             dbg("captured")
         except Exception as e:  # pragma: no cover - depends on the runtime
             print(f"[bench] hipGraph capture failed ({str(e)[:200]!r}); timing eager steps", file=sys.stderr)
+            ok = False
             self.graph = None
             self._recover_from_failed_capture()
         if self.world > 1:
-            # all ranks replay graphs or all run eager (a capture records collectives without running
-            # them, so dropping every rank's graph after one rank's failure keeps the order matched)
+            # all ranks replay graphs or all run eager. Agreed BEFORE any replay: a replay runs the
+            # recorded collectives, which a rank that could not capture would never join (capture
+            # itself records them without running them, so dropping every graph keeps the order)
             import torch.distributed as tdist
 
             store = tdist.distributed_c10d._get_default_store()
             _Run._gen = getattr(_Run, "_gen", 0) + 1
             keys = [f"cdp_bench_graph/{_Run._gen}/{r}" for r in range(self.world)]
-            store.set(keys[tdist.get_rank()], "1" if self.graph is not None else "0")
+            store.set(keys[tdist.get_rank()], "1" if ok else "0")
             store.wait(keys)
             if any(store.get(k) != b"1" for k in keys) and self.graph is not None:
                 print("[bench] another rank could not capture; all ranks time eager steps", file=sys.stderr)
                 self.graph.reset()
                 self.graph = None
+                self.graph_collectives = None
+                self.opt.zero_grad()
+        if self.graph is not None:
+            for i in range(2):  # warm replays
+                self.graph.replay()
+            torch.cuda.synchronize()
 
     def _recover_from_failed_capture(self):
         """An invalidated capture leaves the thread's last HIP error set (the next launch would report
@@ -282,6 +302,26 @@ class _Run:
             dist.all_reduce(el_t, "max")  # the slowest rank defines the step
         return float(el_t.item()) / steps * 1e3
 
+    def replica_digest(self):
+        """Exact digest of this replica's training state: the int64 sum of the parameters' and the
+        momentum buffers' fp32 bit patterns (order-independent, bit-exact) and their fp64 sum. DDP's
+        invariant (``/root/reference/src/Part 3/main.py:61,96-97``) is that every rank holds the same
+        parameters after every step; BN running statistics are per-rank between forwards (DDP
+        broadcasts them from rank 0 at the next forward) and are not part of the digest."""
+        torch = self.torch
+        ts = [p.detach() for p in self.model.parameters()]
+        for p in self.model.parameters():
+            st = self.opt.state.get(p) if hasattr(self.opt, "state") else None
+            if st and st.get("momentum_buffer") is not None:
+                ts.append(st["momentum_buffer"].detach())
+        bits = torch.zeros((), dtype=torch.int64, device=self.dev)
+        val = torch.zeros((), dtype=torch.float64, device=self.dev)
+        for t in ts:
+            t = t.contiguous().reshape(-1)
+            bits += t.view(torch.int32).to(torch.int64).sum()
+            val += t.to(torch.float64).sum()
+        return torch.stack([bits, val.view(torch.int64)])
+
     def release(self):
         if self.graph is not None:
             self.graph.reset()
@@ -292,6 +332,17 @@ class _Run:
         if self.sync is not None:
             self.sync.remove()
             self.sync = None
+
+
+def _measure(args, world, rank, dev, lb, dbg, dist, steps=None, warmup=None, **kw):
+    """ms/step of one more (local batch, model, sync) point, measured like the headline."""
+    r = _Run(args, world, rank, dev, lb, **kw)
+    r.prepare(args.warmup if warmup is None else warmup, dbg)
+    ms = r.time(args.steps if steps is None else steps, dist)
+    hg = r.graph is not None
+    r.release()
+    del r
+    return ms, hg
 
 
 def rank_main(args) -> int:
@@ -354,46 +405,60 @@ def rank_main(args) -> int:
     run.prepare(args.warmup, dbg)
     ms = run.time(args.steps, dist)
     hipgraph = run.graph is not None
+    graph_collectives = run.graph_collectives
+    replicas_identical = None
+    if world > 1:
+        # every rank's parameters + momentum after the timed steps must be bit-identical
+        dg = run.replica_digest()
+        allg = [torch.empty_like(dg) for _ in range(world)]
+        dist.all_gather(allg, dg)
+        replicas_identical = all(torch.equal(allg[0].cpu(), a.cpu()) for a in allg)
     run.release()
     del run
 
     extra = {}
     if world > 1 and not args.no_extra:
-        nos = _Run(args, world, rank, dev, main_lb, sync_grads=False)
-        nos.prepare(args.warmup, dbg)
-        ms_nosync = nos.time(args.steps, dist)
-        nos.release()
-        del nos
+        ms_nosync, _ = _measure(args, world, rank, dev, main_lb, dbg, dist, sync_grads=False)
         extra["ms_per_step_no_sync"] = round(ms_nosync, 4)
         extra["exposed_comm_ms"] = round(max(0.0, ms - ms_nosync), 4)
         other_lb = strong_lb if args.scaling == "weak" else args.local_batch
         if other_lb != main_lb:
-            oth = _Run(args, world, rank, dev, other_lb, sync_grads=True)
-            oth.prepare(args.warmup, dbg)
-            ms_o = oth.time(args.steps, dist)
-            oth.release()
-            del oth
+            ms_o, _ = _measure(args, world, rank, dev, other_lb, dbg, dist)
             key = "strong" if args.scaling == "weak" else "weak"
             extra[key] = {"value": round(other_lb * world / ms_o * 1e3, 1), "ms_per_step": round(ms_o, 4),
                           "global_batch": other_lb * world, "local_batch": other_lb}
 
     engine = "reference" if cpu else _conv_gemm_engine(args.backend)
-    if (world == 1 and not args.no_extra and not cpu and args.backend == "native" and args.precision == "fp32"
-            and engine == "f16x2"):
+    headline = (world == 1 and not args.no_extra and not cpu and args.backend == "native" and args.precision == "fp32"
+                and args.model == "vgg11")
+    if headline and engine == "f16x2":
         # the same step on the strict engine (3-term bf16 split: every conv GEMM output within the
         # fp32 per-element error bound, tests/test_accuracy_gpu.py), so both numbers are measured here
         C = cdp._native.lib()
         C.set_conv_gemm("x3")
         try:
-            sx = _Run(args, world, rank, dev, main_lb, sync_grads=True)
-            sx.prepare(args.warmup, dbg)
-            ms_x3 = sx.time(args.steps, dist)
-            sx.release()
-            del sx
+            ms_x3, _ = _measure(args, world, rank, dev, main_lb, dbg, dist)
         finally:
             C.set_conv_gemm(engine)
         extra["strict_fp32"] = {"conv_gemm": "x3", "value": round(main_lb * world / ms_x3 * 1e3, 1),
                                 "ms_per_step": round(ms_x3, 4)}
+    if headline and args.local_batch == REF_GLOBAL_BATCH:
+        # the reference's strong-scaling rule (int(256 / W) images per rank,
+        # /root/reference/src/Part 2a/main.py:22): the per-GPU step of its W = 2 / 4 / 8 points,
+        # measured here on one GPU (no gradient sync: what the W-rank run costs before communication)
+        pts = []
+        for w_ref in (2, 4, 8):
+            lb = REF_GLOBAL_BATCH // w_ref
+            ms_s, hg = _measure(args, 1, rank, dev, lb, dbg, dist, steps=max(args.steps, 20))
+            pts.append({"reference_world_size": w_ref, "local_batch": lb, "ms_per_step": round(ms_s, 4),
+                        "img_s_per_gpu": round(lb / ms_s * 1e3, 1), "hipgraph": hg})
+        extra["per_gpu_strong"] = pts
+        # BASELINE.json config #5 (ResNet-50, ImageNet-shaped, 64 images per GPU), one GPU
+        ms_r, hg = _measure(args, 1, rank, dev, 64, dbg, dist, steps=min(args.steps, 10), warmup=3,
+                            model_name="resnet50")
+        extra["resnet50"] = {"local_batch": 64, "image_shape": [3, 224, 224], "ms_per_step": round(ms_r, 3),
+                             "value": round(64 / ms_r * 1e3, 1), "unit": "images/sec", "hipgraph": hg,
+                             "conv_gemm": engine}
 
     global_batch = main_lb * world
     img_s = global_batch / ms * 1e3
@@ -417,6 +482,7 @@ def rank_main(args) -> int:
                      "synthetic (random uint8 CIFAR-10-shaped 32x32x3, GPU-resident, on-GPU crop/flip/normalize); ")
                     + "random-init weights",
             "ranks_seen": ranks_seen,
+            "replicas_identical": replicas_identical,
             "config": {
                 "model": {"vgg11": "VGG-11", "resnet50": "ResNet-50"}.get(args.model, args.model),
                 "global_batch": global_batch,
@@ -426,6 +492,10 @@ def rank_main(args) -> int:
                 "parallelism": f"dp{world}",
                 "strategy": args.strategy if world > 1 else "single",
                 "comm": comm_kind,
+                "comm_fallback_reason": dist.comm_fallback_reason() if world > 1 else None,
+                # native-communicator collectives recorded inside the captured step (replayed every
+                # step); null when the step is not captured or collectives go through torch
+                "graph_collectives": graph_collectives if hipgraph else None,
                 "backend": args.backend,
                 "device": "cpu" if cpu else "mi355x",
                 "hipgraph": hipgraph,
@@ -442,6 +512,9 @@ def rank_main(args) -> int:
     if world > 1:
         dist.destroy_process_group()
     faulthandler.cancel_dump_traceback_later()
+    if replicas_identical is False:
+        print(f"[bench] rank {rank}: replicas diverged after the timed steps", file=sys.stderr)
+        return 3
     return 0
 
 

@@ -52,6 +52,11 @@ def require(*tensors) -> bool:
     return on_gpu
 
 
+def import_error() -> str | None:
+    _load()
+    return None if _err is None else repr(_err)
+
+
 def so_path() -> str | None:
     m = _load()
     return getattr(m, "__file__", None) if m is not None else None

@@ -30,7 +30,7 @@ __all__ = [
     "ReduceOp", "reduce_op", "init_process_group", "destroy_process_group", "is_initialized", "get_rank",
     "get_world_size", "get_local_rank", "get_backend", "all_reduce", "broadcast", "gather", "scatter", "all_gather",
     "all_gather_into_tensor", "reduce_scatter_tensor", "reduce", "barrier", "communicator_for", "device",
-    "set_timeout", "healthy", "ranks_seen",
+    "set_timeout", "healthy", "ranks_seen", "comm_fallback_reason", "collective_counts",
 ]
 
 
@@ -61,6 +61,7 @@ class _State:
     host: Optional[TorchCommunicator] = None
     device: Optional[torch.device] = None
     local_rank: int = 0
+    fallback_reason: Optional[str] = None  # why the native communicator is not in use (CDP_RCCL_FALLBACK)
 
 
 _S = _State()
@@ -104,6 +105,7 @@ def _init_native_rccl(rank, world_size, local, store, timeout_s) -> Optional[Rcc
     if os.environ.get("CDP_RCCL_FALLBACK", "0") != "1":
         raise RuntimeError(msg + "; set CDP_RCCL_FALLBACK=1 to run every rank on the torch nccl process group")
     warnings.warn(msg + "; all ranks use the torch nccl process group")
+    _S.fallback_reason = msg
     return None
 
 
@@ -125,6 +127,7 @@ def init_process_group(
     if world_size < 0:
         world_size = int(os.environ.get("WORLD_SIZE", "1"))
     timeout = timeout or datetime.timedelta(minutes=30)
+    _S.fallback_reason = None
     if backend in ("rccl", "nccl"):
         local = _local_rank(rank) if device_id is None else int(device_id)
         torch.cuda.set_device(local)
@@ -135,6 +138,8 @@ def init_process_group(
             store = tdist.distributed_c10d._get_default_store()
             t = comm_timeout_s if comm_timeout_s is not None else timeout.total_seconds()
             _S.rccl = _init_native_rccl(rank, world_size, local, store, t)
+        elif backend == "rccl":
+            _S.fallback_reason = "native extension not importable: " + (_native.import_error() or "unknown")
     elif backend == "gloo":
         tdist.init_process_group("gloo", init_method=init_method, rank=rank, world_size=world_size, timeout=timeout)
         _S.device = torch.device("cpu")
@@ -194,6 +199,20 @@ def communicator_for(t: Optional[torch.Tensor] = None) -> Communicator:
 
 def native_communicator() -> Optional[RcclCommunicator]:
     return _S.rccl
+
+
+def comm_fallback_reason() -> Optional[str]:
+    """Why tensor collectives run on torch's nccl group instead of the native communicator (None when
+    the native communicator is up, or when a non-rccl backend was asked for)."""
+    return _S.fallback_reason
+
+
+def collective_counts() -> Optional[dict]:
+    """{"captured": n, "eager": n}: native-communicator collectives enqueued inside / outside a
+    hipGraph capture so far (None without the native communicator)."""
+    if _S.rccl is None:
+        return None
+    return {"captured": int(_S.rccl.native.captured_collectives()), "eager": int(_S.rccl.native.eager_collectives())}
 
 
 def ranks_seen() -> int:

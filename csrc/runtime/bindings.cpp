@@ -96,6 +96,8 @@ PYBIND11_MODULE(_C, m) {
       .def("set_test_postop", &RcclComm::set_test_postop, py::arg("delay_us"), py::arg("scale"),
            "test hook: delay + scale after every all_reduce, inside its completion event")
       .def("timeout", &RcclComm::timeout)
+      .def("captured_collectives", &RcclComm::captured_collectives)
+      .def("eager_collectives", &RcclComm::eager_collectives)
       .def("all_reduce", &RcclComm::all_reduce, py::arg("t"), py::arg("op") = "sum", py::arg("async_op") = false)
       .def("broadcast", &RcclComm::broadcast, py::arg("t"), py::arg("root") = 0, py::arg("async_op") = false)
       .def("reduce", &RcclComm::reduce, py::arg("t"), py::arg("root") = 0, py::arg("op") = "sum",

@@ -196,6 +196,7 @@ std::shared_ptr<RcclWork> RcclComm::end(hipStream_t cur, bool async, std::vector
   hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
   hipStreamIsCapturing(cur, &cs);
   const bool captured = cs != hipStreamCaptureStatusNone;
+  (captured ? n_captured_ : n_eager_).fetch_add(1);
   if (!async) {
     HIP_CHECK(hipStreamWaitEvent(cur, ev->ev, 0));
   } else if (!captured) {

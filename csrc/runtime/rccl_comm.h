@@ -62,6 +62,10 @@ class RcclComm : public std::enable_shared_from_this<RcclComm> {
   void abort(const std::string& why);
   void set_timeout(double s) { timeout_s_ = s; }
   double timeout() const { return timeout_s_.load(); }
+  // collectives enqueued while the caller's stream was being captured into a hipGraph (they run
+  // at every replay), and collectives enqueued eagerly
+  long long captured_collectives() const { return n_captured_.load(); }
+  long long eager_collectives() const { return n_eager_.load(); }
   void shutdown();
 
   std::shared_ptr<RcclWork> all_reduce(at::Tensor t, const std::string& op, bool async);
@@ -115,6 +119,7 @@ class RcclComm : public std::enable_shared_from_this<RcclComm> {
   std::thread wd_thread_;
   std::atomic<bool> stop_{false};
   std::atomic<bool> failed_{false};
+  std::atomic<long long> n_captured_{0}, n_eager_{0};
   std::atomic<double> timeout_s_;
   mutable std::mutex err_mu_;
   std::string err_;

@@ -314,6 +314,9 @@ def test_bench_self_launches_ranks_cpu():
     assert rec["config"]["parallelism"] == "dp2" and rec["config"]["global_batch"] == 8
     assert rec["strong"]["global_batch"] == 256 and rec["strong"]["local_batch"] == 128
     assert rec["exposed_comm_ms"] >= 0 and rec["value"] > 0
+    # self-verification: every rank holds the same parameters + momentum after the timed steps
+    assert rec["replicas_identical"] is True
+    assert rec["config"]["comm_fallback_reason"] is None and rec["config"]["graph_collectives"] is None
 
 
 @pytest.mark.parametrize("strategy", ["gather_scatter", "allreduce_blocking", "bucketed_overlap"])
@@ -325,6 +328,7 @@ def test_bench_every_strategy_through_the_launcher_cpu(strategy):
     assert r.returncode == 0, r.stderr[-3000:]
     rec = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
     assert rec["ranks_seen"] == 2 and rec["config"]["strategy"] == strategy
+    assert rec["replicas_identical"] is True
 
 
 def test_bench_failing_rank_fails_the_launcher():
@@ -332,3 +336,15 @@ def test_bench_failing_rank_fails_the_launcher():
                 "--dataset-size", "16", "--no-extra"], env_extra={"CDP_BENCH_FAIL_RANK": "1"})
     assert r.returncode != 0
     assert not [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+
+
+@pytest.mark.parametrize("strategy", ["ddp", "allreduce_blocking"])
+def test_bench_detects_diverged_replicas(strategy):
+    """One rank's gradient perturbed after the sync (CDP_BENCH_CORRUPT_RANK=1): the replicas differ
+    after the timed steps, the record says so and the run fails (a broken reducer cannot produce a
+    pretty number)."""
+    r = _bench(["--gpus", "2", "--device", "cpu", "--strategy", strategy, "--steps", "1", "--warmup", "1",
+                "--local-batch", "2", "--dataset-size", "16", "--no-extra"], env_extra={"CDP_BENCH_CORRUPT_RANK": "1"})
+    assert r.returncode != 0
+    rec = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    assert rec["replicas_identical"] is False
