@@ -177,6 +177,9 @@ class DeviceLoader:
         """
         pad = self.ds.pad if self.train else 0
         flip = self.train
+        if offset < 0 or offset + max(nbatches, 1) * bsz > idx.numel():
+            raise ValueError(f"DeviceLoader.batch: offset {offset} + {max(nbatches, 1)} batches x {bsz} exceeds the "
+                             f"{idx.numel()} indices of this shard")
         if self.dev.type == "cuda":
             C = _native.lib()
             target = torch.empty(bsz, dtype=torch.int64, device=self.dev)

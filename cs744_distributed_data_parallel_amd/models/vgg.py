@@ -18,8 +18,6 @@ On CPU tensors the plain ``nn.Sequential`` path runs (reference semantics).
 """
 from __future__ import annotations
 
-import os
-
 import torch
 import torch.nn as nn
 
@@ -82,28 +80,9 @@ class VGG(nn.Module):
             # (the first conv's input needs no gradient: no transpose)
             need = [k > 0 or x.requires_grad for k in range(len(self._plan))]
             weights = [layers[ci].weight for ci, _, _ in self._plan]
-            # the RGB stem needs neither output of the weight preparation, so the preparation can
-            # run on a side stream beside it (a parallel branch under hipGraph capture). Opt-in
-            # (CDP_WPREP_SIDE=1): measured on MI355X the fork/join costs more than it hides (VGG-11
-            # B=256: 1.440 -> 1.495 ms/step), like every parallel graph branch tried (docs/PERF.md)
-            ci0, bi0, _ = self._plan[0]
-            stem = (x.size(1) <= 4 and layers[bi0].training and tuple(layers[ci0].kernel_size) == (3, 3)
-                    and layers[ci0].stride[0] == 1 and layers[ci0].padding[0] == 1 and layers[ci0].out_channels == 64
-                    and os.environ.get("CDP_STEM", "1") != "0")
-            side = _prep_stream() if stem and os.environ.get("CDP_WPREP_SIDE", "0") == "1" else None
-            if side is not None:
-                cur = torch.cuda.current_stream()
-                side.wait_stream(cur)
-                with torch.cuda.stream(side):
-                    wam, wts = CF.weight_prep(weights, need)
-                for t in (wam or []) + [t for t in wts if t is not None]:
-                    t.record_stream(cur)
-            else:
-                wam, wts = CF.weight_prep(weights, need)
+            wam, wts = CF.weight_prep(weights, need)
             last = len(self._plan) - 1
             for k, (ci, bi, pool) in enumerate(self._plan):
-                if k == 1 and side is not None:
-                    torch.cuda.current_stream().wait_stream(side)
                 # each block's output feeds only the next block: its BN statistics reduction rides
                 # on that block's backward (CF.conv_bn_act bn_link)
                 x = CF.conv_bn_act(x, layers[ci], layers[bi], relu=True, pool=pool,
@@ -113,16 +92,6 @@ class VGG(nn.Module):
         y = self.layers(x)
         y = y.reshape(y.size(0), -1)
         return self.fc1(y)
-
-
-_PREP_STREAMS = {}
-
-
-def _prep_stream():
-    dev = torch.cuda.current_device()
-    if dev not in _PREP_STREAMS:
-        _PREP_STREAMS[dev] = torch.cuda.Stream(dev)
-    return _PREP_STREAMS[dev]
 
 
 def VGG11(**kw):

@@ -115,13 +115,17 @@ class _BNLink:
     L+1. Block L+1's backward, whose data-gradient reduction produces the gradient at block L's
     output anyway, also reduces block L's BatchNorm statistics from it in the same launch
     (csrc/kernels/bwd_fuse.hip) and leaves them in ``part``; block L's backward then skips its own
-    statistics pass. ``gptr`` pins the hand-off to that exact gradient tensor."""
+    statistics pass. ``gptr`` / ``gver`` pin the hand-off to that exact gradient tensor, unmodified
+    (autograd accumulating a second consumer's gradient into it in place bumps its version), and
+    ``consumers`` counts the fused blocks that read the tagged output: with two, neither takes the
+    link and the producer reduces its own statistics."""
 
-    __slots__ = ("y", "stats", "pool", "relu", "ps", "part", "gptr")
+    __slots__ = ("y", "stats", "pool", "relu", "ps", "part", "gptr", "gver", "consumers")
 
     def __init__(self, y, stats, pool, relu, ps):
         self.y, self.stats, self.pool, self.relu, self.ps = y, stats, pool, relu, ps
-        self.part, self.gptr = None, None
+        self.part, self.gptr, self.gver = None, None, None
+        self.consumers = 0
 
 
 LINK_HANDOFFS = [0]  # BN statistics reductions taken from the consumer block's backward (tests read it)
@@ -139,11 +143,9 @@ class _ConvBNAct(torch.autograd.Function):
     def forward(ctx, x, w, b, gamma, beta, rm, rv, nbt, momentum, eps, training, stride, pad, pool, relu, residual,
                 res_sink=None, dx_sink=None, w_amax=None, w_t=None, bn_link=False):
         C = _native.lib()
-        # an RGB stem whose input needs no gradient may rebuild its conv output from x in backward
-        # instead of storing it (the stem kernels then return a storage-less y, stride 0)
         out, y, stats, xsave, out_amax, x_amax, w_amax = C.conv_bn_act_fwd(
             x, w, b, gamma, beta, rm, rv, nbt, momentum, eps, training, stride, pad, pool, relu, residual, _get_amax(x),
-            w_amax, not x.requires_grad and _stem_recompute_on(),
+            w_amax,
         )
         ctx.cfg = (stride, pad, pool, relu, training, b is not None, residual is not None)
         ctx.params = (w, b, gamma, beta)
@@ -153,10 +155,12 @@ class _ConvBNAct(torch.autograd.Function):
         zout = out if residual is not None else None
         ctx.save_for_backward(xsave, w, y, stats, zout)  # xsave: x, or x zero-padded to 4k channels
         _set_amax(out, out_amax)
-        # the producer of x handed over its BN (see _BNLink); this block is its only consumer
+        # the producer of x handed over its BN (see _BNLink) if this block is its only consumer
         ctx.link_in = _get_link(x) if dx_sink is None else None
+        if ctx.link_in is not None:
+            ctx.link_in.consumers += 1
         ctx.link_out = None
-        if bn_link and residual is None and _bwd_fuse_on() and y.stride(0) != 0:
+        if bn_link and residual is None and _bwd_fuse_on():
             odd_pool = pool and (y.shape[2] % 2 == 1 or y.shape[3] % 2 == 1)
             ps = 3 if (b is not None and not odd_pool and training) else 2  # as conv_bn_act_bwd's
             ctx.link_out = _BNLink(y, stats, pool, relu, ps)
@@ -179,13 +183,14 @@ class _ConvBNAct(torch.autograd.Function):
                 addend, dx_sink.grad = dx_sink.grad, None
         part_in, lo = None, ctx.link_out
         if lo is not None:
-            if lo.part is not None and lo.gptr == gout.data_ptr():
+            if (lo.part is not None and lo.consumers == 1 and lo.gptr == gout.data_ptr()
+                    and lo.gver == gout._version):
                 part_in = lo.part
                 LINK_HANDOFFS[0] += 1
-            lo.part = lo.gptr = None
+            lo.part = lo.gptr = lo.gver = None
         li = ctx.link_in
         prev = (None, None, False, False, 2)
-        if li is not None and nig[0] and not park_dx and addend is None:
+        if li is not None and li.consumers == 1 and nig[0] and not park_dx and addend is None:
             prev = (li.y, li.stats, li.pool, li.relu, li.ps)
         dx, dw, db, dgamma, dbeta, dres, prev_part = C.conv_bn_act_bwd(
             gout, x, w, y, stats, stride, pad, pool, relu, nig[0], has_bias, zout, training,
@@ -196,6 +201,7 @@ class _ConvBNAct(torch.autograd.Function):
         if li is not None:
             li.part = prev_part if (prev_part is not None and dx is not None) else None
             li.gptr = dx.data_ptr() if li.part is not None else None
+            li.gver = dx._version if li.part is not None else None
             ctx.link_in = None
         if park_dx:
             dx_sink.grad, dx = dx, None
@@ -221,16 +227,6 @@ def _bwd_fuse_on() -> bool:
     import os
 
     return os.environ.get("CDP_BWD_FUSE", "1") != "0"
-
-
-def _stem_recompute_on() -> bool:
-    """Opt-in (CDP_STEM_RECOMPUTE=1): the RGB stem rebuilds its 67 MB (VGG-11, B=256) conv output
-    from the 3 MB input in its activation pass and in both backward passes instead of storing it.
-    Measured on MI355X it ties the stored path (1.448-1.454 vs 1.452-1.455 ms/step): each rebuild
-    costs a full exact-fp32 MFMA pass (~9 us) against the ~11 us of HBM traffic it saves."""
-    import os
-
-    return os.environ.get("CDP_STEM_RECOMPUTE", "0") == "1"
 
 
 def conv_bn_act(x, conv, bn, relu: bool = True, pool: bool = False, residual=None, res_sink=None, dx_sink=None,

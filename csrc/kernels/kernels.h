@@ -130,17 +130,6 @@ void slab_sum_strided_launch(const float* slab, int S, long long n_src, int src_
 bool stem_ok(int Cin, int KH, int KW, int stride, int pad, int Co);
 void stem_fwd_launch(const float* x, const float* w, const float* bias, float* y, float* part, int N, int H, int W,
                      int Cin, int Co, hipStream_t st);
-// recompute mode (pool + ReLU stems; whole 256-pixel chunks of 2x2-window rows): y is never
-// stored -- the forward's second pass and both backward passes rebuild it from x (bitwise the same)
-bool stem_recompute_ok(int N, int H, int W);
-void stem_act_launch(const float* x, const float* w, const float* bias, const float* stats, float* out,
-                     float* amax_part, int N, int H, int W, int Cin, hipStream_t st);  // amax: M / 256 partials
-int stem_bnstat_parts(int N, int H, int W);
-void stem_bnstat_launch(const float* x, const float* w, const float* bias, const float* gout, const float* stats,
-                        float* part, int ps, int N, int H, int W, int Cin, hipStream_t st);
-int stem_wgrad_rc_blocks(int N, int H, int W);
-void stem_wgrad_rc_launch(const float* x, const float* w, const float* bias, const float* gout, const float* stats,
-                          const float* sums, float* slab, int nblk, int N, int H, int W, int Cin, hipStream_t st);
 int stem_wgrad_blocks(int N, int H, int W);
 // dW partials [nblk][64][36] with the pool(2x2)/ReLU/BatchNorm(training) backward applied on the fly;
 // Co = 64, even H and W

@@ -27,8 +27,7 @@ namespace {
 
 
 // ---------------------------------------------------------------------------------- y tile
-// The 256-pixel x 64-channel conv tile shared by every stem kernel, so a recomputed tile is
-// bitwise the forward's: 4 waves of 64 pixels x 64 channels (2 x 2 tiles of 32 x 32). K = 9 taps x
+// The 256-pixel x 64-channel conv tile: 4 waves of 64 pixels x 64 channels (2 x 2 tiles of 32 x 32). K = 9 taps x
 // 4 channels = 36 = 18 MFMA steps of k = 2; per tap a lane feeds two channels of its pixel (k even /
 // odd half of the wave).
 //
@@ -104,13 +103,15 @@ __device__ __forceinline__ void stem_y_mfma(const float (&lo)[9][2], const float
         acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x2f32(hi[t][a], wl[32 * b + i][4 * t + 2 + h], acc[a][b], 0, 0, 0);
       }
 }
-// LDS barrier that does not wait for global loads still in flight (lgkmcnt(0) only; vmcnt and
-// expcnt fields left at their maximum) -- __syncthreads' fence would drain them. (A variant built
-// from LDS-only workgroup fences around s_barrier made the two-rank strategy-equivalence test fail
-// in 2 of 3 runs -- results no longer deterministic -- and was reverted; this form passes 3 of 3.)
+// LDS barrier that does not wait for global loads still in flight: __syncthreads' fence would
+// drain them (vmcnt(0)). The release / acquire fences are workgroup-scope and LDS-only
+// ("local" address space), so they order the LDS stores before the barrier and the LDS loads after
+// it in the compiler's memory model (a bare s_barrier is not a memory operation to LLVM, so nothing
+// would stop an LDS access from being scheduled across it) while lowering to lgkmcnt(0) alone.
 __device__ __forceinline__ void lds_barrier() {
-  __builtin_amdgcn_s_waitcnt(0xc07f);
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
   __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
 }
 
 // ---------------------------------------------------------------------------------- forward
@@ -191,7 +192,6 @@ __global__ __launch_bounds__(256, 2) void stem_fwd_kernel(const float* __restric
       }
     }
   }
-  if (!y) return;  // recompute mode: the consumers rebuild y from x
   // y (lane: column i of each 32-wide tile, 16 rows): one base address per lane, the 64 stores at
   // compile-time offsets
   float* yb = y + (long long)(m0 + 4 * h) * Co + i;
@@ -211,182 +211,6 @@ __global__ __launch_bounds__(256, 2) void stem_fwd_kernel(const float* __restric
         for (int r = 0; r < 16; ++r)
           if (m0 + 32 * a + (r & 3) + 8 * (r >> 2) + 4 * h < M)
             yb[(32 * a + (r & 3) + 8 * (r >> 2)) * Co + 32 * b] = acc[a][b][r];
-  }
-}
-
-// Recompute mode (pool + ReLU, 256 pixels = whole 2x2-window rows of one image): the y tile goes
-// through the LDS image yt[256][YLD] instead of memory.
-constexpr int YLD = 68;  // 16-B aligned rows for the float4 window reads
-
-// acc (this wave's 64 rows of the tile) -> yt rows, optionally as relu(y * scale + shift)
-__device__ __forceinline__ void stem_tile_to_lds(const f32x16 (&acc)[2][2], float (*yt)[YLD], const float* sc,
-                                                 const float* sh) {
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, i = lane & 31, h = lane >> 5;
-#pragma unroll
-  for (int b = 0; b < 2; ++b) {
-    const float s = sc ? sc[32 * b + i] : 1.f, t = sh ? sh[32 * b + i] : 0.f;
-#pragma unroll
-    for (int a = 0; a < 2; ++a)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const float v = acc[a][b][r];
-        yt[wv * 64 + 32 * a + (r & 3) + 8 * (r >> 2) + 4 * h][32 * b + i] = sc ? fmaxf(fmaf(v, s, t), 0.f) : v;
-      }
-  }
-}
-
-// chunk-local 2x2 window wl (64 per 256-pixel chunk) -> its top-left local pixel and its index in the
-// pooled output map
-struct StemWin {
-  int px;
-  int pooled;
-};
-__device__ __forceinline__ StemWin stem_window(int m0, int wl, int H, int W) {
-  const int Wo = W >> 1, Ho = H >> 1;
-  const int pr = wl / Wo, pc = wl - pr * Wo;
-  const int n = m0 / (H * W), h0 = (m0 - n * H * W) / W;
-  return StemWin{2 * pr * W + 2 * pc, (n * Ho + (h0 >> 1) + pr) * Wo + pc};
-}
-
-// out = maxpool2(relu(BN(conv(x) + b))) from x directly (the forward's second pass), plus the
-// per-block |max| of out (the next conv's f16x2 operand scale)
-__global__ __launch_bounds__(256, 2) void stem_act_kernel(const float* __restrict__ x, const float* __restrict__ w,
-                                                       const float* __restrict__ bias,
-                                                       const float* __restrict__ stats, float* __restrict__ out,
-                                                       float* __restrict__ amax_part, int N, int H, int W, int Cin) {
-  __shared__ float wl[64][37];
-  __shared__ __attribute__((aligned(16))) float yt[256][YLD];
-  const int tid = threadIdx.x, wv = tid >> 6;
-  const int M = N * H * W;
-  const int m0 = blockIdx.x * 256;
-  float wv9[9];
-  stem_w_issue(w, Cin, wv9);
-  float lo[9][2], hi[9][2];
-  stem_x_issue(make_rsrc(x, (unsigned)((long long)M * Cin * 4)), m0 + wv * 64, M, H, W, Cin, lo, hi);
-  stem_w_store(wv9, wl);
-  lds_barrier();
-  f32x16 acc[2][2];
-  stem_y_mfma(lo, hi, wl, bias, acc);
-  stem_tile_to_lds(acc, yt, stats + 128, stats + 192);  // stats = [mean | invstd | scale | shift] x 64
-  lds_barrier();
-  float am = 0.f;
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const int item = tid + 256 * q, cq = item & 15;
-    const StemWin wn = stem_window(m0, item >> 4, H, W);
-    const float4 z0 = *reinterpret_cast<const float4*>(&yt[wn.px][4 * cq]);
-    const float4 z1 = *reinterpret_cast<const float4*>(&yt[wn.px + 1][4 * cq]);
-    const float4 z2 = *reinterpret_cast<const float4*>(&yt[wn.px + W][4 * cq]);
-    const float4 z3 = *reinterpret_cast<const float4*>(&yt[wn.px + W + 1][4 * cq]);
-    float4 m;
-    m.x = fmaxf(fmaxf(z0.x, z1.x), fmaxf(z2.x, z3.x));
-    m.y = fmaxf(fmaxf(z0.y, z1.y), fmaxf(z2.y, z3.y));
-    m.z = fmaxf(fmaxf(z0.z, z1.z), fmaxf(z2.z, z3.z));
-    m.w = fmaxf(fmaxf(z0.w, z1.w), fmaxf(z2.w, z3.w));
-    *reinterpret_cast<float4*>(out + (long long)wn.pooled * 64 + 4 * cq) = m;
-    am = fmaxf(am, fmaxf(fmaxf(m.x, m.y), fmaxf(m.z, m.w)));  // >= 0 after the ReLU
-  }
-  if (amax_part) {
-    __shared__ float red[4];
-    am = wave_max(am);
-    if ((tid & 63) == 0) red[wv] = am;
-    __syncthreads();
-    if (tid == 0) amax_part[blockIdx.x] = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
-  }
-}
-
-// Backward statistics of the stem's BatchNorm from the recomputed y: per (block, channel) partial
-// sums of dz, dz * xhat and xhat (what bn_bwd_reduce_kernel computes from a stored y), PS of them.
-__global__ __launch_bounds__(256, 2) void stem_bnstat_kernel(const float* __restrict__ x, const float* __restrict__ w,
-                                                          const float* __restrict__ bias,
-                                                          const float* __restrict__ gout,
-                                                          const float* __restrict__ stats, float* __restrict__ part,
-                                                          int N, int H, int W, int Cin, int PS) {
-  __shared__ float wl[64][37];
-  __shared__ __attribute__((aligned(16))) float yt[256][YLD];
-  const int tid = threadIdx.x, wv = tid >> 6;
-  const int M = N * H * W;
-  const int m0 = blockIdx.x * 256;
-  float wv9[9];
-  stem_w_issue(w, Cin, wv9);
-  float lo[9][2], hi[9][2];
-  stem_x_issue(make_rsrc(x, (unsigned)((long long)M * Cin * 4)), m0 + wv * 64, M, H, W, Cin, lo, hi);
-  // this thread's channel quad is fixed (tid & 15); its 4 windows' output gradients load meanwhile
-  const int cq = tid & 15;
-  float4 gv[4];
-  StemWin wn[4];
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    wn[q] = stem_window(m0, (tid + 256 * q) >> 4, H, W);
-    gv[q] = *reinterpret_cast<const float4*>(gout + (long long)wn[q].pooled * 64 + 4 * cq);
-  }
-  stem_w_store(wv9, wl);
-  lds_barrier();
-  f32x16 acc[2][2];
-  stem_y_mfma(lo, hi, wl, bias, acc);
-  stem_tile_to_lds(acc, yt, nullptr, nullptr);
-  lds_barrier();
-  const float* mean = stats;
-  const float* invstd = stats + 64;
-  const float* scale = stats + 128;
-  const float* shift = stats + 192;
-  float mu[4], is[4], sc[4], sh[4];
-#pragma unroll
-  for (int e = 0; e < 4; ++e) {
-    mu[e] = mean[4 * cq + e];
-    is[e] = invstd[4 * cq + e];
-    sc[e] = scale[4 * cq + e];
-    sh[e] = shift[4 * cq + e];
-  }
-  float a1[4] = {0.f, 0.f, 0.f, 0.f}, a2[4] = {0.f, 0.f, 0.f, 0.f}, a3[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const float4 v[4] = {*reinterpret_cast<const float4*>(&yt[wn[q].px][4 * cq]),
-                         *reinterpret_cast<const float4*>(&yt[wn[q].px + 1][4 * cq]),
-                         *reinterpret_cast<const float4*>(&yt[wn[q].px + W][4 * cq]),
-                         *reinterpret_cast<const float4*>(&yt[wn[q].px + W + 1][4 * cq])};
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      float yy[4], z[4];
-#pragma unroll
-      for (int p = 0; p < 4; ++p) {
-        yy[p] = e == 0 ? v[p].x : e == 1 ? v[p].y : e == 2 ? v[p].z : v[p].w;
-        z[p] = fmaxf(fmaf(yy[p], sc[e], sh[e]), 0.f);
-      }
-      const float g = e == 0 ? gv[q].x : e == 1 ? gv[q].y : e == 2 ? gv[q].z : gv[q].w;
-      int arg = 0;
-      float mx = z[0];
-      if (z[1] > mx) { mx = z[1]; arg = 1; }
-      if (z[2] > mx) { mx = z[2]; arg = 2; }
-      if (z[3] > mx) { mx = z[3]; arg = 3; }
-      const float gg = mx > 0.f ? g : 0.f;
-      float xh[4];
-#pragma unroll
-      for (int p = 0; p < 4; ++p) xh[p] = (yy[p] - mu[e]) * is[e];
-      const float xs = (xh[0] + xh[1]) + (xh[2] + xh[3]);
-      const float xa = arg == 0 ? xh[0] : arg == 1 ? xh[1] : arg == 2 ? xh[2] : xh[3];
-      a1[e] += gg;
-      a2[e] += gg * xa;
-      a3[e] += xs;
-    }
-  }
-  // reduce over the 16 threads sharing the channel quad (tid >> 4), through the (now free) LDS image
-  lds_barrier();
-  float* red = &yt[0][0];  // [16][16][12]
-#pragma unroll
-  for (int e = 0; e < 4; ++e) {
-    red[((tid >> 4) * 16 + cq) * 12 + e] = a1[e];
-    red[((tid >> 4) * 16 + cq) * 12 + 4 + e] = a2[e];
-    red[((tid >> 4) * 16 + cq) * 12 + 8 + e] = a3[e];
-  }
-  __syncthreads();
-  if (tid < 192) {  // (channel c = tid / 3, sum s = tid % 3)
-    const int c = tid / 3, sidx = tid - 3 * (tid / 3);
-    if (sidx < PS) {
-      float t = 0.f;
-      for (int k = 0; k < 16; ++k) t += red[(k * 16 + (c >> 2)) * 12 + 4 * sidx + (c & 3)];
-      part[((long long)blockIdx.x * 64 + c) * PS + sidx] = t;
-    }
   }
 }
 
@@ -516,144 +340,6 @@ __global__ __launch_bounds__(256, 2) void stem_wgrad_kernel(const float* __restr
 }
 
 
-// Weight gradient from the recomputed y (recompute mode): the blocks walk 256-pixel chunks; per
-// chunk the y tile is rebuilt on the matrix cores into LDS while the chunk's output gradients and
-// x taps load, then each wave takes 16 of the chunk's 64 pool windows (4 groups of 4) through the
-// same per-lane window scheme and MFMA accumulation as stem_wgrad_kernel.
-template <int CIN>
-__global__ __launch_bounds__(256, 2) void stem_wgrad_rc_kernel(const float* __restrict__ x, const float* __restrict__ w,
-                                                            const float* __restrict__ bias,
-                                                            const float* __restrict__ gout,
-                                                            const float* __restrict__ stats,
-                                                            const float* __restrict__ sums, float* __restrict__ slab,
-                                                            int N, int H, int W) {
-  constexpr int C = 64;
-  __shared__ float wl[64][37];
-  __shared__ __attribute__((aligned(16))) float yt[256][YLD];
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const int i = lane & 15, j = lane >> 4;
-  const int M = N * H * W;
-  const int nchunk = M / 256;
-  const float invM = 1.f / (float)M;
-
-  float sc[4], sh[4], mu[4], is[4], k1[4], k2[4];
-#pragma unroll
-  for (int e = 0; e < 4; ++e) {
-    const int c = 4 * i + e;
-    mu[e] = stats[c];
-    is[e] = stats[C + c];
-    sc[e] = stats[2 * C + c];
-    sh[e] = stats[3 * C + c];
-    k1[e] = sums[c] * invM;
-    k2[e] = sums[C + c] * invM;
-  }
-  const bool tap_ok = i < 9;
-  const int tkh = i / 3 - 1, tkw = i - 3 * (i / 3) - 1;
-  const __amdgpu_buffer_rsrc_t xr = make_rsrc(x, (unsigned)((long long)M * CIN * 4));
-
-  float wv9[9];
-  stem_w_issue(w, CIN, wv9);
-  stem_w_store(wv9, wl);  // (first lds_barrier below publishes it)
-
-  f32x4 acc[4][CIN];
-#pragma unroll
-  for (int ct = 0; ct < 4; ++ct)
-#pragma unroll
-    for (int c = 0; c < CIN; ++c) acc[ct][c] = f32x4{};
-
-  for (int ch = blockIdx.x; ch < nchunk; ch += gridDim.x) {
-    const int m0 = ch * 256;
-    float lo[9][2], hi[9][2];
-    stem_x_issue(xr, m0 + wv * 64, M, H, W, CIN, lo, hi);
-    // this lane's windows: j of group g, groups 4 wv .. 4 wv + 3 of the chunk
-    float4 gv[4];
-    StemWin wn[4];
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      wn[g] = stem_window(m0, 16 * wv + 4 * g + j, H, W);
-      gv[g] = *reinterpret_cast<const float4*>(gout + (long long)wn[g].pooled * C + 4 * i);
-    }
-    lds_barrier();  // every wave is done with the previous chunk's tile (and wl is published)
-    f32x16 yacc[2][2];
-    stem_y_mfma(lo, hi, wl, bias, yacc);
-    stem_tile_to_lds(yacc, yt, nullptr, nullptr);
-    // the x taps load once the tile's registers are free (they would not fit beside them)
-    float xv[4][4][CIN];
-    {
-      const int n = m0 / (H * W);
-      const int pr0 = (m0 - n * H * W) / W;  // chunk's first image row
-#pragma unroll
-      for (int g = 0; g < 4; ++g)
-#pragma unroll
-        for (int p = 0; p < 4; ++p) {
-          const int lp = wn[g].px + (p >> 1) * W + (p & 1);  // chunk-local pixel
-          const int ph = pr0 + lp / W, pw = lp - (lp / W) * W;
-          const int ih = ph + tkh, iw = pw + tkw;
-          const bool ok = tap_ok && (unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W;
-          const unsigned o = ok ? (unsigned)(((n * H + ih) * W + iw) * CIN * 4) : kOOB;
-#pragma unroll
-          for (int c = 0; c < CIN; ++c)
-            xv[g][p][c] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xr, (int)(o + 4u * c), 0, 0));
-        }
-    }
-    lds_barrier();
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      float4 yv[4];
-#pragma unroll
-      for (int p = 0; p < 4; ++p) yv[p] = *reinterpret_cast<const float4*>(&yt[wn[g].px + (p >> 1) * W + (p & 1)][4 * i]);
-      float dyv[4][4];  // [pixel][channel e]
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        float yy[4], z[4];
-#pragma unroll
-        for (int p = 0; p < 4; ++p) {
-          yy[p] = e == 0 ? yv[p].x : e == 1 ? yv[p].y : e == 2 ? yv[p].z : yv[p].w;
-          z[p] = fmaxf(fmaf(yy[p], sc[e], sh[e]), 0.f);
-        }
-        const float gg = e == 0 ? gv[g].x : e == 1 ? gv[g].y : e == 2 ? gv[g].z : gv[g].w;
-        int arg = 0;
-        float mx = z[0];
-        if (z[1] > mx) { mx = z[1]; arg = 1; }
-        if (z[2] > mx) { mx = z[2]; arg = 2; }
-        if (z[3] > mx) { mx = z[3]; arg = 3; }
-#pragma unroll
-        for (int p = 0; p < 4; ++p) {
-          const float dz = (arg == p && mx > 0.f) ? gg : 0.f;
-          const float xh = (yy[p] - mu[e]) * is[e];
-          dyv[p][e] = sc[e] * (dz - k1[e] - xh * k2[e]);
-        }
-      }
-#pragma unroll
-      for (int p = 0; p < 4; ++p)
-#pragma unroll
-        for (int ct = 0; ct < 4; ++ct)
-#pragma unroll
-          for (int c = 0; c < CIN; ++c)
-            acc[ct][c] = __builtin_amdgcn_mfma_f32_16x16x4f32(dyv[p][ct], xv[g][p][c], acc[ct][c], 0, 0, 0);
-    }
-  }
-  // D layout: lane l holds rows 4 (l / 16) + v (channel co = 4 row + ct), column l % 16 (tap);
-  // the per-wave partials meet in the (now free) LDS image
-  lds_barrier();
-  float (*red)[C][36] = reinterpret_cast<float (*)[C][36]>(&yt[0][0]);  // [4][64][36] = 36 KB
-#pragma unroll
-  for (int ct = 0; ct < 4; ++ct)
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      if (i < 9) {
-#pragma unroll
-        for (int v = 0; v < 4; ++v) red[wv][4 * (4 * j + v) + ct][4 * i + c] = c < CIN ? acc[ct][c < CIN ? c : 0][v] : 0.f;
-      }
-    }
-  __syncthreads();
-  float* dst = slab + (long long)blockIdx.x * C * 36;
-  for (int e = tid; e < C * 36; e += 256) {
-    const int co = e / 36, k = e - co * 36;
-    dst[e] = (red[0][co][k] + red[1][co][k]) + (red[2][co][k] + red[3][co][k]);
-  }
-}
-
 }  // namespace
 
 bool stem_ok(int Cin, int KH, int KW, int stride, int pad, int Co) {
@@ -666,44 +352,6 @@ void stem_fwd_launch(const float* x, const float* w, const float* bias, float* y
   (void)Co;  // == 64 (stem_ok)
   hipLaunchKernelGGL(stem_fwd_kernel, dim3((unsigned)((M + 255) / 256)), dim3(256), 0, st, x, w, bias, y, part, N, H,
                      W, Cin);
-}
-
-bool stem_recompute_ok(int N, int H, int W) {
-  const long long M = (long long)N * H * W;
-  return (H % 2) == 0 && (W % 2) == 0 && (256 % (2 * W)) == 0 && ((long long)H * W) % 256 == 0 && M >= 256 &&
-         M < (1LL << 31) / 64;
-}
-
-void stem_act_launch(const float* x, const float* w, const float* bias, const float* stats, float* out,
-                     float* amax_part, int N, int H, int W, int Cin, hipStream_t st) {
-  const long long M = (long long)N * H * W;
-  hipLaunchKernelGGL(stem_act_kernel, dim3((unsigned)(M / 256)), dim3(256), 0, st, x, w, bias, stats, out, amax_part,
-                     N, H, W, Cin);
-}
-
-int stem_bnstat_parts(int N, int H, int W) { return (int)((long long)N * H * W / 256); }
-
-void stem_bnstat_launch(const float* x, const float* w, const float* bias, const float* gout, const float* stats,
-                        float* part, int ps, int N, int H, int W, int Cin, hipStream_t st) {
-  hipLaunchKernelGGL(stem_bnstat_kernel, dim3((unsigned)stem_bnstat_parts(N, H, W)), dim3(256), 0, st, x, w, bias,
-                     gout, stats, part, N, H, W, Cin, ps);
-}
-
-int stem_wgrad_rc_blocks(int N, int H, int W) {
-  const long long chunks = (long long)N * H * W / 256;
-  return (int)std::max<long long>(1, std::min<long long>(512, chunks));
-}
-
-void stem_wgrad_rc_launch(const float* x, const float* w, const float* bias, const float* gout, const float* stats,
-                          const float* sums, float* slab, int nblk, int N, int H, int W, int Cin, hipStream_t st) {
-#define CDP_STEM_RC(CI)                                                                                          \
-  hipLaunchKernelGGL(stem_wgrad_rc_kernel<CI>, dim3(nblk), dim3(256), 0, st, x, w, bias, gout, stats, sums, slab, N, H, \
-                     W)
-  if (Cin == 3) CDP_STEM_RC(3);
-  else if (Cin == 4) CDP_STEM_RC(4);
-  else if (Cin == 2) CDP_STEM_RC(2);
-  else CDP_STEM_RC(1);
-#undef CDP_STEM_RC
 }
 
 int stem_wgrad_blocks(int N, int H, int W) {

@@ -31,8 +31,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("conv_bn_act_fwd", &conv_bn_act_fwd, py::arg("x"), py::arg("w"), py::arg("b"), py::arg("gamma"),
         py::arg("beta"), py::arg("running_mean"), py::arg("running_var"), py::arg("num_batches_tracked"),
         py::arg("momentum"), py::arg("eps"), py::arg("training"), py::arg("stride"), py::arg("pad"), py::arg("pool"),
-        py::arg("relu"), py::arg("residual"), py::arg("x_amax") = py::none(), py::arg("w_amax") = py::none(),
-        py::arg("stem_recompute") = false);
+        py::arg("relu"), py::arg("residual"), py::arg("x_amax") = py::none(), py::arg("w_amax") = py::none());
   m.def("multi_amax", &multi_amax, py::arg("tensors"),
         "f16x2 engine: partial |max| values of many tensors in one launch (empty list for other engines)");
   m.def("conv_bn_act_bwd", &conv_bn_act_bwd, py::arg("gout"), py::arg("x"), py::arg("w"), py::arg("y"),

@@ -408,53 +408,6 @@ WgradPlan plan_wgrad(int Cout, int Kdim, long long M) {
   return w;
 }
 
-// ---- side stream for dgrad || wgrad overlap
-bool conc_enabled() {
-  static const bool on = [] {
-    // measured on MI355X: running two full-occupancy GEMM grids concurrently is slower (VGG-11
-    // B=256: 3.0 -> 4.8 ms/step), so this is opt-in (CDP_BWD_OVERLAP=1)
-    const char* e = std::getenv("CDP_BWD_OVERLAP");
-    return e && e[0] == '1';
-  }();
-  return on;
-}
-
-c10::hip::HIPStream side_stream() {
-  static thread_local std::vector<c10::hip::HIPStream> streams;
-  const int dev = c10::hip::current_device();
-  while ((int)streams.size() <= dev) streams.push_back(c10::hip::getStreamFromPool(true, (c10::DeviceIndex)streams.size()));
-  return streams[dev];
-}
-
-struct EventPool {
-  std::vector<hipEvent_t> evs;
-  size_t next = 0;
-  hipEvent_t get() {
-    if (next == evs.size()) {
-      hipEvent_t e;
-      hipEventCreateWithFlags(&e, hipEventDisableTiming);
-      evs.push_back(e);
-    }
-    hipEvent_t e = evs[next];
-    next = (next + 1) % 64;  // reuse after 64 forks (re-recording an event is legal once waited on)
-    return e;
-  }
-};
-
-void fork_to(const c10::hip::HIPStream& side) {
-  static thread_local EventPool pool;
-  hipEvent_t e = pool.get();
-  hipEventRecord(e, c10::hip::getCurrentHIPStream().stream());
-  hipStreamWaitEvent(side.stream(), e, 0);
-}
-
-void join_from(const c10::hip::HIPStream& side) {
-  static thread_local EventPool pool;
-  hipEvent_t e = pool.get();
-  hipEventRecord(e, side.stream());
-  hipStreamWaitEvent(c10::hip::getCurrentHIPStream().stream(), e, 0);
-}
-
 template <class P>
 void set_divs(P& p) {
   p.fd_PQ = make_fastdiv(p.P * p.Q);
@@ -757,7 +710,7 @@ std::vector<at::Tensor> stem_bn_act_fwd(const at::Tensor& x_, const at::Tensor& 
                                         const c10::optional<at::Tensor>& running_mean,
                                         const c10::optional<at::Tensor>& running_var,
                                         const c10::optional<at::Tensor>& num_batches_tracked, double momentum,
-                                        double eps, bool pool, bool relu, bool recompute) {
+                                        double eps, bool pool, bool relu) {
   check_f32_cuda(x_, "x");
   check_f32_cuda(w_, "weight");
   const at::Tensor x = nhwc(x_), w = nhwc(w_);
@@ -765,13 +718,11 @@ std::vector<at::Tensor> stem_bn_act_fwd(const at::Tensor& x_, const at::Tensor& 
   TORCH_CHECK(w.size(1) == Cin, "stem weight in-channels mismatch");
   auto opts = x.options();
   hipStream_t st = cur_stream();
-  // recompute mode: y is never stored; the activation pass and the backward rebuild it from x
-  const bool rc = recompute && pool && relu && stem_recompute_ok(N, H, W);
-  at::Tensor y = rc ? at::Tensor() : at::empty({N, Co, H, W}, opts.memory_format(at::MemoryFormat::ChannelsLast));
+  at::Tensor y = at::empty({N, Co, H, W}, opts.memory_format(at::MemoryFormat::ChannelsLast));
   const long long M = (long long)N * H * W;
   const int nparts = (int)((M + 255) / 256);
   at::Tensor part = at::empty({nparts, Co, 2}, opts);
-  stem_fwd_launch(x.data_ptr<float>(), w.data_ptr<float>(), fptr(b), rc ? nullptr : y.data_ptr<float>(),
+  stem_fwd_launch(x.data_ptr<float>(), w.data_ptr<float>(), fptr(b), y.data_ptr<float>(),
                   part.data_ptr<float>(), N, H, W, Cin, Co, st);
   at::Tensor stats = at::empty({4, Co}, opts);
   long long* nbt = nullptr;
@@ -783,17 +734,9 @@ std::vector<at::Tensor> stem_bn_act_fwd(const at::Tensor& x_, const at::Tensor& 
   at::Tensor out = at::empty({N, Co, pool ? H / 2 : H, pool ? W / 2 : W},
                              opts.memory_format(at::MemoryFormat::ChannelsLast));
   at::Tensor out_amax;
-  if (rc) {
-    if (f16x2_mode()) out_amax = at::empty({M / 256}, opts);
-    stem_act_launch(x.data_ptr<float>(), w.data_ptr<float>(), fptr(b), stats.data_ptr<float>(), out.data_ptr<float>(),
-                    out_amax.defined() ? out_amax.data_ptr<float>() : nullptr, N, H, W, Cin, st);
-    // y's shape without storage (stride 0): conv_bn_act_bwd takes this as "recompute from x"
-    y = at::empty({1}, opts).expand({N, Co, H, W});
-  } else {
-    if (f16x2_mode()) out_amax = at::empty({bn_act_grid(N, H, W, Co, pool)}, opts);
-    bn_act_fwd_launch(y.data_ptr<float>(), stats.data_ptr<float>(), nullptr, out.data_ptr<float>(), N, H, W, Co, pool,
-                      relu, st, out_amax.defined() ? out_amax.data_ptr<float>() : nullptr);
-  }
+  if (f16x2_mode()) out_amax = at::empty({bn_act_grid(N, H, W, Co, pool)}, opts);
+  bn_act_fwd_launch(y.data_ptr<float>(), stats.data_ptr<float>(), nullptr, out.data_ptr<float>(), N, H, W, Co, pool,
+                    relu, st, out_amax.defined() ? out_amax.data_ptr<float>() : nullptr);
   return {out, y, stats, x, out_amax, at::Tensor(), at::Tensor()};
 }
 
@@ -822,14 +765,13 @@ std::vector<at::Tensor> conv_bn_act_fwd(const at::Tensor& x, const at::Tensor& w
                                         double eps, bool training, int64_t stride, int64_t pad, bool pool, bool relu,
                                         const c10::optional<at::Tensor>& residual,
                                         const c10::optional<at::Tensor>& x_amax,
-                                        const c10::optional<at::Tensor>& w_amax, bool stem_recompute) {
+                                        const c10::optional<at::Tensor>& w_amax) {
   // RGB stem (3x3 / stride 1 / pad 1, Cin <= 4, training BN): one exact-fp32 MFMA kernel reading
-  // the raw NHWC input, no channel padding, no operand scales (stem.hip); stem_recompute (the
-  // caller needs no input gradient): y is rebuilt from x instead of stored
+  // the raw NHWC input, no channel padding, no operand scales (stem.hip)
   if (stem_enabled() && stem_ok((int)x.size(1), (int)w.size(2), (int)w.size(3), stride, pad, (int)w.size(0)) &&
       training && !(residual.has_value() && residual->defined()))
     return stem_bn_act_fwd(x, w, b, gamma, beta, running_mean, running_var, num_batches_tracked, momentum, eps, pool,
-                           relu, stem_recompute);
+                           relu);
   // other stems: zero-pad 3 -> 4 channels so the float4 gather path runs (the padded input is what
   // backward needs, so it is returned for saving)
   const bool padc = (x.size(1) % 4) != 0;
@@ -921,38 +863,6 @@ std::vector<at::Tensor> conv_bn_act_bwd(const at::Tensor& gout_, const at::Tenso
     if (o.has_value() && o->defined()) return *o;
     return cl ? at::empty(shape, opts.memory_format(at::MemoryFormat::ChannelsLast)) : at::empty(shape, opts);
   };
-  if (y.dim() == 4 && y.stride(0) == 0) {
-    // RGB stem in recompute mode (stem_bn_act_fwd): y is rebuilt from x by the statistics pass and
-    // by the weight-gradient pass; no input gradient
-    const at::Tensor xin = nhwc(x), win = nhwc(w);
-    const int cin = (int)xin.size(1);
-    TORCH_CHECK(!need_dx && training && pool && relu && !(zout_.has_value() && zout_->defined()) && C == 64 &&
-                    stem_ok(cin, (int)w.size(2), (int)w.size(3), stride, pad, C) && stem_recompute_ok(N, H, W) &&
-                    !(part_in.has_value() && part_in->defined()) && (has_bias == (bias.has_value() && bias->defined())),
-                "conv_bn_act_bwd: recompute-mode stem backward with an unsupported configuration");
-    const float* bp = has_bias ? bias->data_ptr<float>() : nullptr;
-    const int ps = has_bias ? 3 : 2;
-    const int nparts = stem_bnstat_parts(N, H, W);
-    at::Tensor part = at::empty({nparts, C, ps}, opts);
-    stem_bnstat_launch(xin.data_ptr<float>(), win.data_ptr<float>(), bp, gout.data_ptr<float>(),
-                       stats.data_ptr<float>(), part.data_ptr<float>(), ps, N, H, W, cin, st);
-    at::Tensor sums = at::empty({2, C}, opts);
-    at::Tensor dgamma = slot(dgamma_out, {C}, false), dbeta = slot(dbeta_out, {C}, false);
-    at::Tensor db;
-    if (has_bias) db = slot(db_out, {C}, false);
-    chan_finalize_launch(part.data_ptr<float>(), nparts, C, sums.data_ptr<float>(), dbeta.data_ptr<float>(),
-                         dgamma.data_ptr<float>(), false, st, ps, has_bias ? db.data_ptr<float>() : nullptr,
-                         stats.data_ptr<float>() + 2 * C, (long long)N * H * W, has_bias ? 1 : 0);
-    const int nb = stem_wgrad_rc_blocks(N, H, W);
-    at::Tensor slab = at::empty({nb, C, 36}, opts);
-    stem_wgrad_rc_launch(xin.data_ptr<float>(), win.data_ptr<float>(), bp, gout.data_ptr<float>(),
-                         stats.data_ptr<float>(), sums.data_ptr<float>(), slab.data_ptr<float>(), nb, N, H, W, cin,
-                         st);
-    at::Tensor dw = slot(dw_out, {C, cin, w.size(2), w.size(3)}, true);
-    TORCH_CHECK(dw.is_contiguous(at::MemoryFormat::ChannelsLast), "stem dW slot must be channels_last");
-    slab_sum_strided_launch(slab.data_ptr<float>(), nb, (long long)C * 36, 4, cin, dw.data_ptr<float>(), false, st);
-    return {at::Tensor(), dw, db, dgamma, dbeta, at::Tensor(), at::Tensor()};
-  }
   at::Tensor zout;
   if (zout_.has_value() && zout_->defined()) zout = nhwc(*zout_);
   const int nblk = bn_bwd_grid(N, H, W, C, pool);
@@ -1035,10 +945,9 @@ std::vector<at::Tensor> conv_bn_act_bwd(const at::Tensor& gout_, const at::Tenso
     chan_finalize_launch(dbpart.data_ptr<float>(), nblk, C, nullptr, db.data_ptr<float>(), nullptr, false, st);
   // x may carry zero-padded channels (RGB stem, see conv_bn_act_fwd)
   const bool padc = x.size(1) != w.size(1);
-  // data- and weight-gradient GEMMs are independent: optionally run the weight gradient on a side
-  // stream (fork/join by events, so it is also a parallel branch under hipGraph capture).
+  // (running the weight gradient on a side stream beside the data gradient was measured 2x slower
+  // on MI355X: two full-occupancy GEMM grids compete instead of overlapping; docs/PERF.md)
   at::Tensor dx, dw;
-  const bool overlap = need_dx && conc_enabled();
   // both GEMMs' split-K reductions (and, given prev_*, the previous block's BN statistics
   // reduction) in one bwd_reduce launch after the two GEMMs (bwd_fuse.hip)
   // Only with a previous BN to serve: on its own the merge of the two reductions buys nothing (the
@@ -1046,16 +955,9 @@ std::vector<at::Tensor> conv_bn_act_bwd(const at::Tensor& gout_, const at::Tenso
   // 0.4 % slower with it)
   DeferredReduce dr;
   const bool has_prev = prev_y.has_value() && prev_y->defined() && prev_stats.has_value() && prev_stats->defined();
-  DeferredReduce* defer = (bwd_fuse_enabled() && !overlap && !padc && has_prev) ? &dr : nullptr;
-  c10::hip::HIPStream side = overlap ? side_stream() : c10::hip::getCurrentHIPStream();
-  if (overlap) fork_to(side);
-  {
-    c10::hip::HIPStreamGuard guard(side);
-    dw = wgrad_impl(dy, x, {w.size(0), x.size(1), w.size(2), w.size(3)}, stride, pad, dw_out, false,
-                    padc ? w.size(1) : -1, dya, x_amax, defer);
-  }
-  if (overlap && !(dw_out.has_value() && dw_out->defined()))  // allocated on the side stream, consumed on main
-    c10::hip::HIPCachingAllocator::recordStream(dw.storage().data_ptr(), c10::hip::getCurrentHIPStream());
+  DeferredReduce* defer = (bwd_fuse_enabled() && !padc && has_prev) ? &dr : nullptr;
+  dw = wgrad_impl(dy, x, {w.size(0), x.size(1), w.size(2), w.size(3)}, stride, pad, dw_out, false,
+                  padc ? w.size(1) : -1, dya, x_amax, defer);
   if (need_dx) {
     if (padc) {
       at::Tensor dx4 = conv2d_dgrad(dy, pad_channels4(nhwc(w)), {x.size(0), x.size(1), x.size(2), x.size(3)}, stride,
@@ -1107,7 +1009,6 @@ std::vector<at::Tensor> conv_bn_act_bwd(const at::Tensor& gout_, const at::Tenso
     }
     bwd_reduce_launch(a, st);
   }
-  if (overlap) join_from(side);
   return {dx, dw, db, dgamma, dbeta, dres, prev_part};
 }
 
@@ -1259,8 +1160,21 @@ at::Tensor augment(const at::Tensor& images, const c10::optional<at::Tensor>& in
     m[i] = (float)mean[std::min<size_t>(i, mean.size() - 1)];
     is[i] = (float)(1.0 / std_[std::min<size_t>(i, std_.size() - 1)]);
   }
+  TORCH_CHECK(o.is_cuda() && o.device() == images.device() && o.scalar_type() == at::kFloat && o.numel() >= batch * C * H * W,
+              "augment: out must be a float32 tensor on the images' device holding the batch");
   const long long* ip = nullptr;
-  if (indices.has_value() && indices->defined()) ip = reinterpret_cast<const long long*>(indices->data_ptr<int64_t>());
+  if (indices.has_value() && indices->defined()) {
+    TORCH_CHECK(indices->device() == images.device() && indices->scalar_type() == at::kLong && indices->is_contiguous(),
+                "augment: indices must be a contiguous int64 tensor on the images' device");
+    // the kernel reads idx[idx_offset + (counter % nbatches) * batch + b] for b < batch
+    TORCH_CHECK(idx_offset >= 0 && idx_offset + std::max<int64_t>(nbatches, 1) * batch <= indices->numel(),
+                "augment: idx_offset + max(nbatches, 1) * batch = ", idx_offset + std::max<int64_t>(nbatches, 1) * batch,
+                " exceeds the ", indices->numel(), " indices");
+    ip = reinterpret_cast<const long long*>(indices->data_ptr<int64_t>());
+  } else {
+    TORCH_CHECK(idx_offset >= 0 && idx_offset + std::max<int64_t>(nbatches, 1) * batch <= images.size(0),
+                "augment: the batch range exceeds the ", images.size(0), " images");
+  }
   const long long* cp = nullptr;
   if (counter.has_value() && counter->defined()) cp = reinterpret_cast<const long long*>(counter->data_ptr<int64_t>());
   TORCH_CHECK(nbatches == 0 || cp, "counter-driven batch offsets need the counter");
@@ -1270,6 +1184,9 @@ at::Tensor augment(const at::Tensor& images, const c10::optional<at::Tensor>& in
     TORCH_CHECK(labels.has_value() && labels->defined() && labels->scalar_type() == at::kLong &&
                     labels_out->scalar_type() == at::kLong && labels_out->numel() >= batch,
                 "labels / labels_out must be int64, labels_out holding the batch");
+    TORCH_CHECK(labels->device() == images.device() && labels_out->device() == images.device() &&
+                    labels->numel() >= images.size(0) && labels->is_contiguous() && labels_out->is_contiguous(),
+                "augment: labels (one per image) and labels_out must be contiguous on the images' device");
     lp = reinterpret_cast<const long long*>(labels->data_ptr<int64_t>());
     lo = reinterpret_cast<long long*>(labels_out->data_ptr<int64_t>());
   }

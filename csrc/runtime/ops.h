@@ -33,8 +33,7 @@ std::vector<at::Tensor> conv_bn_act_fwd(const at::Tensor& x, const at::Tensor& w
                                         double eps, bool training, int64_t stride, int64_t pad, bool pool, bool relu,
                                         const c10::optional<at::Tensor>& residual,
                                         const c10::optional<at::Tensor>& x_amax = c10::nullopt,
-                                        const c10::optional<at::Tensor>& w_amax = c10::nullopt,
-                                        bool stem_recompute = false);
+                                        const c10::optional<at::Tensor>& w_amax = c10::nullopt);
 std::vector<at::Tensor> multi_amax(const std::vector<at::Tensor>& ts);
 std::vector<std::vector<at::Tensor>> weight_prep(const std::vector<at::Tensor>& ts, const std::vector<bool>& want_t);
 std::vector<at::Tensor> conv_bn_act_bwd(const at::Tensor& gout, const at::Tensor& x, const at::Tensor& w,
