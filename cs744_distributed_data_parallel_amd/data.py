@@ -51,11 +51,25 @@ class ImageDataset:
         return tuple(self.images.shape[1:])
 
 
-def synthetic_cifar10(n: int = 50000, seed: int = 0, device="cpu", train: bool = True) -> ImageDataset:
-    """Random CIFAR-10-shaped data (uint8 32x32x3, 10 classes) -- a stand-in for the real set."""
+def synthetic_cifar10(n: int = 50000, seed: int = 0, device="cpu", train: bool = True,
+                      learnable: bool = False) -> ImageDataset:
+    """Random CIFAR-10-shaped data (uint8 32x32x3, 10 classes) -- a stand-in for the real set.
+
+    ``learnable``: the label is a fixed function of the image (argmax of one fixed random projection
+    of its 8x8-average-pooled, normalised pixels, the same projection for train and test), so the
+    loss falls and test accuracy rises above chance -- a check of the whole pipeline that random
+    labels cannot give."""
     g = torch.Generator().manual_seed(seed + (0 if train else 1))
     imgs = torch.randint(0, 256, (n, 32, 32, 3), dtype=torch.uint8, generator=g)
     labels = torch.randint(0, 10, (n,), dtype=torch.int64, generator=g)
+    if learnable:
+        proj = torch.randn(10, 3 * 4 * 4, generator=torch.Generator().manual_seed(12345))
+        mean = torch.tensor(CIFAR_MEAN).view(1, 3, 1, 1)
+        std = torch.tensor(CIFAR_STD).view(1, 3, 1, 1)
+        for i in range(0, n, 4096):
+            x = (imgs[i : i + 4096].permute(0, 3, 1, 2).float() / 255.0 - mean) / std
+            feat = torch.nn.functional.avg_pool2d(x, 8).reshape(x.shape[0], -1)
+            labels[i : i + 4096] = (feat @ proj.t()).argmax(1)
     return ImageDataset(imgs, labels, CIFAR_MEAN, CIFAR_STD, 4, "synthetic-cifar10").to(device)
 
 

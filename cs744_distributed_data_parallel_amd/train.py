@@ -125,7 +125,7 @@ def build_data(args, device, train: bool):
         n = args.synthetic_size or (1281 if train else 500)
         return synthetic_imagenet(n, seed=0 if train else 1, device=device)
     n = args.synthetic_size or (50000 if train else 10000)
-    return synthetic_cifar10(n, seed=0, device=device, train=train)
+    return synthetic_cifar10(n, seed=0, device=device, train=train, learnable=args.data == "synthetic-learnable")
 
 
 def run(rank, size, epochs, batch_size, args):
@@ -141,6 +141,13 @@ def run(rank, size, epochs, batch_size, args):
     test_loader = DeviceLoader(test_set, batch_size, shuffle=False, train=False)
     print("Size of test set is {}".format(len(test_loader)))
 
+    if dist.is_initialized() and device.type == "cuda":
+        # which communicator carries the gradient collectives (stderr: stdout keeps the reference's lines)
+        import sys
+
+        kind = "rccl-native" if dist.native_communicator() is not None else "torch-" + str(dist.get_backend())
+        print(f"[cdp] rank {rank}: collectives on {kind}"
+              + (f" ({dist.comm_fallback_reason()})" if dist.comm_fallback_reason() else ""), file=sys.stderr)
     criterion = CrossEntropyLoss()
     model = get_model(args.model).to(device)
     sync = None
@@ -241,7 +248,9 @@ def parse_args(argv=None):
     p.add_argument("--strategy", default=None,
                    choices=["none", "gather_scatter", "allreduce_blocking", "bucketed_overlap", "ddp"])
     p.add_argument("--model", default="vgg11")
-    p.add_argument("--data", default="synthetic", help="synthetic | cifar10-bin:<root>")
+    p.add_argument("--data", default="synthetic",
+                   help="synthetic (random labels) | synthetic-learnable (labels a fixed function of the image) "
+                        "| cifar10-bin:<root>")
     p.add_argument("--synthetic-size", type=int, default=None)
     p.add_argument("--batch-size", type=int, default=256, help="global batch (split int(B/W) per rank)")
     p.add_argument("--lr", type=float, default=0.1)

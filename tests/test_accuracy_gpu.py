@@ -211,3 +211,67 @@ def test_vgg11_loss_curve_tracks_torch_fp32(engine):
     # over the run: within the spread that fp32 rounding noise itself induces (+ a small floor)
     assert dev.mean() <= 3.0 * noise.mean() + 0.02, (dev.mean(), noise.mean())
     assert abs(nat[-10:].mean() - ref[-10:].mean()) <= 3.0 * (pert[-10:].mean() - ref[-10:].mean()).abs() + 0.05
+
+
+# --------------------------------------------------------------------- headline GEMM plans
+# VGG-11 layers 1-7 (layer 0 runs the exact-fp32 stem kernels, test_kernels_gpu.py) at the bench's
+# batch (B=256) and at the reference's 8-rank strong-scaling batch (B=32): the conv entry points
+# plan tiles and split-K exactly as the training step does (plan_gemm / plan_wgrad in
+# csrc/runtime/ops.cpp), so these launches are the headline's GEMM configurations.
+VGG_LAYERS = [(64, 128, 16), (128, 256, 8), (256, 256, 8), (256, 512, 4), (512, 512, 4), (512, 512, 2),
+              (512, 512, 2)]
+
+
+def _patches(xp, n, p, q):
+    """[S, Ci*9] rows of the zero-padded input around output pixels (n, p, q), (ci, kh, kw) order."""
+    idx_h = p[:, None] + torch.arange(3, device=xp.device)[None, :]
+    idx_w = q[:, None] + torch.arange(3, device=xp.device)[None, :]
+    g = xp[n[:, None, None, None], torch.arange(xp.shape[1], device=xp.device)[None, :, None, None],
+           idx_h[:, None, :, None], idx_w[:, None, None, :]]
+    return g.reshape(len(n), -1)
+
+
+@pytest.mark.parametrize("engine", ["f16x2", "x3"])
+@pytest.mark.parametrize("B", [256, 32])
+@pytest.mark.parametrize("layer", range(1, 8))
+def test_headline_plan_gemms_meet_fp32_bound_on_samples(engine, B, layer):
+    Ci, Co, HW = VGG_LAYERS[layer - 1]
+    gen = torch.Generator(device="cuda").manual_seed(100 + layer)
+    x = torch.randn(B, Ci, HW, HW, device="cuda", generator=gen)
+    w = torch.randn(Co, Ci, 3, 3, device="cuda", generator=gen) * (1.0 / (Ci * 9) ** 0.5)
+    gy = torch.randn(B, Co, HW, HW, device="cuda", generator=gen)
+    orig = C().get_conv_gemm()
+    try:
+        C().set_conv_gemm(engine)
+        y = C().conv2d_fwd(cl(x), cl(w), None, 1, 1, False)[0]
+        dx = C().conv2d_dgrad(cl(gy), cl(w), list(x.shape), 1, 1)
+        dw = C().conv2d_wgrad(cl(gy), cl(x), list(w.shape), 1, 1)
+        torch.cuda.synchronize()
+    finally:
+        C().set_conv_gemm(orig)
+    xd, wd, gyd = x.double(), w.double(), gy.double()
+    S = 4096 // Co + 1  # output pixels sampled for fwd (x Co columns >= 4096 outputs)
+    n = torch.randint(0, B, (S,), device="cuda", generator=gen)
+    p = torch.randint(0, HW, (S,), device="cuda", generator=gen)
+    q = torch.randint(0, HW, (S,), device="cuda", generator=gen)
+    # forward: y[n, :, p, q] = patches(x) @ W^T
+    px = _patches(F.pad(xd, (1, 1, 1, 1)), n, p, q)
+    wm = wd.reshape(Co, -1)
+    ratios = [_check("fwd", y[n, :, p, q], (px @ wm.t()).cpu(), (px.abs() @ wm.abs().t()).cpu(), Ci * 9)]
+    # data gradient: a stride-1 pad-1 conv of gy with the flipped, transposed filter
+    S2 = 4096 // Ci + 1
+    n2 = torch.randint(0, B, (S2,), device="cuda", generator=gen)
+    p2 = torch.randint(0, HW, (S2,), device="cuda", generator=gen)
+    q2 = torch.randint(0, HW, (S2,), device="cuda", generator=gen)
+    pg = _patches(F.pad(gyd, (1, 1, 1, 1)), n2, p2, q2)
+    wt = wd.flip(2, 3).transpose(0, 1).reshape(Ci, -1)
+    ratios.append(_check("dgrad", dx[n2, :, p2, q2], (pg @ wt.t()).cpu(), (pg.abs() @ wt.abs().t()).cpu(), Co * 9))
+    # weight gradient: whole rows of dW for a few output channels, reduction over all B*HW*HW pixels
+    rows = torch.randperm(Co, device="cuda", generator=gen)[: 4096 // (Ci * 9) + 1]
+    xu = F.unfold(xd, 3, padding=1)  # [B, Ci*9, HW*HW]
+    g_sel = gyd[:, rows].reshape(B, len(rows), -1)
+    ref = torch.einsum("bkp,bcp->ck", xu, g_sel)
+    absref = torch.einsum("bkp,bcp->ck", xu.abs(), g_sel.abs())
+    ratios.append(_check("wgrad", dw[rows].reshape(len(rows), -1), ref.cpu(), absref.cpu(), B * HW * HW))
+    print(f"{engine} B={B} layer {layer}: worst err/bound fwd {ratios[0]:.2e} dgrad {ratios[1]:.2e} "
+          f"wgrad {ratios[2]:.2e}")

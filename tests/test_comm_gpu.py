@@ -191,3 +191,51 @@ def test_reducer_comm_to_compute_ordering_with_delayed_postop():
     r = subprocess.run([sys.executable, "-c", ORDER_SCRIPT], env=env, capture_output=True, text=True, timeout=300)
     assert "ORDER_ALL_OK" in r.stdout, r.stdout[-3000:] + r.stderr[-5000:]
     assert r.stdout.count("ORDER_OK") == 4
+
+
+WATCHDOG_SCRIPT = textwrap.dedent(
+    r"""
+    import os, time, torch
+    # every all_reduce is followed, on the comm stream and inside its completion event, by a 1.5 s
+    # idle wait (RcclComm::set_test_postop): to the watchdog that is a collective that never finishes
+    os.environ["CDP_REDUCER_TEST_POSTOP"] = "1500000:1"
+    from cs744_distributed_data_parallel_amd import distributed as dist
+    dist.init_process_group("rccl", rank=0, world_size=1)
+    comm = dist.native_communicator()
+    assert comm is not None and comm.healthy()
+    comm.set_timeout(0.2)
+    t = torch.ones(1024, device="cuda")
+    w = comm.all_reduce(t, "sum", async_op=True)
+    t0 = time.time()
+    try:
+        w.synchronize()
+        raise SystemExit("synchronize returned although the collective outlived the timeout")
+    except RuntimeError as e:
+        msg = str(e)
+    waited = time.time() - t0
+    assert "did not complete within" in msg and "all_reduce" in msg, msg
+    assert waited < 1.2, waited  # the watchdog's abort ended the wait, not the collective finishing
+    assert not comm.healthy() and not dist.healthy()
+    assert "all_reduce" in comm.error()
+    try:  # every later collective fails fast instead of hanging on the aborted communicator
+        dist.all_reduce(t)
+        raise SystemExit("a collective ran on the aborted communicator")
+    except RuntimeError as e:
+        assert "RCCL communicator failed" in str(e), str(e)
+    torch.cuda.synchronize()  # the delay kernel drains
+    dist.destroy_process_group()
+    print("WATCHDOG_OK", round(waited, 3))
+    """
+)
+
+
+def test_watchdog_aborts_a_stuck_collective():
+    """A collective that outlives set_timeout: the communicator's watchdog aborts it, the waiting
+    host call raises instead of hanging, healthy() goes false and the next collective raises
+    (csrc/runtime/rccl_comm.cpp watchdog_loop / abort / check)."""
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()), RANK="0", WORLD_SIZE="1",
+               LOCAL_RANK="0")
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env["PYTHONPATH"] = repo + os.pathsep + env.get("PYTHONPATH", "")
+    r = subprocess.run([sys.executable, "-c", WATCHDOG_SCRIPT], env=env, capture_output=True, text=True, timeout=200)
+    assert "WATCHDOG_OK" in r.stdout, r.stdout[-3000:] + r.stderr[-5000:]
