@@ -187,147 +187,4 @@ __device__ __forceinline__ void conv_tile_stats(const ConvGemmParams& p,
   }
 }
 
-// Same epilogue for the v_mfma_f32_16x16x32_bf16 accumulator layout: lane l holds column l&15
-// and rows 4*(l>>4) + r (r = 0..3) of each 16x16 tile; each wave owns (BM/2)x(BN/2) as
-// (BM/32)x(BN/32) tiles.
-template <int BM, int BN>
-__device__ __forceinline__ void conv_epilogue16(const ConvGemmParams& p,
-                                                f32x4 (&acc)[BM / waves_m<BM>() / 16][BN / 32], float* red, int m0,
-                                                int n0, int tm_idx, int split) {
-  constexpr int WM = waves_m<BM>();
-  constexpr int TM = BM / WM / 16, TN = BN / 32;
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wid = tid >> 6;
-  const int wm = wid >> 1, wn = wid & 1;
-  const int l16 = lane & 15;
-  const int q4 = (lane >> 4) * 4;
-  auto row_of = [&](int a, int r) { return m0 + wm * (BM / WM) + a * 16 + q4 + r; };
-  auto col_of = [&](int b) { return n0 + wn * (BN / 2) + b * 16 + l16; };
-  const bool full = m0 + BM <= p.M && n0 + BN <= p.Nout;
-  if (p.splits > 1) {
-    float* out = p.y + (long long)split * p.M * p.Nout;
-    auto slab_store = [&](auto pred) {
-#pragma unroll
-      for (int a = 0; a < TM; ++a)
-#pragma unroll
-        for (int b = 0; b < TN; ++b) {
-          const int n = col_of(b);
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int m = row_of(a, r);
-            if (!decltype(pred)::value || (m < p.M && n < p.Nout)) out[(long long)m * p.Nout + n] = acc[a][b][r];
-          }
-        }
-    };
-    if (full) slab_store(std::false_type{});
-    else slab_store(std::true_type{});
-    return;
-  }
-  if (p.addend) {  // y += addend (may alias y): every load is issued before any store
-#pragma unroll
-    for (int a = 0; a < TM; ++a)
-#pragma unroll
-      for (int b = 0; b < TN; ++b) {
-        const int n = col_of(b);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int m = row_of(a, r);
-          // branch-free (clamped address + select) so all loads issue before the first wait
-          const bool ok = m < p.M && n < p.Nout;
-          const float av = p.addend[ok ? remap_row(p.rr, m) * p.Nout + n : 0];
-          acc[a][b][r] += ok ? av : 0.f;
-        }
-      }
-  }
-  float bias_v[TN];
-#pragma unroll
-  for (int b = 0; b < TN; ++b) {
-    const int n = col_of(b);
-    bias_v[b] = (p.bias && n < p.Nout) ? p.bias[n] : 0.f;
-  }
-  auto out_store = [&](auto pred) {
-#pragma unroll
-    for (int a = 0; a < TM; ++a)
-#pragma unroll
-      for (int b = 0; b < TN; ++b) {
-        const int n = col_of(b);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int m = row_of(a, r);
-          const float v = acc[a][b][r] + bias_v[b];
-          acc[a][b][r] = v;
-          if (!decltype(pred)::value || (m < p.M && n < p.Nout)) p.y[remap_row(p.rr, m) * p.Nout + n] = v;
-        }
-      }
-  };
-  if (full) out_store(std::false_type{});
-  else out_store(std::true_type{});
-  if (!p.part) return;
-
-  __syncthreads();  // `red` aliases the operand LDS
-  const int cnt = min(BM, p.M - m0);
-  float colsum[TN];
-#pragma unroll
-  for (int b = 0; b < TN; ++b) {
-    float s = 0.f;
-#pragma unroll
-    for (int a = 0; a < TM; ++a)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) s += (row_of(a, r) < p.M) ? acc[a][b][r] : 0.f;
-    s += __shfl_xor(s, 16, kWave);
-    s += __shfl_xor(s, 32, kWave);
-    colsum[b] = s;
-  }
-  if (lane < 16) {
-#pragma unroll
-    for (int b = 0; b < TN; ++b) red[wm * BN + wn * (BN / 2) + b * 16 + l16] = colsum[b];
-  }
-  __syncthreads();
-  float mean_b[TN];
-#pragma unroll
-  for (int b = 0; b < TN; ++b) {
-    const int c = wn * (BN / 2) + b * 16 + l16;
-    float t = 0.f;
-#pragma unroll
-    for (int w = 0; w < WM; ++w) t += red[w * BN + c];
-    mean_b[b] = t / (float)cnt;
-  }
-  __syncthreads();
-#pragma unroll
-  for (int b = 0; b < TN; ++b) {
-    float s = 0.f;
-#pragma unroll
-    for (int a = 0; a < TM; ++a)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float d = acc[a][b][r] - mean_b[b];
-        s += (row_of(a, r) < p.M) ? d * d : 0.f;
-      }
-    s += __shfl_xor(s, 16, kWave);
-    s += __shfl_xor(s, 32, kWave);
-    colsum[b] = s;
-  }
-  if (lane < 16) {
-#pragma unroll
-    for (int b = 0; b < TN; ++b) red[wm * BN + wn * (BN / 2) + b * 16 + l16] = colsum[b];
-  }
-  __syncthreads();
-  if (wm == 0 && lane < 16) {
-#pragma unroll
-    for (int b = 0; b < TN; ++b) {
-      const int c = wn * (BN / 2) + b * 16 + l16;
-      const int n = n0 + c;
-      if (n < p.Nout) {
-        float* dst = p.part + ((long long)tm_idx * p.Nout + n) * 2;
-        float t = 0.f;
-#pragma unroll
-        for (int w = 0; w < WM; ++w) t += red[w * BN + c];
-        dst[0] = mean_b[b];
-        dst[1] = t;
-      }
-    }
-  }
-}
-
 }  // namespace cdp

@@ -21,518 +21,52 @@
 // 64 B with XOR-swizzled 16-B chunks (chunk_pos), conflict free for the ds_write_b128 stores and
 // the ds_read_b128 fragment reads. 96 KB of LDS for 128x128 (one workgroup per CU, the MFMA
 // pipe kept busy by the in-wave interleave), 72 KB for 64x128.
-#include <type_traits>
-
-#include "common.h"
-#include "kernels.h"
-#include "conv_epilogue.h"
-#include "x3_common.h"
+#include "conv_x3_body.h"
 
 namespace cdp {
 
 namespace {
 
-constexpr int BK = 32;
-constexpr int LDH = BK;  // bf16 per LDS row (64 B, 16-B chunks XOR-swizzled, see chunk_pos)
+using namespace x3conv;
 
-// 16-B chunk c (0..3) of LDS row r lives at chunk position c ^ f((r >> 2) & 3), f(q) = -q mod 4:
-// the 8-lane groups of the ds_write_b128 stores (two rows x four chunks) and the 16-lane groups
-// of the ds_read_b128 fragment reads hit distinct banks, both for the 32x32x16 operand (16 rows,
-// one chunk) and for the 16x16x32 operand (8 rows x 2 chunks).
-__device__ __forceinline__ int chunk_pos(int r, int c) { return c ^ ((-(r >> 2)) & 3); }
-
-// Split 8 consecutive-k fp32 values into three bf16x8 planes (as 4 packed pairs each).
-__device__ __forceinline__ void split8(const float (&v)[8], u32x4& s0, u32x4& s1, u32x4& s2) {
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    unsigned a, b, c;
-    split_pair(v[2 * j], v[2 * j + 1], a, b, c);
-    s0[j] = a;
-    s1[j] = b;
-    s2[j] = c;
-  }
-}
-
-// Split 8 consecutive-k fp32 values of an operand scaled by s into two fp16x8 planes (f16x2).
-__device__ __forceinline__ void split8h(const float (&v)[8], float s, u32x4& s0, u32x4& s1) {
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    unsigned a, b;
-    split_pair_h(v[2 * j], v[2 * j + 1], s, a, b);
-    s0[j] = a;
-    s1[j] = b;
-  }
-}
-
-// PS (pre-split): p.x / p.w hold three bf16 planes each ([3][N][H][W][C], [3][Nout][Kdim], as
-// written by split3_launch) and the tiles are copied to LDS without the split (MODE 0 only).
-// NP = 16-bit planes per operand: 3 = fp32-accurate bf16 split (six products), 2 = f16x2
-// (power-of-two-scaled operands as two fp16 terms, three products on v_mfma_f32_32x32x16_f16, see
-// x3_common.h), 1 = plain bf16 operands with fp32 accumulation (one product; the non-parity fast
-// mode, CDP_CONV_GEMM=bf16).
-// 8 consecutive-k fp32 values rounded to bf16 (one plane)
-__device__ __forceinline__ u32x4 pack8(const float (&v)[8]) {
-  u32x4 r;
-#pragma unroll
-  for (int j = 0; j < 4; ++j) r[j] = pack_bf16x2(f32x2{v[2 * j], v[2 * j + 1]});
-  return r;
-}
-
-template <int BM, int BN, int MODE, bool DGRAD, bool M16, bool PS = false, int NP = 3>
+template <int BM, int BN, int MODE, bool DGRAD, int NP = 3>
 __global__ __launch_bounds__(waves_m<BM>() * 128, (NP == 2 && BM + BN <= 256) ? 2 : (BM + BN >= 256) ? 1 : 2) void
 conv_x3_kernel(ConvGemmParams p) {
-  static_assert(!PS || MODE == 0, "pre-split operands need C % 32 == 0");
-  static_assert(NP == 3 || ((NP == 1 || NP == 2) && !PS), "planes");
-  static_assert(NP != 2 || !M16, "f16x2 uses the 32x32x16 tiles");
-  constexpr unsigned ES = PS ? 1u : 2u;  // log2 bytes per element of the global operands
-  constexpr int WM = waves_m<BM>();  // waves along M (2 x WM waves)
-  constexpr int NT = WM * 128;       // threads
-  constexpr int RS = NT / 4;         // rows covered by one pass of the loaders
-  constexpr int TM = BM / WM / 32;
-  constexpr int TN = BN / 64;
-  constexpr int A_LD = BM / RS;  // A rows per thread (row = tid/4 + RS i), 8 consecutive k each
-  constexpr int B_LD = BN / RS;
-  static_assert(A_LD >= 1 && B_LD >= 1, "tile too narrow for the loader");
-  constexpr int PA = BM * LDH, PB = BN * LDH;
-  constexpr int STAGE = NP * (PA + PB);  // bf16 per stage: A planes [NP][BM][LDH], B planes [NP][BN][LDH]
-  static_assert(2 * STAGE * 2 >= 2 * BN * 4, "epilogue scratch");
-  __shared__ __attribute__((aligned(16))) __bf16 smem[2 * STAGE];
-
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wid = tid >> 6;
-  const int wm = wid >> 1, wn = wid & 1;
-
-  const int ntn = (p.Nout + BN - 1) / BN;
-  const int bid = xcd_remap(blockIdx.x, gridDim.x);
-  const int tn_idx = bid % ntn;
-  const int rest = bid / ntn;
-  const int split = rest % p.splits;
-  const int tm_idx = rest / p.splits;
-  const int m0 = tm_idx * BM, n0 = tn_idx * BN;
-  const int kt_begin = (int)(((long long)split * p.ktiles) / p.splits);
-  const int kt_end = (int)(((long long)(split + 1) * p.ktiles) / p.splits);
-  const int PQ = p.P * p.Q;
-  const int HWC = p.H * p.W * p.C;
-
-  const int kq = (tid & 3) * 8;  // this thread's 8 consecutive k within the tile
-  const int rrow = tid >> 2;     // + RS i
-
-  // buffers (host guarantees < 2 GiB each): out-of-range offsets read as zero
-  const unsigned xplane = ((unsigned)p.N * (unsigned)HWC) << ES;
-  const unsigned wplane = ((unsigned)p.Nout * (unsigned)p.Kdim) << ES;
-  const __amdgpu_buffer_rsrc_t xr = make_rsrc(p.x, PS ? 3u * xplane : xplane);
-  const __amdgpu_buffer_rsrc_t wr = make_rsrc(p.w, PS ? 3u * wplane : wplane);
-
-  // per A row: spatial anchor and element offset of (n, anchor, kq)
-  int a_h[A_LD], a_w[A_LD], a_n[A_LD], a_off[A_LD];
-#pragma unroll
-  for (int i = 0; i < A_LD; ++i) {
-    const int m = m0 + rrow + RS * i;
-    const bool ok = m < p.M;
-    const int mm = ok ? m : 0;
-    const int n = fdiv(mm, p.fd_PQ);
-    const int rem = mm - mul24(n, PQ);
-    const int pp = fdiv(rem, p.fd_Q);
-    const int qq = rem - mul24(pp, p.Q);
-    if (DGRAD) {
-      a_h[i] = pp + p.pad;  // oh*stride = ih + pad - kh
-      a_w[i] = qq + p.pad_w;  // column pad (differs from pad in sub-pixel class launches)
-    } else {
-      a_h[i] = mul24(pp, p.stride) - p.pad;
-      a_w[i] = mul24(qq, p.stride) - p.pad;
-    }
-    if (!ok) a_h[i] = -(1 << 22);  // fails every bounds test below
-    a_n[i] = mul24(n, HWC);
-    a_off[i] = a_n[i] + mul24(mul24(a_h[i], p.W) + a_w[i], p.C) + kq;
-  }
-  // per B row: byte offset of (row, kq); rows past Nout read zeros
-  unsigned b_off[B_LD];
-#pragma unroll
-  for (int i = 0; i < B_LD; ++i) {
-    const int n = n0 + rrow + RS * i;
-    b_off[i] = n < p.Nout ? (unsigned)(mul24(n, p.Kdim) + kq) << ES : kOOB;
-  }
-
-  // f16x2: power-of-two operand scales from the producers' partial maxima (wave-uniform); the
-  // partial loads go out first and are waited for after the first tiles' loads are issued
-  float sa = 1.f, sb = 1.f;
-  float amx_a[NP == 2 ? kAmaxK : 1], amx_b[NP == 2 ? kAmaxK : 1];
-  if constexpr (NP == 2) {
-    amax_issue(p.amax_a, p.amax_na, amx_a);
-    amax_issue(p.amax_b, p.amax_nb, amx_b);
-  }
-
-  // byte offset of A row i at filter tap (kh, kw), channel offset c (relative to kq); OOB if padded
-  auto a_voff = [&](int i, int kh, int kw, int c) -> unsigned {
-    if (DGRAD) {
-      int oh = a_h[i] - kh, ow = a_w[i] - kw;
-      if (p.stride == 1) {
-        const bool ok = (unsigned)oh < (unsigned)p.H && (unsigned)ow < (unsigned)p.W;
-        return ok ? (unsigned)(a_off[i] - mul24(mul24(kh, p.W) + kw, p.C) + c) << ES : kOOB;
-      }
-      bool ok = oh >= 0 && ow >= 0 && ((oh | ow) & (p.stride - 1)) == 0;  // stride is 2 (power of two)
-      oh >>= 1;
-      ow >>= 1;
-      ok = ok && oh < p.H && ow < p.W;
-      return ok ? (unsigned)(a_n[i] + mul24(mul24(oh, p.W) + ow, p.C) + kq + c) << ES : kOOB;
-    } else {
-      const int ih = a_h[i] + kh, iw = a_w[i] + kw;
-      const bool ok = (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W;
-      return ok ? (unsigned)(a_off[i] + mul24(mul24(kh, p.W) + kw, p.C) + c) << ES : kOOB;
-    }
-  };
-
-  // register ping-pong: fp32 tiles (8 k per row) or, pre-split, three bf16x8 planes per row
-  typedef std::conditional_t<PS, u32x4[A_LD][3], float[A_LD][8]> StageA;
-  typedef std::conditional_t<PS, u32x4[B_LD][3], float[B_LD][8]> StageB;
-  StageA va0, va1;
-  StageB vb0, vb1;
-
-  auto put4 = [](float (&d)[8], int off, float4 v) {
-    d[off] = v.x;
-    d[off + 1] = v.y;
-    d[off + 2] = v.z;
-    d[off + 3] = v.w;
-  };
-
-  // valid == false: every offset is past the buffers, so the loads return zeros without touching
-  // memory. Issuing them unconditionally (no branch around the prefetch) lets the compiler wait
-  // with vmcnt(#newer loads) for the older tile instead of vmcnt(0) at a control-flow merge,
-  // which would have drained the prefetch of the next tile.
-  auto load_tile = [&](int kt, auto& va, auto& vb, bool valid) {
-    const int r0 = kt * BK;
-    if constexpr (PS) {
-      const int tap = fdiv(r0, p.fd_C);
-      const int c0 = r0 - tap * p.C;
-      const int kh = fdiv(tap, p.fd_KW), kw = tap - kh * p.KW;
-#pragma unroll
-      for (int i = 0; i < A_LD; ++i) {
-        const unsigned o = valid ? a_voff(i, kh, kw, c0) : kOOB;
-#pragma unroll
-        for (int q = 0; q < 3; ++q) va[i][q] = __builtin_amdgcn_raw_buffer_load_b128(xr, (int)(o + q * xplane), 0, 0);
-      }
-#pragma unroll
-      for (int i = 0; i < B_LD; ++i) {
-        const unsigned o = valid ? b_off[i] + ((unsigned)r0 << ES) : kOOB;
-#pragma unroll
-        for (int q = 0; q < 3; ++q) vb[i][q] = __builtin_amdgcn_raw_buffer_load_b128(wr, (int)(o + q * wplane), 0, 0);
-      }
-      return;
-    } else if (MODE == 0) {
-      // the whole K-tile lies in one filter tap (C % 32 == 0): tap decode is wave-uniform
-      const int tap = fdiv(r0, p.fd_C);
-      const int c0 = r0 - tap * p.C;
-      const int kh = fdiv(tap, p.fd_KW), kw = tap - kh * p.KW;
-#pragma unroll
-      for (int i = 0; i < A_LD; ++i) {
-        const unsigned o = valid ? a_voff(i, kh, kw, c0) : kOOB;
-        put4(va[i], 0, bload4(xr, o));
-        put4(va[i], 4, bload4(xr, o + 16u));
-      }
-    } else if (MODE == 1) {
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const int r = r0 + kq + 4 * h;
-        const bool rok = valid && r < p.Kdim;
-        const int tap = fdiv(rok ? r : 0, p.fd_C);
-        const int c = r - tap * p.C;
-        const int kh = fdiv(tap, p.fd_KW), kw = tap - kh * p.KW;
-#pragma unroll
-        for (int i = 0; i < A_LD; ++i) {
-          const unsigned o = rok ? a_voff(i, kh, kw, c - kq) : kOOB;
-          put4(va[i], 4 * h, bload4(xr, o));
-        }
-      }
-    } else {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int r = r0 + kq + j;
-        const bool rok = valid && r < p.Kdim;
-        const int tap = fdiv(rok ? r : 0, p.fd_C);
-        const int c = r - tap * p.C;
-        const int kh = fdiv(tap, p.fd_KW), kw = tap - kh * p.KW;
-#pragma unroll
-        for (int i = 0; i < A_LD; ++i) {
-          const unsigned o = rok ? a_voff(i, kh, kw, c - kq) : kOOB;
-          va[i][j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xr, (int)o, 0, 0));
-        }
-      }
-    }
-    if constexpr (!PS) {
-#pragma unroll
-    for (int i = 0; i < B_LD; ++i) {
-      const unsigned o = valid ? b_off[i] + ((unsigned)r0 << ES) : kOOB;
-      if (MODE == 0) {
-        put4(vb[i], 0, bload4(wr, o));
-        put4(vb[i], 4, bload4(wr, o + 16u));
-      } else if (MODE == 1) {
-        // Kdim % 4 == 0: a float4 is either inside the row or wholly past its end
-        put4(vb[i], 0, bload4(wr, r0 + kq < p.Kdim ? o : kOOB));
-        put4(vb[i], 4, bload4(wr, r0 + kq + 4 < p.Kdim ? o + 16u : kOOB));
-      } else {
-#pragma unroll
-        for (int j = 0; j < 8; ++j)
-          vb[i][j] = __uint_as_float(
-              __builtin_amdgcn_raw_buffer_load_b32(wr, (int)(r0 + kq + j < p.Kdim ? o + 4u * j : kOOB), 0, 0));
-      }
-    }
-    }
-  };
-
-  auto store_tile = [&](const auto& va, const auto& vb, __bf16* st) {
-    const int cp = chunk_pos(rrow, tid & 3) * 8;  // rrow + RS i has the same (row >> 2) & 3
-    if constexpr (PS) {
-#pragma unroll
-      for (int i = 0; i < A_LD; ++i) {
-        __bf16* d = st + (rrow + RS * i) * LDH + cp;
-#pragma unroll
-        for (int q = 0; q < 3; ++q) *reinterpret_cast<u32x4*>(d + q * PA) = va[i][q];
-      }
-#pragma unroll
-      for (int i = 0; i < B_LD; ++i) {
-        __bf16* d = st + NP * PA + (rrow + RS * i) * LDH + cp;
-#pragma unroll
-        for (int q = 0; q < 3; ++q) *reinterpret_cast<u32x4*>(d + q * PB) = vb[i][q];
-      }
-    } else {
-#pragma unroll
-    for (int i = 0; i < A_LD; ++i) {
-      __bf16* d = st + (rrow + RS * i) * LDH + cp;
-      if constexpr (NP == 1) {
-        *reinterpret_cast<u32x4*>(d) = pack8(va[i]);
-      } else if constexpr (NP == 2) {
-        u32x4 s0, s1;
-        split8h(va[i], sa, s0, s1);
-        *reinterpret_cast<u32x4*>(d) = s0;
-        *reinterpret_cast<u32x4*>(d + PA) = s1;
-      } else {
-        u32x4 s0, s1, s2;
-        split8(va[i], s0, s1, s2);
-        *reinterpret_cast<u32x4*>(d) = s0;
-        *reinterpret_cast<u32x4*>(d + PA) = s1;
-        *reinterpret_cast<u32x4*>(d + 2 * PA) = s2;
-      }
-    }
-#pragma unroll
-    for (int i = 0; i < B_LD; ++i) {
-      __bf16* d = st + NP * PA + (rrow + RS * i) * LDH + cp;
-      if constexpr (NP == 1) {
-        *reinterpret_cast<u32x4*>(d) = pack8(vb[i]);
-      } else if constexpr (NP == 2) {
-        u32x4 s0, s1;
-        split8h(vb[i], sb, s0, s1);
-        *reinterpret_cast<u32x4*>(d) = s0;
-        *reinterpret_cast<u32x4*>(d + PB) = s1;
-      } else {
-        u32x4 s0, s1, s2;
-        split8(vb[i], s0, s1, s2);
-        *reinterpret_cast<u32x4*>(d) = s0;
-        *reinterpret_cast<u32x4*>(d + PB) = s1;
-        *reinterpret_cast<u32x4*>(d + 2 * PB) = s2;
-      }
-    }
-    }
-  };
-
-  // accumulators: 32x32x16 tiles (TM x TN) or 16x16x32 tiles (2TM x 2TN)
-  f32x16 acc[TM][TN];
-  f32x4 acc16[M16 ? 2 * TM : 1][M16 ? 2 * TN : 1];
-  if constexpr (M16) {
-#pragma unroll
-    for (int a = 0; a < 2 * TM; ++a)
-#pragma unroll
-      for (int b = 0; b < 2 * TN; ++b) acc16[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
-  } else {
-#pragma unroll
-    for (int a = 0; a < TM; ++a)
-#pragma unroll
-      for (int b = 0; b < TN; ++b)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
-  }
-
-  const int l32 = lane & 31;
-  const int hh = lane >> 5;
-
-  // MFMAs over one LDS stage: six split products per output tile and 32-deep K-tile, as two
-  // 32x32x16 steps or one 16x16x32 step
-  auto compute = [&](const __bf16* st) {
-    if constexpr (M16) {
-      const int l16 = lane & 15, ch = lane >> 4;
-      bf16x8 bf[2 * TN][3];
-#pragma unroll
-      for (int b = 0; b < 2 * TN; ++b) {
-        const int r = wn * (BN / 2) + b * 16 + l16;
-        const __bf16* src = st + NP * PA + r * LDH + chunk_pos(r, ch) * 8;
-#pragma unroll
-        for (int q = 0; q < NP; ++q) bf[b][q] = *reinterpret_cast<const bf16x8*>(src + q * PB);
-      }
-#pragma unroll
-      for (int a = 0; a < 2 * TM; ++a) {
-        bf16x8 af[3];
-        const int r = wm * (BM / WM) + a * 16 + l16;
-        const __bf16* src = st + r * LDH + chunk_pos(r, ch) * 8;
-#pragma unroll
-        for (int q = 0; q < NP; ++q) af[q] = *reinterpret_cast<const bf16x8*>(src + q * PA);
-#pragma unroll
-        for (int b = 0; b < 2 * TN; ++b) {
-          f32x4 c = acc16[a][b];
-          if constexpr (NP == 1) {
-            acc16[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[0], bf[b][0], c, 0, 0, 0);
-            continue;
-          }
-          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[2], bf[b][0], c, 0, 0, 0);
-          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[1], bf[b][1], c, 0, 0, 0);
-          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[0], bf[b][2], c, 0, 0, 0);
-          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[1], bf[b][0], c, 0, 0, 0);
-          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[0], bf[b][1], c, 0, 0, 0);
-          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[0], bf[b][0], c, 0, 0, 0);
-          acc16[a][b] = c;
-        }
-      }
-    } else if constexpr (NP == 2) {
-#pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        f16x8 af[TM][2], bf[TN][2];
-#pragma unroll
-        for (int a = 0; a < TM; ++a) {
-          const int r = wm * (BM / WM) + a * 32 + l32;
-          const __bf16* src = st + r * LDH + chunk_pos(r, 2 * s + hh) * 8;
-#pragma unroll
-          for (int q = 0; q < 2; ++q) af[a][q] = *reinterpret_cast<const f16x8*>(src + q * PA);
-        }
-#pragma unroll
-        for (int b = 0; b < TN; ++b) {
-          const int r = wn * (BN / 2) + b * 32 + l32;
-          const __bf16* src = st + NP * PA + r * LDH + chunk_pos(r, 2 * s + hh) * 8;
-#pragma unroll
-          for (int q = 0; q < 2; ++q) bf[b][q] = *reinterpret_cast<const f16x8*>(src + q * PB);
-        }
-#pragma unroll
-        for (int a = 0; a < TM; ++a)
-#pragma unroll
-          for (int b = 0; b < TN; ++b) {
-            f32x16 c = acc[a][b];
-            c = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[a][1], bf[b][0], c, 0, 0, 0);
-            c = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[a][0], bf[b][1], c, 0, 0, 0);
-            c = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[a][0], bf[b][0], c, 0, 0, 0);
-            acc[a][b] = c;
-          }
-      }
-    } else {
-#pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        bf16x8 af[TM][3], bf[TN][3];
-#pragma unroll
-        for (int a = 0; a < TM; ++a) {
-          const int r = wm * (BM / WM) + a * 32 + l32;
-          const __bf16* src = st + r * LDH + chunk_pos(r, 2 * s + hh) * 8;
-#pragma unroll
-          for (int q = 0; q < NP; ++q) af[a][q] = *reinterpret_cast<const bf16x8*>(src + q * PA);
-        }
-#pragma unroll
-        for (int b = 0; b < TN; ++b) {
-          const int r = wn * (BN / 2) + b * 32 + l32;
-          const __bf16* src = st + NP * PA + r * LDH + chunk_pos(r, 2 * s + hh) * 8;
-#pragma unroll
-          for (int q = 0; q < NP; ++q) bf[b][q] = *reinterpret_cast<const bf16x8*>(src + q * PB);
-        }
-#pragma unroll
-        for (int a = 0; a < TM; ++a)
-#pragma unroll
-          for (int b = 0; b < TN; ++b) {
-            f32x16 c = acc[a][b];
-            if constexpr (NP == 1) {
-              acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[a][0], bf[b][0], c, 0, 0, 0);
-              continue;
-            }
-            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[a][2], bf[b][0], c, 0, 0, 0);
-            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[a][1], bf[b][1], c, 0, 0, 0);
-            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[a][0], bf[b][2], c, 0, 0, 0);
-            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[a][1], bf[b][0], c, 0, 0, 0);
-            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[a][0], bf[b][1], c, 0, 0, 0);
-            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[a][0], bf[b][0], c, 0, 0, 0);
-            acc[a][b] = c;
-          }
-      }
-    }
-  };
-
-  // Software pipeline, one barrier per K-tile: while the MFMAs consume stage t&1, tile t+1
-  // (loaded into registers one iteration earlier) is split into stage (t+1)&1 and tile t+2 is
-  // being fetched into the other register set.
-  if (kt_begin < kt_end) {
-    load_tile(kt_begin, va0, vb0, true);
-    load_tile(kt_begin + 1, va1, vb1, kt_begin + 1 < kt_end);
-    if constexpr (NP == 2) {
-      sa = amax_finish(p.amax_a, p.amax_na, amx_a);
-      sb = amax_finish(p.amax_b, p.amax_nb, amx_b);
-    }
-    store_tile(va0, vb0, smem);
-    __syncthreads();
-    int kt = kt_begin;
-    for (; kt + 1 < kt_end; kt += 2) {
-      load_tile(kt + 2, va0, vb0, kt + 2 < kt_end);
-      compute(smem);
-      store_tile(va1, vb1, smem + STAGE);
-      __syncthreads();
-      load_tile(kt + 3, va1, vb1, kt + 3 < kt_end);
-      compute(smem + STAGE);
-      // unconditional (past the last tile it stores stale registers into a stage nothing reads),
-      // so the split can interleave with the MFMAs above
-      store_tile(va0, vb0, smem);
-      __syncthreads();
-    }
-    if (kt < kt_end) compute(smem);  // odd tile count: the last tile sits in stage 0
-  } else if constexpr (NP == 2) {  // no K-tiles: the (zero) accumulators still get unscaled
-    sa = amax_finish(p.amax_a, p.amax_na, amx_a);
-    sb = amax_finish(p.amax_b, p.amax_nb, amx_b);
-  }
-
-  if constexpr (NP == 2) {  // undo the operand scales (exact: powers of two)
-    const float inv = 1.f / (sa * sb);
-#pragma unroll
-    for (int a = 0; a < TM; ++a)
-#pragma unroll
-      for (int b = 0; b < TN; ++b) acc[a][b] *= inv;
-  }
-  if constexpr (M16) conv_epilogue16<BM, BN>(p, acc16, reinterpret_cast<float*>(smem), m0, n0, tm_idx, split);
-  else conv_epilogue<BM, BN>(p, acc, reinterpret_cast<float*>(smem), m0, n0, tm_idx, split);
+  __shared__ __attribute__((aligned(16))) __bf16 smem[conv_x3_smem_elems<BM, BN, NP>()];
+  conv_x3_body<BM, BN, MODE, DGRAD, NP>(p, smem, blockIdx.x, gridDim.x);
 }
 
 template <int BM, int BN, int MODE, bool DGRAD>
-void launch_x3(const ConvGemmParams& p, int ntiles, bool m16, int np, hipStream_t st) {
+void launch_x3(const ConvGemmParams& p, int ntiles, int np, hipStream_t st) {
   const dim3 blk(waves_m<BM>() * 128), grd(ntiles * p.splits);
-  if (np == 1) hipLaunchKernelGGL((conv_x3_kernel<BM, BN, MODE, DGRAD, false, false, 1>), grd, blk, 0, st, p);
-  else if (np == 2) hipLaunchKernelGGL((conv_x3_kernel<BM, BN, MODE, DGRAD, false, false, 2>), grd, blk, 0, st, p);
-  else if (m16) hipLaunchKernelGGL((conv_x3_kernel<BM, BN, MODE, DGRAD, true>), grd, blk, 0, st, p);
-  else hipLaunchKernelGGL((conv_x3_kernel<BM, BN, MODE, DGRAD, false>), grd, blk, 0, st, p);
+  if (np == 1) hipLaunchKernelGGL((conv_x3_kernel<BM, BN, MODE, DGRAD, 1>), grd, blk, 0, st, p);
+  else if (np == 2) hipLaunchKernelGGL((conv_x3_kernel<BM, BN, MODE, DGRAD, 2>), grd, blk, 0, st, p);
+  else hipLaunchKernelGGL((conv_x3_kernel<BM, BN, MODE, DGRAD, 3>), grd, blk, 0, st, p);
 }
 
 template <int MODE, bool DGRAD>
-void dispatch_x3(const ConvGemmParams& p, int bm, int bn, bool m16, int np, hipStream_t st) {
+void dispatch_x3(const ConvGemmParams& p, int bm, int bn, int np, hipStream_t st) {
   const int ntm = (p.M + bm - 1) / bm, ntn = (p.Nout + bn - 1) / bn;
   const int nt = ntm * ntn;
-  if (bm == 256) launch_x3<256, 128, MODE, DGRAD>(p, nt, m16, np, st);
-  else if (bm == 128 && bn == 128) launch_x3<128, 128, MODE, DGRAD>(p, nt, m16, np, st);
-  else if (bm == 128 && bn == 64) launch_x3<128, 64, MODE, DGRAD>(p, nt, m16, np, st);
-  else if (bm == 64 && bn == 128) launch_x3<64, 128, MODE, DGRAD>(p, nt, m16, np, st);
-  else launch_x3<64, 64, MODE, DGRAD>(p, nt, m16, np, st);
+  if (bm == 256) launch_x3<256, 128, MODE, DGRAD>(p, nt, np, st);
+  else if (bm == 128 && bn == 128) launch_x3<128, 128, MODE, DGRAD>(p, nt, np, st);
+  else if (bm == 128 && bn == 64) launch_x3<128, 64, MODE, DGRAD>(p, nt, np, st);
+  else if (bm == 64 && bn == 128) launch_x3<64, 128, MODE, DGRAD>(p, nt, np, st);
+  else launch_x3<64, 64, MODE, DGRAD>(p, nt, np, st);
 }
 
 }  // namespace
 
-void conv_x3_launch(const ConvGemmParams& p, int bm, int bn, bool dgrad, bool m16, hipStream_t st, int np) {
+void conv_x3_launch(const ConvGemmParams& p, int bm, int bn, bool dgrad, hipStream_t st, int np) {
   if ((p.C % BK) == 0 && (p.Kdim % BK) == 0) {
-    if (dgrad) dispatch_x3<0, true>(p, bm, bn, m16, np, st);
-    else dispatch_x3<0, false>(p, bm, bn, m16, np, st);
+    if (dgrad) dispatch_x3<0, true>(p, bm, bn, np, st);
+    else dispatch_x3<0, false>(p, bm, bn, np, st);
   } else if ((p.C % 4) == 0 && (p.Kdim % 4) == 0) {
-    if (dgrad) dispatch_x3<1, true>(p, bm, bn, m16, np, st);
-    else dispatch_x3<1, false>(p, bm, bn, m16, np, st);
+    if (dgrad) dispatch_x3<1, true>(p, bm, bn, np, st);
+    else dispatch_x3<1, false>(p, bm, bn, np, st);
   } else {
-    if (dgrad) dispatch_x3<2, true>(p, bm, bn, m16, np, st);
-    else dispatch_x3<2, false>(p, bm, bn, m16, np, st);
+    if (dgrad) dispatch_x3<2, true>(p, bm, bn, np, st);
+    else dispatch_x3<2, false>(p, bm, bn, np, st);
   }
 }
 

@@ -85,11 +85,10 @@ struct WgradParams {
 // conv_igemm.hip (exact fp32-input MFMA)
 void conv_igemm_launch(const ConvGemmParams& p, int bm, int bn, bool dgrad, hipStream_t st);
 // conv_x3.hip (fp32-accurate 3-term bf16 split on the bf16 MFMA)
-// (m16: v_mfma_f32_16x16x32_bf16 tiles instead of 32x32x16)
 // np = operand planes: 3 = split-bf16 (six products), 2 = f16x2 (power-of-two-scaled operands,
 // two fp16 terms, three products; needs p.amax_*), 1 = operands rounded to bf16, one product per
 // MAC (the non-parity fast mode)
-void conv_x3_launch(const ConvGemmParams& p, int bm, int bn, bool dgrad, bool m16, hipStream_t st, int np = 3);
+void conv_x3_launch(const ConvGemmParams& p, int bm, int bn, bool dgrad, hipStream_t st, int np = 3);
 void splitk_reduce_launch(const float* slab, int S, int M, int Nout, const float* bias, float* y, float* part,
                           hipStream_t st, const RowRemap* rr = nullptr, const float* addend = nullptr);
 int splitk_rows_per_part();
@@ -135,6 +134,11 @@ int stem_wgrad_blocks(int N, int H, int W);
 // Co = 64, even H and W
 void stem_wgrad_launch(const float* y, const float* gout, const float* stats, const float* sums, const float* x,
                        float* slab, int nblk, int N, int H, int W, int Cin, hipStream_t st);
+
+// bwd_pair.hip: a block's data-gradient GEMM (MODE 0 transposed gather) and weight-gradient GEMM in
+// one launch, when both are f16x2 256x128 tiles (bwd_pair_ok)
+bool bwd_pair_ok(const ConvGemmParams& pd, int bm, int bn, const WgradParams& pw, int wbm, int wbn, int np);
+void bwd_pair_launch(const ConvGemmParams& pd, const WgradParams& pw, hipStream_t st);
 
 // bwd_fuse.hip: one launch that finishes a block's two gradient GEMMs' split-K slabs and starts the
 // previous block's BatchNorm backward (see the file header).

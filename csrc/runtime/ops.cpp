@@ -199,18 +199,10 @@ bool x3_ok(const WgradParams& p) {
          (long long)p.P * p.Q < kIdx;
 }
 
-bool m16_on() {
-  static const bool m16 = [] {
-    const char* e = std::getenv("CDP_MFMA16");
-    return e && e[0] == '1';  // measured: 16x16x32 tiles ran ~2% slower on VGG-11
-  }();
-  return m16 && !f16x2_mode();
-}
-
 void conv_launch(const ConvGemmParams& p, int bm, int bn, bool dgrad, hipStream_t st) {
   if (x3_family() && x3_ok(p, dgrad)) {
     TORCH_CHECK(!f16x2_mode() || (p.amax_a && p.amax_b), "f16x2 conv GEMM launched without operand maxima");
-    conv_x3_launch(p, bm, bn, dgrad, m16_on(), st, split_planes());
+    conv_x3_launch(p, bm, bn, dgrad, st, split_planes());
   }
   else conv_igemm_launch(p, bm, bn, dgrad, st);
 }
@@ -237,6 +229,32 @@ struct DeferredReduce {
   int d_S = 0, d_M = 0, d_Nout = 0;
 };
 
+// A weight-gradient GEMM held back so the data-gradient GEMM of the same block can run beside it in
+// one launch (bwd_pair.hip); `after` is the work that must follow it (its slab reduction), if any.
+struct PendingWgrad {
+  bool set = false;
+  WgradParams p{};
+  int bm = 0, bn = 0;
+  std::function<void()> after;
+  void run_after() {
+    set = false;
+    if (after) after();
+    after = nullptr;
+  }
+  // launch it alone (no data-gradient GEMM took it)
+  void flush(hipStream_t st) {
+    if (!set) return;
+    wgrad_launch(p, bm, bn, true, st, 2);
+    run_after();
+  }
+};
+
+// CDP_BWD_PAIR=0: the two gradient GEMMs of a block as two launches
+bool bwd_pair_enabled() {
+  const char* e = std::getenv("CDP_BWD_PAIR");
+  return !(e && e[0] == '0');
+}
+
 bool bwd_fuse_enabled() {
   static const bool on = [] {
     const char* e = std::getenv("CDP_BWD_FUSE");
@@ -248,13 +266,26 @@ bool bwd_fuse_enabled() {
 // alloc_part(rows_per_part), when given, returns the BN partial buffer for that layout.
 // defer, when given, takes over a plain split-K reduction (no bias / BN partials / row scatter):
 // the GEMM is enqueued and the reduction left to the caller's bwd_reduce launch.
+// The conv GEMM launch, or -- a pending weight gradient of the same block given and both GEMMs
+// being f16x2 256x128 tiles -- both GEMMs in one bwd_pair launch.
+void conv_launch_or_pair(const ConvGemmParams& p, const GemmPlan& g, bool dgrad, hipStream_t st,
+                         PendingWgrad* pending) {
+  if (pending && pending->set && dgrad && f16x2_mode() && x3_ok(p, true) && p.amax_a && p.amax_b &&
+      bwd_pair_ok(p, g.bm, g.bn, pending->p, pending->bm, pending->bn, split_planes())) {
+    bwd_pair_launch(p, pending->p, st);
+    pending->run_after();
+    return;
+  }
+  conv_launch(p, g.bm, g.bn, dgrad, st);
+}
+
 int conv_gemm_splitk(ConvGemmParams p, const GemmPlan& g, bool dgrad, hipStream_t st, at::TensorOptions opts,
                      std::vector<at::Tensor>& keep, const std::function<float*(int)>& alloc_part = nullptr,
-                     DeferredReduce* defer = nullptr) {
+                     DeferredReduce* defer = nullptr, PendingWgrad* pending = nullptr) {
   p.splits = g.splits;
   if (g.splits == 1) {
     if (alloc_part) p.part = alloc_part(g.bm);
-    conv_launch(p, g.bm, g.bn, dgrad, st);
+    conv_launch_or_pair(p, g, dgrad, st, pending);
     return g.bm;
   }
   at::Tensor slab = at::empty({g.splits, (long long)p.M, p.Nout}, opts);
@@ -268,7 +299,7 @@ int conv_gemm_splitk(ConvGemmParams p, const GemmPlan& g, bool dgrad, hipStream_
     defer->d_Nout = p.Nout;
     p.y = slab.data_ptr<float>();
     p.addend = nullptr;
-    conv_launch(p, g.bm, g.bn, dgrad, st);
+    conv_launch_or_pair(p, g, dgrad, st, pending);
     return splitk_rows_per_part();
   }
   float* y = p.y;
@@ -281,7 +312,7 @@ int conv_gemm_splitk(ConvGemmParams p, const GemmPlan& g, bool dgrad, hipStream_
   p.addend = nullptr;
   p.part = nullptr;
   p.rr.on = 0;  // slabs are class-local; the reduction scatters
-  conv_launch(p, g.bm, g.bn, dgrad, st);
+  conv_launch_or_pair(p, g, dgrad, st, pending);
   splitk_reduce_launch(slab.data_ptr<float>(), g.splits, p.M, p.Nout, bias, y, part, st, rr.on ? &rr : nullptr,
                        addend);
   return splitk_rows_per_part();
@@ -564,7 +595,7 @@ bool conv2d_dgrad_subpixel(const at::Tensor& dy, const at::Tensor& w, at::Tensor
 at::Tensor dgrad_impl(const at::Tensor& dy_, const at::Tensor& w_, std::vector<int64_t> in_shape, int64_t stride,
                       int64_t pad, const c10::optional<at::Tensor>& addend, const c10::optional<at::Tensor>& dy_amax,
                       const c10::optional<at::Tensor>& w_amax, const c10::optional<at::Tensor>& w_t,
-                      DeferredReduce* defer) {
+                      DeferredReduce* defer, PendingWgrad* pending = nullptr) {
   check_f32_cuda(dy_, "grad_output");
   check_f32_cuda(w_, "weight");
   const at::Tensor dy = nhwc(dy_);
@@ -611,7 +642,7 @@ at::Tensor dgrad_impl(const at::Tensor& dy_, const at::Tensor& w_, std::vector<i
   p.y = dx.data_ptr<float>();
   p.addend = addp;
   std::vector<at::Tensor> keep;
-  conv_gemm_splitk(p, g, true, st, opts, keep, nullptr, defer);
+  conv_gemm_splitk(p, g, true, st, opts, keep, nullptr, defer, pending);
   return dx;
 }
 
@@ -634,7 +665,7 @@ at::Tensor conv2d_wgrad(const at::Tensor& dy_, const at::Tensor& x_, std::vector
 at::Tensor wgrad_impl(const at::Tensor& dy_, const at::Tensor& x_, std::vector<int64_t> w_shape, int64_t stride,
                       int64_t pad, const c10::optional<at::Tensor>& out, bool accumulate, int64_t keep_c,
                       const c10::optional<at::Tensor>& dy_amax, const c10::optional<at::Tensor>& x_amax,
-                      DeferredReduce* defer) {
+                      DeferredReduce* defer, PendingWgrad* pending = nullptr) {
   check_f32_cuda(dy_, "grad_output");
   check_f32_cuda(x_, "input");
   const at::Tensor dy = nhwc(dy_);
@@ -667,13 +698,27 @@ at::Tensor wgrad_impl(const at::Tensor& dy_, const at::Tensor& x_, std::vector<i
   set_divs(p);
   const at::Tensor dya = amax_parts(dy, dy_amax, st), xa = amax_parts(x, x_amax, st);
   set_amax(p, dya, xa);
+  // the GEMM launch, held back in `pending` when it can run beside the block's data gradient
+  const bool hold = pending && f16x2_mode() && x3_ok(p) && wp.bm == 256 && wp.bn == 128 && (C % 4) == 0 &&
+                    (Co % 4) == 0 && p.amax_dy && p.amax_x;
+  auto launch = [&](std::function<void()> after) {
+    if (hold) {
+      pending->set = true;
+      pending->p = p;
+      pending->bm = wp.bm;
+      pending->bn = wp.bn;
+      pending->after = std::move(after);
+      return;
+    }
+    wgrad_launch(p, wp.bm, wp.bn, x3_family() && x3_ok(p), st, split_planes());
+    if (after) after();
+  };
   if (p.splits == 1 && !accumulate && Ckeep == C) {
     p.out = dw.data_ptr<float>();
-    wgrad_launch(p, wp.bm, wp.bn, x3_family() && x3_ok(p), st, split_planes());
+    launch(nullptr);
   } else {
     at::Tensor slab = at::empty({p.splits, Co, Kdim}, opts);
     p.out = slab.data_ptr<float>();
-    wgrad_launch(p, wp.bm, wp.bn, x3_family() && x3_ok(p), st, split_planes());
     const long long n = (long long)Co * Kdim;
     if (defer && !accumulate && Ckeep == C && (n % 4) == 0 &&
         (reinterpret_cast<uintptr_t>(dw.data_ptr<float>()) & 15) == 0) {
@@ -681,8 +726,13 @@ at::Tensor wgrad_impl(const at::Tensor& dy_, const at::Tensor& x_, std::vector<i
       defer->w_dst = dw.data_ptr<float>();
       defer->w_S = p.splits;
       defer->w_n = n;
+      launch(nullptr);
     } else {
-      slab_sum_strided_launch(slab.data_ptr<float>(), p.splits, n, C, Ckeep, dw.data_ptr<float>(), accumulate, st);
+      float* dst = dw.data_ptr<float>();
+      const int S = p.splits;
+      launch([slab, S, n, C, Ckeep, dst, accumulate, st] {
+        slab_sum_strided_launch(slab.data_ptr<float>(), S, n, C, Ckeep, dst, accumulate, st);
+      });
     }
   }
   return dw;
@@ -956,8 +1006,11 @@ std::vector<at::Tensor> conv_bn_act_bwd(const at::Tensor& gout_, const at::Tenso
   DeferredReduce dr;
   const bool has_prev = prev_y.has_value() && prev_y->defined() && prev_stats.has_value() && prev_stats->defined();
   DeferredReduce* defer = (bwd_fuse_enabled() && !padc && has_prev) ? &dr : nullptr;
+  // the weight gradient waits for the data gradient so both GEMMs can share one launch (bwd_pair)
+  PendingWgrad pend;
+  PendingWgrad* pp = (need_dx && !padc && stride == 1 && bwd_pair_enabled()) ? &pend : nullptr;
   dw = wgrad_impl(dy, x, {w.size(0), x.size(1), w.size(2), w.size(3)}, stride, pad, dw_out, false,
-                  padc ? w.size(1) : -1, dya, x_amax, defer);
+                  padc ? w.size(1) : -1, dya, x_amax, defer, pp);
   if (need_dx) {
     if (padc) {
       at::Tensor dx4 = conv2d_dgrad(dy, pad_channels4(nhwc(w)), {x.size(0), x.size(1), x.size(2), x.size(3)}, stride,
@@ -967,9 +1020,10 @@ std::vector<at::Tensor> conv_bn_act_bwd(const at::Tensor& gout_, const at::Tenso
     } else {
       // residual-branch gradient (dx_addend) is accumulated by the data-gradient GEMM's epilogue
       dx = dgrad_impl(dy, w, {x.size(0), x.size(1), x.size(2), x.size(3)}, stride, pad, dx_addend, dya, w_amax, w_t,
-                      defer);
+                      defer, pp);
     }
   }
+  pend.flush(st);  // no data-gradient GEMM took it: launch the weight gradient alone
   at::Tensor prev_part;
   if (dr.w_slab.defined() || dr.d_slab.defined()) {
     BwdReduceArgs a{};
