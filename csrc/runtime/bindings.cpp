@@ -18,6 +18,9 @@ PYBIND11_MODULE(_C, m) {
         "select the conv GEMM engine: x3 (3-term bf16 split), f16x2 (scaled 2-term fp16 split), f32 (exact fp32 "
         "MFMA) or bf16 (bf16 operands, non-parity)");
   m.def("get_conv_gemm", &get_conv_gemm);
+  m.def("set_gemm_override", &set_gemm_override, py::arg("kind"), py::arg("bm") = 0, py::arg("bn") = 0,
+        py::arg("splits") = 0, "force the tile / split-K plan of later GEMMs (tuning sweeps; zeros restore the planner)");
+  m.def("plan_info", &plan_info, py::arg("kind"), py::arg("M"), py::arg("N"), py::arg("K"));
   m.def("clear_hip_error", [] { return std::string(hipGetErrorName(hipGetLastError())); },
         "reset the thread's last HIP error (e.g. after an invalidated stream capture) and return its name");
   m.def("conv2d_fwd", &conv2d_fwd, py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("stride"), py::arg("pad"),

@@ -382,6 +382,20 @@ int choose_splits(long long tiles, int ktiles, int slots, int min_kt, double flo
   return best;
 }
 
+// Plan override for tuning sweeps (scripts/sweep_gemm.py): when set, every conv GEMM / weight-gradient
+// GEMM planned afterwards uses this tile and split count (0 = keep the planner's choice).
+struct PlanOverride {
+  int bm = 0, bn = 0, splits = 0;
+};
+PlanOverride& conv_override() {
+  static PlanOverride o;
+  return o;
+}
+PlanOverride& wgrad_override() {
+  static PlanOverride o;
+  return o;
+}
+
 GemmPlan plan_gemm(long long M, int Nout, int Kdim) {
   GemmPlan g;
   g.ktiles = (Kdim + 31) / 32;
@@ -404,6 +418,12 @@ GemmPlan plan_gemm(long long M, int Nout, int Kdim) {
   const int slots = conv_blocks_per_cu(g.bm, g.bn) * num_cus();
   g.splits = std::min(16, choose_splits(tiles, g.ktiles, slots, 4, 2.0 * M * Nout * Kdim, 4.0 * M * Nout,
                                         conv_mfma_rate()));
+  const PlanOverride& o = conv_override();
+  if (o.bm) g.bm = o.bm;
+  if (o.bn) g.bn = o.bn;
+  if (o.splits) g.splits = std::max(1, std::min(o.splits, g.ktiles));
+  if (g.bm == 256 && !x3_family()) g.bm = 128;
+  if (g.bm == 256) g.bn = 128;  // the only 256-row conv tile (dispatch_x3)
   return g;
 }
 
@@ -436,6 +456,11 @@ WgradPlan plan_wgrad(int Cout, int Kdim, long long M) {
   const int slots = wgrad_blocks_per_cu(w.bm, w.bn) * num_cus();
   w.splits = std::min(1024, choose_splits(tiles, mt, slots, 4, 2.0 * M * Cout * Kdim, 4.0 * Cout * Kdim,
                                           conv_mfma_rate()));
+  const PlanOverride& o = wgrad_override();
+  if (o.bm) w.bm = o.bm;
+  if (o.bn) w.bn = o.bn;
+  if (o.splits) w.splits = std::max(1, std::min(o.splits, mt));
+  if (w.bm == 256 && !(f16x2_mode() && w.bn == 128 && Cout % 4 == 0)) w.bm = 128;  // 256 rows: f16x2 256x128 only
   return w;
 }
 
@@ -469,6 +494,27 @@ at::Tensor pad_channels4(const at::Tensor& t, at::Tensor* amax = nullptr) {
 }
 
 }  // namespace
+
+void set_gemm_override(const std::string& kind, int64_t bm, int64_t bn, int64_t splits) {
+  TORCH_CHECK(kind == "conv" || kind == "wgrad", "set_gemm_override: kind must be 'conv' or 'wgrad'");
+  TORCH_CHECK(bm == 0 || bm == 64 || bm == 128 || bm == 256, "bm must be 0, 64, 128 or 256");
+  TORCH_CHECK(bn == 0 || bn == 64 || bn == 128, "bn must be 0, 64 or 128");
+  TORCH_CHECK(bm != 256 || bn == 128, "256-row tiles are 256x128");
+  PlanOverride& o = kind == "conv" ? conv_override() : wgrad_override();
+  o.bm = (int)bm;
+  o.bn = (int)bn;
+  o.splits = (int)splits;
+}
+
+std::vector<int64_t> plan_info(const std::string& kind, int64_t M, int64_t N, int64_t K) {
+  if (kind == "conv") {
+    const GemmPlan g = plan_gemm(M, (int)N, (int)K);
+    return {g.bm, g.bn, g.splits};
+  }
+  TORCH_CHECK(kind == "wgrad", "plan_info: kind must be 'conv' or 'wgrad'");
+  const WgradPlan w = plan_wgrad((int)N, (int)K, M);  // N = Cout, K = Kdim, M = reduction rows
+  return {w.bm, w.bn, w.splits};
+}
 
 void set_conv_gemm(const std::string& mode) {
   TORCH_CHECK(mode == "x3" || mode == "f32" || mode == "bf16" || mode == "f16x2",

@@ -7,6 +7,10 @@
 namespace cdp {
 
 void set_conv_gemm(const std::string& mode);
+// tuning sweeps: force the tile / split-K plan of later conv ('conv') or weight-gradient ('wgrad')
+// GEMMs (0 = planner's choice); plan_info returns the planner's {bm, bn, splits}
+void set_gemm_override(const std::string& kind, int64_t bm, int64_t bn, int64_t splits);
+std::vector<int64_t> plan_info(const std::string& kind, int64_t M, int64_t N, int64_t K);
 std::string get_conv_gemm();
 std::vector<at::Tensor> conv2d_fwd(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tensor>& bias,
                                    int64_t stride, int64_t pad, bool want_stats,
