@@ -22,7 +22,8 @@ ARCH = os.environ.get("CDP_OFFLOAD_ARCH", "gfx950")
 EXT_SUFFIX = sysconfig.get_config_var("EXT_SUFFIX") or ".so"
 OUTPUT = os.path.join(PKG_DIR, "_C" + EXT_SUFFIX)
 
-KERNELS = ["conv_igemm.hip", "conv_x3.hip", "wgrad.hip", "bn.hip", "misc.hip", "stem.hip", "bwd_fuse.hip", "bwd_pair.hip"]
+KERNELS = ["conv_igemm.hip", "conv_x3.hip", "wgrad.hip", "bn.hip", "misc.hip", "stem.hip", "bwd_fuse.hip", "bwd_pair.hip",
+           "bwd_pair_d128x128.hip", "bwd_pair_d128x64.hip", "bwd_pair_d64x128.hip", "bwd_pair_d64x64.hip"]
 RUNTIME = ["ops.cpp", "rccl_comm.cpp", "reducer.cpp", "torch_ops.cpp", "bindings.cpp"]
 
 
@@ -46,7 +47,8 @@ def _hipcc() -> str:
 # GEMM kernels whose operand split must stay scalar f32: packed-f32 VALU issued between MFMAs
 # costs ~22 extra cycles per MFMA gap on gfx950 (x3_common.h), and the SLP vectorizer would re-pack
 # adjacent scalar multiplies / FMAs into v_pk_mul_f32 / v_pk_fma_f32
-NO_SLP = {"conv_x3.hip", "wgrad.hip", "bwd_pair.hip"}
+NO_SLP = {"conv_x3.hip", "wgrad.hip", "bwd_pair.hip", "bwd_pair_d128x128.hip", "bwd_pair_d128x64.hip",
+          "bwd_pair_d64x128.hip", "bwd_pair_d64x64.hip"}
 
 
 def _ninja_escape(s: str) -> str:

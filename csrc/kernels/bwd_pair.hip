@@ -1,48 +1,27 @@
-// A conv block's two gradient GEMMs in ONE launch (gfx950): the data gradient dX = dY * W^T
-// (conv_x3_body, transposed gather) and the weight gradient dW = dY^T * Xcol (wgrad_x3_body) both
-// read dY and are independent, so the workgroups of one launch are split between them: blocks
-// [0, nd) run the data-gradient tiles, [nd, nd + nw) the weight-gradient tiles.
-//
-// Why one launch: at the reference's strong-scaling batches (32-64 images per GPU,
-// /root/reference/src/Part 2a/main.py:22) each of the two grids of a deep VGG layer is 64-150
-// workgroups on a 256-CU chip, and run back to back they leave most CUs idle twice; side by side in
-// one grid they fill the chip once and save a dependent dispatch. (Two streams were measured 2x
-// slower: under hipGraph every fork/join costs more than the overlap returns, docs/PERF.md.) Both
-// bodies are the f16x2 engine's 512-thread 256x128 tiles, so the pair keeps their occupancy (one
-// workgroup per CU); the LDS array is the larger of the two images.
-#include "conv_x3_body.h"
-#include "wgrad_x3_body.h"
+// Paired data- / weight-gradient launches (bwd_pair.h): the 512-thread 256x128 pair and the dispatch
+// over the 256-thread pairs, whose instantiations live in bwd_pair_d*.hip.
+#include "bwd_pair.h"
 
 namespace cdp {
-namespace {
-
-using namespace x3conv;
-using namespace x3wgrad;
-
-constexpr int kPairBM = 256, kPairBN = 128;
-constexpr int kPairSmem = conv_x3_smem_elems<kPairBM, kPairBN, 2>() > wgrad_x3_smem_elems<kPairBM, kPairBN, 2, true>()
-                              ? conv_x3_smem_elems<kPairBM, kPairBN, 2>()
-                              : wgrad_x3_smem_elems<kPairBM, kPairBN, 2, true>();
-static_assert(waves_m<kPairBM>() * 128 == wg_threads<kPairBM>(), "both bodies run 512-thread workgroups");
-
-__global__ __launch_bounds__(512, 1) void bwd_pair_kernel(ConvGemmParams pd, WgradParams pw, int nd, int nw) {
-  __shared__ __attribute__((aligned(16))) __bf16 smem[kPairSmem];
-  const int b = blockIdx.x;
-  if (b < nd) conv_x3_body<kPairBM, kPairBN, 0, true, 2>(pd, smem, b, nd);
-  else wgrad_x3_body<kPairBM, kPairBN, true, 2, true>(pw, smem, b - nd, nw);
-}
-
-}  // namespace
 
 bool bwd_pair_ok(const ConvGemmParams& pd, int bm, int bn, const WgradParams& pw, int wbm, int wbn, int np) {
-  return np == 2 && bm == kPairBM && bn == kPairBN && wbm == kPairBM && wbn == kPairBN && (pd.C % 32) == 0 &&
-         (pd.Kdim % 32) == 0 && (pw.C % 4) == 0 && (pw.Cout % 4) == 0;
+  if (np != 2 || (pd.C % 32) != 0 || (pd.Kdim % 32) != 0 || (pw.C % 4) != 0 || (pw.Cout % 4) != 0) return false;
+  if (bm == 256) return bn == 128 && wbm == 256 && wbn == 128;
+  return (bm == 64 || bm == 128) && (bn == 64 || bn == 128) && (wbm == 64 || wbm == 128) && (wbn == 64 || wbn == 128);
 }
 
-void bwd_pair_launch(const ConvGemmParams& pd, const WgradParams& pw, hipStream_t st) {
-  const int nd = ((pd.M + kPairBM - 1) / kPairBM) * ((pd.Nout + kPairBN - 1) / kPairBN) * pd.splits;
-  const int nw = ((pw.Cout + kPairBM - 1) / kPairBM) * ((pw.Kdim + kPairBN - 1) / kPairBN) * pw.splits;
-  hipLaunchKernelGGL(bwd_pair_kernel, dim3(nd + nw), dim3(512), 0, st, pd, pw, nd, nw);
+void bwd_pair_launch(const ConvGemmParams& pd, int bm, int bn, const WgradParams& pw, int wbm, int wbn,
+                     hipStream_t st) {
+  using namespace pair_detail;
+  bool ok = false;
+  if (bm == 256) {
+    launch_pair<256, 128, 256, 128>(pd, pw, st);
+    ok = true;
+  } else if (bm == 128 && bn == 128) ok = launch_pair_d<128, 128>(wbm, wbn, pd, pw, st);
+  else if (bm == 128 && bn == 64) ok = launch_pair_d<128, 64>(wbm, wbn, pd, pw, st);
+  else if (bm == 64 && bn == 128) ok = launch_pair_d<64, 128>(wbm, wbn, pd, pw, st);
+  else if (bm == 64 && bn == 64) ok = launch_pair_d<64, 64>(wbm, wbn, pd, pw, st);
+  (void)ok;  // callers check bwd_pair_ok first
 }
 
 }  // namespace cdp

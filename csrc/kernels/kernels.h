@@ -136,9 +136,10 @@ void stem_wgrad_launch(const float* y, const float* gout, const float* stats, co
                        float* slab, int nblk, int N, int H, int W, int Cin, hipStream_t st);
 
 // bwd_pair.hip: a block's data-gradient GEMM (MODE 0 transposed gather) and weight-gradient GEMM in
-// one launch, when both are f16x2 256x128 tiles (bwd_pair_ok)
+// one launch, when both are f16x2 tiles of one workgroup size (bwd_pair_ok)
 bool bwd_pair_ok(const ConvGemmParams& pd, int bm, int bn, const WgradParams& pw, int wbm, int wbn, int np);
-void bwd_pair_launch(const ConvGemmParams& pd, const WgradParams& pw, hipStream_t st);
+void bwd_pair_launch(const ConvGemmParams& pd, int bm, int bn, const WgradParams& pw, int wbm, int wbn,
+                     hipStream_t st);
 
 // bwd_fuse.hip: one launch that finishes a block's two gradient GEMMs' split-K slabs and starts the
 // previous block's BatchNorm backward (see the file header).

@@ -16,9 +16,12 @@
 #include <torch/extension.h>
 
 #include <algorithm>
+#include <array>
 #include <cstdlib>
 #include <functional>
+#include <mutex>
 #include <string>
+#include <unordered_map>
 
 #include "../kernels/kernels.h"
 
@@ -272,7 +275,7 @@ void conv_launch_or_pair(const ConvGemmParams& p, const GemmPlan& g, bool dgrad,
                          PendingWgrad* pending) {
   if (pending && pending->set && dgrad && f16x2_mode() && x3_ok(p, true) && p.amax_a && p.amax_b &&
       bwd_pair_ok(p, g.bm, g.bn, pending->p, pending->bm, pending->bn, split_planes())) {
-    bwd_pair_launch(p, pending->p, st);
+    bwd_pair_launch(p, g.bm, g.bn, pending->p, pending->bm, pending->bn, st);
     pending->run_after();
     return;
   }
@@ -396,6 +399,96 @@ PlanOverride& wgrad_override() {
   return o;
 }
 
+// ---- f16x2 planner: a cost model fitted to measurements
+// A tile / split-K sweep of the VGG-11 conv GEMMs (forward, data and weight gradient, each with its
+// split-K reduction; 32 / 64 / 128 / 256 images per GPU; 5,240 timed configurations) on MI355X
+// (scripts/sweep_gemm.py -> profiles/tuning/vgg11_gemm_sweep_r3.json) was fitted by
+// scripts/fit_plan_model.py to
+//   t = t0 + rounds * (a0 + kps * max(l0 + l1 (bm + bn), k bm bn / rho, k (bm + bn) / beta))
+//       + [splits > 1] (r0 + r1 * splits * P * Q * 4e-6)                                    (us)
+// for a P x Q output tiled bm x bn, reduction R split `splits` ways (kps K-tiles of 32 per block);
+// a CU holds nb = ceil(blocks / CUs) blocks, k = min(nb, residency) at a time, in rounds of the
+// residency. The three per-K-tile terms are a latency floor, the CU's MAC rate and its operand-load
+// rate, the last two shared by co-resident blocks. The planner takes the modelled argmin over every
+// tile and split count; its choices come within 3.4 % (conv) / 1.1 % (weight gradient) of the
+// measured best over the sweep, against 13 % for the previous heuristic (which preferred 256x128
+// tiles with up to 16 splits everywhere: 2x slower at 32 images per GPU on the deep layers).
+struct GemmCostModel {
+  double t0, a0, l0, l1, rho, beta, r0, r1;
+};
+constexpr GemmCostModel kConvCost{9.934, 3.163e-06, 1.698e-07, 0.002637, 3.041e4, 558.2, 0.05613, 0.3461};
+constexpr GemmCostModel kWgradCost{8.188, 1.54e-05, 0.1129, 0.003117, 2.541e4, 367.8, 2.707, 0.345};
+
+double model_time(const GemmCostModel& m, int residency, long long P, long long Q, long long R, int bm, int bn,
+                  int s) {
+  const long long tiles = ((P + bm - 1) / bm) * ((Q + bn - 1) / bn);
+  const long long blocks = tiles * s;
+  const long long kt = (R + 31) / 32, kps = (kt + s - 1) / s;
+  const long long nb = (blocks + num_cus() - 1) / num_cus();
+  const long long k = std::min<long long>(nb, residency);
+  const long long rounds = (nb + residency - 1) / residency;
+  const double per = m.a0 + (double)kps * std::max({m.l0 + m.l1 * (bm + bn), (double)(k * bm * bn) / m.rho,
+                                                     (double)(k * (bm + bn)) / m.beta});
+  return m.t0 + (double)rounds * per + (s > 1 ? m.r0 + m.r1 * (double)s * (double)P * (double)Q * 4e-6 : 0.0);
+}
+
+// CDP_PLANNER=legacy: the previous heuristic (A/B)
+bool model_planner_on() {
+  static const bool on = [] {
+    const char* e = std::getenv("CDP_PLANNER");
+    return !(e && std::string(e) == "legacy");
+  }();
+  return on && f16x2_mode();
+}
+
+struct PlanKey {
+  int kind, mode;
+  long long a, b, c;
+  bool operator==(const PlanKey& o) const {
+    return kind == o.kind && mode == o.mode && a == o.a && b == o.b && c == o.c;
+  }
+};
+struct PlanKeyHash {
+  size_t operator()(const PlanKey& k) const {
+    size_t h = std::hash<long long>()(k.a) * 1000003u ^ std::hash<long long>()(k.b) * 10007u ^
+               std::hash<long long>()(k.c) * 101u;
+    return h ^ (size_t)(k.kind * 31 + k.mode);
+  }
+};
+
+// argmin of the model over the f16x2 tiles and split counts (each block keeps >= 2 K-tiles);
+// returns {bm, bn, splits}
+std::array<int, 3> model_plan(bool wgrad, long long P, long long Q, long long R) {
+  static std::unordered_map<PlanKey, std::array<int, 3>, PlanKeyHash> cache;
+  static std::mutex mu;
+  const PlanKey key{wgrad ? 1 : 0, conv_gemm_mode(), P, Q, R};
+  {
+    std::lock_guard<std::mutex> g(mu);
+    auto it = cache.find(key);
+    if (it != cache.end()) return it->second;
+  }
+  static const int tiles[5][2] = {{256, 128}, {128, 128}, {128, 64}, {64, 128}, {64, 64}};
+  const long long kt = (R + 31) / 32;
+  const int smax = (int)std::max<long long>(1, std::min<long long>(wgrad ? 1024 : 64, kt / 2));
+  std::array<int, 3> best{128, 64, 1};
+  double best_t = 1e30;
+  for (const auto& t : tiles) {
+    const int bm = t[0], bn = t[1];
+    if (bm == 256 && wgrad && (Q % 128) != 0) continue;  // 256-row weight-gradient tiles: 128-wide k only
+    const int res = wgrad ? wgrad_blocks_per_cu(bm, bn) : conv_blocks_per_cu(bm, bn);
+    for (int s = 1; s <= smax; ++s) {
+      const double tm = model_time(wgrad ? kWgradCost : kConvCost, res, P, Q, R, bm, bn, s);
+      if (tm < best_t) {
+        best_t = tm;
+        best = {bm, bn, s};
+      }
+    }
+  }
+  std::lock_guard<std::mutex> g(mu);
+  cache[key] = best;
+  return best;
+}
+
 GemmPlan plan_gemm(long long M, int Nout, int Kdim) {
   GemmPlan g;
   g.ktiles = (Kdim + 31) / 32;
@@ -418,6 +511,12 @@ GemmPlan plan_gemm(long long M, int Nout, int Kdim) {
   const int slots = conv_blocks_per_cu(g.bm, g.bn) * num_cus();
   g.splits = std::min(16, choose_splits(tiles, g.ktiles, slots, 4, 2.0 * M * Nout * Kdim, 4.0 * M * Nout,
                                         conv_mfma_rate()));
+  if (model_planner_on() && force_bm == 0) {
+    const auto m = model_plan(false, M, Nout, Kdim);
+    g.bm = m[0];
+    g.bn = m[1];
+    g.splits = m[2];
+  }
   const PlanOverride& o = conv_override();
   if (o.bm) g.bm = o.bm;
   if (o.bn) g.bn = o.bn;
@@ -456,6 +555,12 @@ WgradPlan plan_wgrad(int Cout, int Kdim, long long M) {
   const int slots = wgrad_blocks_per_cu(w.bm, w.bn) * num_cus();
   w.splits = std::min(1024, choose_splits(tiles, mt, slots, 4, 2.0 * M * Cout * Kdim, 4.0 * Cout * Kdim,
                                           conv_mfma_rate()));
+  if (model_planner_on() && (Cout % 4) == 0) {
+    const auto m = model_plan(true, Cout, Kdim, M);
+    w.bm = m[0];
+    w.bn = m[1];
+    w.splits = m[2];
+  }
   const PlanOverride& o = wgrad_override();
   if (o.bm) w.bm = o.bm;
   if (o.bn) w.bn = o.bn;
@@ -745,8 +850,7 @@ at::Tensor wgrad_impl(const at::Tensor& dy_, const at::Tensor& x_, std::vector<i
   const at::Tensor dya = amax_parts(dy, dy_amax, st), xa = amax_parts(x, x_amax, st);
   set_amax(p, dya, xa);
   // the GEMM launch, held back in `pending` when it can run beside the block's data gradient
-  const bool hold = pending && f16x2_mode() && x3_ok(p) && wp.bm == 256 && wp.bn == 128 && (C % 4) == 0 &&
-                    (Co % 4) == 0 && p.amax_dy && p.amax_x;
+  const bool hold = pending && f16x2_mode() && x3_ok(p) && (C % 4) == 0 && (Co % 4) == 0 && p.amax_dy && p.amax_x;
   auto launch = [&](std::function<void()> after) {
     if (hold) {
       pending->set = true;

@@ -1,8 +1,5 @@
 set -o pipefail
 mkdir -p gpurun_out
-timeout -k 10 300 python bench.py --steps 20 --warmup 5 > gpurun_out/bdef.log 2>&1 || { tail -30 gpurun_out/bdef.log; exit 1; }
-tail -1 gpurun_out/bdef.log
-bash scripts/prof_bench.sh b32 10 --local-batch 32 || exit 1
-for lb in 32 256; do bash scripts/ab_env.sh CDP_BWD_PAIR "0 1" 2 --local-batch $lb || exit 1; done
-timeout -k 10 600 python scripts/sweep_gemm.py --batches 32,256 > gpurun_out/sweep.log 2>&1 || { tail -20 gpurun_out/sweep.log; exit 1; }
-tail -3 gpurun_out/sweep.log
+timeout -k 10 600 python -u -m pytest tests/test_model_gpu.py tests/test_kernels_gpu.py -x -q --timeout 200 --timeout-method thread > gpurun_out/gputest_a.log 2>&1 || { tail -60 gpurun_out/gputest_a.log; exit 1; }
+tail -2 gpurun_out/gputest_a.log
+for lb in 32 64 128 256; do bash scripts/ab_env.sh CDP_PLANNER "legacy model" 2 --local-batch $lb || exit 1; done

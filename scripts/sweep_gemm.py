@@ -26,7 +26,7 @@ VGG = [(3, 64, 32), (64, 128, 16), (128, 256, 8), (256, 256, 8), (256, 512, 4), 
        (512, 512, 2)]
 CONV_TILES = [(256, 128), (128, 128), (128, 64), (64, 128), (64, 64)]
 WGRAD_TILES = [(256, 128), (128, 128), (128, 64), (64, 128), (64, 64)]
-SPLITS = [1, 2, 3, 4, 6, 8, 12, 16, 24, 32, 48, 64]
+SPLITS = [1, 2, 3, 4, 5, 6, 8, 10, 12, 16, 20, 24, 32, 48, 64]
 
 
 def cl(t):
