@@ -432,6 +432,20 @@ double model_time(const GemmCostModel& m, int residency, long long P, long long 
   return m.t0 + (double)rounds * per + (s > 1 ? m.r0 + m.r1 * (double)s * (double)P * (double)Q * 4e-6 : 0.0);
 }
 
+// The model decides only where it predicts a clear gain over the previous heuristic's plan (which was
+// tuned in the full training step at 256 images per GPU, where its 256x128 tiles also pair the two
+// gradient GEMMs of a block in one launch): its plan must model at most kModelGain x the heuristic's
+// time. Measured in the bench step, VGG-11 (ms/step, heuristic -> model everywhere): 32 images
+// 0.638 -> 0.551, 64: 0.757 -> 0.698, 128: 0.970 -> 0.985, 256: 1.409 -> 1.454 -- the model's fit
+// (log-space, dominated by the many small configurations) overrates 128x128 tiles at large M.
+double model_gain() {
+  static const double g = [] {
+    const char* e = std::getenv("CDP_PLANNER_GAIN");
+    return e ? std::atof(e) : 0.87;
+  }();
+  return g;
+}
+
 // CDP_PLANNER=legacy: the previous heuristic (A/B)
 bool model_planner_on() {
   static const bool on = [] {
@@ -513,9 +527,13 @@ GemmPlan plan_gemm(long long M, int Nout, int Kdim) {
                                         conv_mfma_rate()));
   if (model_planner_on() && force_bm == 0) {
     const auto m = model_plan(false, M, Nout, Kdim);
-    g.bm = m[0];
-    g.bn = m[1];
-    g.splits = m[2];
+    const double t_model = model_time(kConvCost, conv_blocks_per_cu(m[0], m[1]), M, Nout, Kdim, m[0], m[1], m[2]);
+    const double t_heur = model_time(kConvCost, conv_blocks_per_cu(g.bm, g.bn), M, Nout, Kdim, g.bm, g.bn, g.splits);
+    if (t_model <= model_gain() * t_heur) {
+      g.bm = m[0];
+      g.bn = m[1];
+      g.splits = m[2];
+    }
   }
   const PlanOverride& o = conv_override();
   if (o.bm) g.bm = o.bm;
@@ -557,9 +575,13 @@ WgradPlan plan_wgrad(int Cout, int Kdim, long long M) {
                                           conv_mfma_rate()));
   if (model_planner_on() && (Cout % 4) == 0) {
     const auto m = model_plan(true, Cout, Kdim, M);
-    w.bm = m[0];
-    w.bn = m[1];
-    w.splits = m[2];
+    const double t_model = model_time(kWgradCost, wgrad_blocks_per_cu(m[0], m[1]), Cout, Kdim, M, m[0], m[1], m[2]);
+    const double t_heur = model_time(kWgradCost, wgrad_blocks_per_cu(w.bm, w.bn), Cout, Kdim, M, w.bm, w.bn, w.splits);
+    if (t_model <= model_gain() * t_heur) {
+      w.bm = m[0];
+      w.bn = m[1];
+      w.splits = m[2];
+    }
   }
   const PlanOverride& o = wgrad_override();
   if (o.bm) w.bm = o.bm;

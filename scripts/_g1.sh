@@ -1,5 +1,3 @@
 set -o pipefail
 mkdir -p gpurun_out
-timeout -k 10 600 python -u -m pytest tests/test_model_gpu.py tests/test_kernels_gpu.py -x -q --timeout 200 --timeout-method thread > gpurun_out/gputest_a.log 2>&1 || { tail -60 gpurun_out/gputest_a.log; exit 1; }
-tail -2 gpurun_out/gputest_a.log
-for lb in 32 64 128 256; do bash scripts/ab_env.sh CDP_PLANNER "legacy model" 2 --local-batch $lb || exit 1; done
+for lb in 32 64 128 256; do bash scripts/ab_env.sh CDP_PLANNER_GAIN "0.8 0.87 0.95" 2 --local-batch $lb || exit 1; done
