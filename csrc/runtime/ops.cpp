@@ -434,16 +434,23 @@ double model_time(const GemmCostModel& m, int residency, long long P, long long 
 
 // The model decides only where it predicts a clear gain over the previous heuristic's plan (which was
 // tuned in the full training step at 256 images per GPU, where its 256x128 tiles also pair the two
-// gradient GEMMs of a block in one launch): its plan must model at most kModelGain x the heuristic's
-// time. Measured in the bench step, VGG-11 (ms/step, heuristic -> model everywhere): 32 images
-// 0.638 -> 0.551, 64: 0.757 -> 0.698, 128: 0.970 -> 0.985, 256: 1.409 -> 1.454 -- the model's fit
-// (log-space, dominated by the many small configurations) overrates 128x128 tiles at large M.
-double model_gain() {
-  static const double g = [] {
-    const char* e = std::getenv("CDP_PLANNER_GAIN");
-    return e ? std::atof(e) : 0.87;
+// gradient GEMMs of a block in one launch): its plan must model at most gain x the heuristic's time,
+// gain = 0.95 for GEMMs under 3.2 GFLOP (the model is accurate there: few blocks, latency-bound) and
+// 0.85 above (it overrates 128x128 tiles at large M; its log-space fit is dominated by the many
+// small configurations). Measured in the bench step, VGG-11 ms/step at 32 / 64 / 128 / 256 images
+// per GPU: heuristic 0.638 / 0.757 / 0.970 / 1.409 (one box); model everywhere 0.551 / 0.698 /
+// 0.985 / 1.454 (same box); a single threshold of 0.95 / 0.87 / 0.80 (another box):
+// 0.552 / 0.731 / 0.981 / 1.377, 0.588 / 0.733 / 0.967 / 1.366, 0.616 / 0.743 / 0.987 / 1.363.
+double model_gain(double flops) {
+  static const double g_small = [] {
+    const char* e = std::getenv("CDP_PLANNER_GAIN_SMALL");
+    return e ? std::atof(e) : 0.95;
   }();
-  return g;
+  static const double g_large = [] {
+    const char* e = std::getenv("CDP_PLANNER_GAIN");
+    return e ? std::atof(e) : 0.85;
+  }();
+  return flops < 3.2e9 ? g_small : g_large;
 }
 
 // CDP_PLANNER=legacy: the previous heuristic (A/B)
@@ -529,7 +536,7 @@ GemmPlan plan_gemm(long long M, int Nout, int Kdim) {
     const auto m = model_plan(false, M, Nout, Kdim);
     const double t_model = model_time(kConvCost, conv_blocks_per_cu(m[0], m[1]), M, Nout, Kdim, m[0], m[1], m[2]);
     const double t_heur = model_time(kConvCost, conv_blocks_per_cu(g.bm, g.bn), M, Nout, Kdim, g.bm, g.bn, g.splits);
-    if (t_model <= model_gain() * t_heur) {
+    if (t_model <= model_gain(2.0 * M * Nout * Kdim) * t_heur) {
       g.bm = m[0];
       g.bn = m[1];
       g.splits = m[2];
@@ -577,7 +584,7 @@ WgradPlan plan_wgrad(int Cout, int Kdim, long long M) {
     const auto m = model_plan(true, Cout, Kdim, M);
     const double t_model = model_time(kWgradCost, wgrad_blocks_per_cu(m[0], m[1]), Cout, Kdim, M, m[0], m[1], m[2]);
     const double t_heur = model_time(kWgradCost, wgrad_blocks_per_cu(w.bm, w.bn), Cout, Kdim, M, w.bm, w.bn, w.splits);
-    if (t_model <= model_gain() * t_heur) {
+    if (t_model <= model_gain(2.0 * M * Cout * Kdim) * t_heur) {
       w.bm = m[0];
       w.bn = m[1];
       w.splits = m[2];
