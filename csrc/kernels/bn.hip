@@ -134,7 +134,8 @@ __device__ __forceinline__ float4 affine_act(float4 y, float4 sc, float4 sh, boo
 // channels' partials itself (fp64, the formulas of bn_finalize_kernel); the chunk-0 blocks publish
 // stats and the running statistics; then the block applies [pool2](relu(y*scale + shift)) to its
 // rows. Saves a dependent launch per layer; the redundant merge reads <= 64 KB per block from L2.
-constexpr int FIN_MAXP = 128;
+constexpr int FIN_MAXP = 128;      // backward fused finalize (bn_bwd_fin_apply) and 64-channel forward blocks
+constexpr int FIN_MAXP16 = 512;    // forward, 16-channel blocks (16 merge threads per channel)
 // A fused-finalize block's row r (pooled window or pixel) of y: the 2x2 window's four pixels (pool)
 // or the pixel in v[0], channels n0..n0+3.
 constexpr int kFinRPT = 4;  // rows per thread loaded before the statistics merge
@@ -199,7 +200,7 @@ __global__ __launch_bounds__(256) void bn_fin_act_kernel(const float* __restrict
   fin_prefetch(y, pv, r0 + rl, r1, pool, H, W, Ho, Wo, C, n0, RL);
   // phase 1: thread (ch, q) merges partials b = q + TQ k -- one batch of buffer loads
   // (only the batches of 8 loads that hold partials are issued: kp = ceil(nparts / TQ) rounded up to 8)
-  constexpr int KP = FIN_MAXP / TQ;
+  constexpr int KP = (CG == 16 ? FIN_MAXP16 : FIN_MAXP) / TQ;
   const int kp = (((nparts + TQ - 1) / TQ) + 7) & ~7;
   float pm[KP], pq[KP];
   const __amdgpu_buffer_rsrc_t pr = make_rsrc(part, (unsigned)nparts * (unsigned)C * 8u);
@@ -864,7 +865,8 @@ void bn_eval_stats_launch(int C, const float* gamma, const float* beta, const fl
                      stats);
 }
 
-bool bn_fin_act_ok(int nparts, int C, bool residual) { return !residual && nparts <= FIN_MAXP && (C % 64) == 0; }
+// (up to 512 partials: 16-channel blocks above CDP_FIN_CG16 partials, 32 M2-merge loads per thread)
+bool bn_fin_act_ok(int nparts, int C, bool residual) { return !residual && nparts <= FIN_MAXP16 && (C % 64) == 0; }
 
 // channels per fused-finalize block: 16 above CDP_FIN_CG16 partials (default 32), else 64
 static int fin_cg(int nparts) {

@@ -227,9 +227,11 @@ struct DeferredReduce {
   int w_S = 0;
   long long w_n = 0;
   at::Tensor d_slab;
+  const float* d_src = nullptr;  // d_slab's data, or (d_S == 1) the finished dX read back in place
   float* d_y = nullptr;
   const float* d_addend = nullptr;
   int d_S = 0, d_M = 0, d_Nout = 0;
+  bool d_on = false;
 };
 
 // A weight-gradient GEMM held back so the data-gradient GEMM of the same block can run beside it in
@@ -289,12 +291,25 @@ int conv_gemm_splitk(ConvGemmParams p, const GemmPlan& g, bool dgrad, hipStream_
   if (g.splits == 1) {
     if (alloc_part) p.part = alloc_part(g.bm);
     conv_launch_or_pair(p, g, dgrad, st, pending);
+    if (defer && !alloc_part && !p.part && !p.bias && !p.rr.on && !p.addend && (p.Nout % 4) == 0) {
+      // no split-K slab, but the block's bwd_reduce launch still runs the previous block's BN
+      // statistics pass over dX (one "slab": dX itself, rewritten unchanged; the addend is already in)
+      defer->d_on = true;
+      defer->d_src = p.y;
+      defer->d_y = p.y;
+      defer->d_addend = nullptr;
+      defer->d_S = 1;
+      defer->d_M = p.M;
+      defer->d_Nout = p.Nout;
+    }
     return g.bm;
   }
   at::Tensor slab = at::empty({g.splits, (long long)p.M, p.Nout}, opts);
   keep.push_back(slab);
   if (defer && !alloc_part && !p.part && !p.bias && !p.rr.on && (p.Nout % 4) == 0) {
     defer->d_slab = slab;
+    defer->d_src = slab.data_ptr<float>();
+    defer->d_on = true;
     defer->d_y = p.y;
     defer->d_addend = p.addend;
     defer->d_S = g.splits;
@@ -1204,10 +1219,10 @@ std::vector<at::Tensor> conv_bn_act_bwd(const at::Tensor& gout_, const at::Tenso
   }
   pend.flush(st);  // no data-gradient GEMM took it: launch the weight gradient alone
   at::Tensor prev_part;
-  if (dr.w_slab.defined() || dr.d_slab.defined()) {
+  if (dr.w_slab.defined() || dr.d_on) {
     BwdReduceArgs a{};
-    if (dr.d_slab.defined()) {
-      a.d_slab = dr.d_slab.data_ptr<float>();
+    if (dr.d_on) {
+      a.d_slab = dr.d_src;
       a.d_y = dr.d_y;
       a.d_addend = dr.d_addend;
       a.d_S = dr.d_S;

@@ -1,7 +1,7 @@
 set -o pipefail
 mkdir -p gpurun_out
+timeout -k 10 300 python -u -m pytest tests/test_model_gpu.py -x -q --timeout 200 --timeout-method thread > gpurun_out/gputest_a.log 2>&1 || { tail -60 gpurun_out/gputest_a.log; exit 1; }
+tail -2 gpurun_out/gputest_a.log
 for lb in 32 64 128 256; do bash scripts/ab_env.sh CDP_PLANNER "legacy model" 2 --local-batch $lb || exit 1; done
-timeout -k 10 300 python bench.py --steps 20 --warmup 5 > gpurun_out/bdef.log 2>&1 || { tail -30 gpurun_out/bdef.log; exit 1; }
-tail -1 gpurun_out/bdef.log
-timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/gputest.log 2>&1 || { tail -60 gpurun_out/gputest.log; exit 1; }
-tail -3 gpurun_out/gputest.log
+CDP_PLANNER=legacy bash scripts/prof_bench.sh p128L 6 --local-batch 128 || exit 1
+CDP_PLANNER=model bash scripts/prof_bench.sh p128M 6 --local-batch 128 || exit 1
