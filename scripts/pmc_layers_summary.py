@@ -1,0 +1,90 @@
+"""Label the last training step's GEMM dispatches of a VGG-11 bench run by layer and report, per
+dispatch: time, achieved TFLOP/s (fp32-equivalent), MFMA busy share of all SIMD cycles, issue-stall
+and wait shares of wave cycles, LDS bank conflicts (scripts/pmc_layers.sh)."""
+import collections
+import csv
+import glob
+import os
+import sys
+
+VGG = [(3, 64, 32), (64, 128, 16), (128, 256, 8), (256, 256, 8), (256, 512, 4), (512, 512, 4), (512, 512, 2),
+       (512, 512, 2)]
+SIMDS = 1024
+
+
+def kind(name):
+    if "stem_fwd" in name:
+        return "fwd0"
+    if "stem_wgrad" in name:
+        return "wgrad0"
+    if "bwd_pair" in name:
+        return "pair"
+    if "wgrad" in name and "slab" not in name:
+        return "wgrad"
+    if "conv_x3_kernel" in name or "conv_igemm" in name:
+        inner = name.split("<", 1)[1] if "<" in name else ""
+        parts = [p.strip() for p in inner.split(">")[0].split(",")]
+        return "dgrad" if len(parts) > 3 and parts[3] == "true" else "fwd"
+    return None
+
+
+def rows_of(pattern):
+    f = glob.glob(pattern)
+    return list(csv.DictReader(open(f[0]))) if f else []
+
+
+def main(d, B):
+    B = int(B)
+    kt = rows_of(os.path.join(d, "kt", "*kernel_trace.csv"))
+    kt.sort(key=lambda r: int(r["Start_Timestamp"]))
+    gemm = [(r["Kernel_Name"], (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3) for r in kt
+            if kind(r["Kernel_Name"])]
+    # one step = stem fwd + 7 fwd + (7 pairs or 7 dgrad + 7 wgrad) + stem wgrad; find the last stem_fwd
+    last = max(i for i, (n, _) in enumerate(gemm) if kind(n) == "fwd0")
+    step = gemm[last:]
+    pmc = rows_of(os.path.join(d, "pmc", "*counter_collection.csv"))
+    byd = collections.defaultdict(dict)
+    names = {}
+    for r in pmc:
+        did = int(r.get("Dispatch_Id") or r.get("Correlation_Id"))
+        byd[did][r["Counter_Name"]] = byd[did].get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
+        names[did] = r["Kernel_Name"]
+    pd = [(did, names[did]) for did in sorted(byd) if kind(names[did])]
+    plast = max(i for i, (_, n) in enumerate(pd) if kind(n) == "fwd0")
+    pstep = pd[plast:]
+    print(f"# VGG-11 B={B}: GEMM dispatches of one training step (eager, rocprofv3)\n")
+    print("| # | layer | GEMM | us | TF/s | MFMA busy % | wait-inst % | wait % | LDS conflict / LDS cycles |")
+    print("|---|---|---|---|---|---|---|---|---|")
+    cnt = collections.Counter()
+    tot_us = tot_fl = 0.0
+    for i, (n, us) in enumerate(step):
+        k = kind(n)
+        cnt[k] += 1
+        if k == "fwd0":
+            layer, fl = 0, 2.0 * B * 32 * 32 * 64 * 27
+        elif k == "wgrad0":
+            layer, fl = 0, 2.0 * B * 32 * 32 * 64 * 27
+        elif k == "fwd":
+            layer = cnt[k]
+            ci, co, hw = VGG[layer]
+            fl = 2.0 * B * hw * hw * co * ci * 9
+        else:
+            layer = 8 - cnt[k]
+            ci, co, hw = VGG[layer]
+            fl = 2.0 * B * hw * hw * co * ci * 9 * (2 if k == "pair" else 1)
+        c = byd[pstep[i][0]] if i < len(pstep) and kind(pstep[i][1]) == k else {}
+        wall = c.get("GRBM_GUI_ACTIVE", 0) / 8.0
+        mfma = 100.0 * c.get("SQ_VALU_MFMA_BUSY_CYCLES", 0) / (SIMDS * wall) if wall else float("nan")
+        wc = c.get("SQ_WAVE_CYCLES", 0)
+        wi = 100.0 * c.get("SQ_WAIT_INST_ANY", 0) / wc if wc else float("nan")
+        wa = 100.0 * c.get("SQ_WAIT_ANY", 0) / wc if wc else float("nan")
+        lds = c.get("SQ_LDS_IDX_ACTIVE", 0)
+        bc = c.get("SQ_LDS_BANK_CONFLICT", 0) / lds if lds else float("nan")
+        tot_us += us
+        tot_fl += fl
+        print(f"| {i} | {layer} | {k} | {us:.1f} | {fl / us / 1e6:.0f} | {mfma:.1f} | {wi:.1f} | {wa:.1f} | {bc:.3f} |")
+    print(f"\nGEMM total {tot_us:.1f} us, {tot_fl / 1e9:.1f} GFLOP, {tot_fl / tot_us / 1e6:.0f} TF/s fp32-equivalent")
+
+
+if __name__ == "__main__":
+    main(sys.argv[1], sys.argv[2] if len(sys.argv) > 2 else 256)
