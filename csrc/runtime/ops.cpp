@@ -988,15 +988,14 @@ std::vector<at::Tensor> stem_bn_act_fwd(const at::Tensor& x_, const at::Tensor& 
 // out = [maxpool2](act(BN(conv3x3(x) + b) [+ residual])), training or eval BatchNorm.
 // Returns {out, y (conv output), stats [4, C] = (mean, invstd, scale, shift)}.
 // One-launch BN finalize + apply for the layers with few statistics partials: forward
-// bn_fin_act (default; CDP_BN_FIN_ACT=0 selects finalize-then-apply) and backward bn_bwd_fin_apply
-// (opt-in, CDP_BN_BWD_FIN=1). Both load their first rows of y (and gout) before merging the
-// partials, so the two round trips overlap. Same-box A/B on MI355X, VGG-11 B=256 hipGraph step:
-// forward 1.399 vs 1.407 ms (fused 0.6 % faster, two boxes agree); backward 1.409 vs 1.404 ms
-// (fused 0.35 % slower, within noise, so it stays opt-in). Read per call so a test can compare
-// both paths in one process.
+// bn_fin_act and backward bn_bwd_fin_apply (both default; CDP_BN_FIN_ACT=0 / CDP_BN_BWD_FIN=0
+// select finalize-then-apply). Both load their first rows of y (and gout) before merging the
+// partials, so the two round trips overlap. Same-box A/B on MI355X, VGG-11 hipGraph step: forward
+// 1.399 vs 1.407 ms at 256 images per GPU (fused 0.6 % faster, two boxes agree); backward 1.409 vs
+// 1.404 ms at 256 images (within noise) and 0.632 vs 0.641 ms at 32 images (1.3 % faster, where
+// every deep layer qualifies). Read per call so a test can compare both paths in one process.
 static bool bn_fin_enabled(bool bwd = false) {
   const char* e = std::getenv(bwd ? "CDP_BN_BWD_FIN" : "CDP_BN_FIN_ACT");
-  if (bwd) return e && e[0] == '1';
   return !(e && e[0] == '0');
 }
 

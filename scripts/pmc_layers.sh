@@ -15,5 +15,12 @@ timeout -s KILL 200 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_WAVE_CYCLES SQ_W
   SQ_ACTIVE_INST_ANY SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_BUSY_CYCLES GRBM_GUI_ACTIVE GRBM_COUNT \
   --output-format csv -d gpurun_out/$TAG/pmc -o run -- \
   python bench.py --no-graph --no-extra --steps 2 --warmup 1 --local-batch $LB > gpurun_out/$TAG/pmc.log 2>&1 || exit $?
+# optional second pass: instruction mix (per wave) of the same dispatches
+if [ -n "$PMC_MIX" ]; then
+  timeout -s KILL 200 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_INSTS_VMEM SQ_INSTS_SALU SQ_WAVES \
+    SQ_ACTIVE_INST_VALU SQ_WAIT_INST_LDS GRBM_GUI_ACTIVE \
+    --output-format csv -d gpurun_out/$TAG/mix -o run -- \
+    python bench.py --no-graph --no-extra --steps 2 --warmup 1 --local-batch $LB > gpurun_out/$TAG/mix.log 2>&1 || exit $?
+fi
 python scripts/pmc_layers_summary.py gpurun_out/$TAG $LB > gpurun_out/$TAG/layers.md
 cat gpurun_out/$TAG/layers.md

@@ -84,6 +84,26 @@ def main(d, B):
         tot_fl += fl
         print(f"| {i} | {layer} | {k} | {us:.1f} | {fl / us / 1e6:.0f} | {mfma:.1f} | {wi:.1f} | {wa:.1f} | {bc:.3f} |")
     print(f"\nGEMM total {tot_us:.1f} us, {tot_fl / 1e9:.1f} GFLOP, {tot_fl / tot_us / 1e6:.0f} TF/s fp32-equivalent")
+    mix = rows_of(os.path.join(d, "mix", "*counter_collection.csv"))
+    if mix:
+        byd2 = collections.defaultdict(dict)
+        nm2 = {}
+        for r in mix:
+            did = int(r.get("Dispatch_Id") or r.get("Correlation_Id"))
+            byd2[did][r["Counter_Name"]] = byd2[did].get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
+            nm2[did] = r["Kernel_Name"]
+        md = [(did, nm2[did]) for did in sorted(byd2) if kind(nm2[did])]
+        ml = max(i for i, (_, n) in enumerate(md) if kind(n) == "fwd0")
+        print("\n| # | GEMM | waves | VALU/wave | MFMA/wave | LDS/wave | VMEM/wave | SALU/wave | VALU-active % of wall x SIMDs | LDS issue-stall / wave |")
+        print("|---|---|---|---|---|---|---|---|---|---|")
+        for i, (did, n) in enumerate(md[ml:]):
+            c = byd2[did]
+            w = c.get("SQ_WAVES", 0) or 1
+            wall = c.get("GRBM_GUI_ACTIVE", 0) / 8.0
+            va = 100.0 * 4 * c.get("SQ_ACTIVE_INST_VALU", 0) / (SIMDS * wall) if wall else float("nan")
+            print(f"| {i} | {kind(n)} | {w:.0f} | {c.get('SQ_INSTS_VALU', 0) / w:.0f} | {c.get('SQ_INSTS_MFMA', 0) / w:.0f} | "
+                  f"{c.get('SQ_INSTS_LDS', 0) / w:.0f} | {c.get('SQ_INSTS_VMEM', 0) / w:.0f} | {c.get('SQ_INSTS_SALU', 0) / w:.0f} | "
+                  f"{va:.1f} | {c.get('SQ_WAIT_INST_LDS', 0) / w:.0f} |")
 
 
 if __name__ == "__main__":
