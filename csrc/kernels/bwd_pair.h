@@ -23,7 +23,7 @@ using namespace x3wgrad;
 
 template <int DBM, int DBN, int WBM, int WBN>
 struct PairCfg {
-  static constexpr int kThreads = waves_m<DBM, DBN>() * 128;
+  static constexpr int kThreads = waves_m<DBM>() * 128;
   static_assert(kThreads == wg_threads<WBM>(), "both bodies must run the same workgroup size");
   static constexpr int kSmem = conv_x3_smem_elems<DBM, DBN, 2>() > wgrad_x3_smem_elems<WBM, WBN, 2, true>()
                                    ? conv_x3_smem_elems<DBM, DBN, 2>()
@@ -31,7 +31,7 @@ struct PairCfg {
 };
 
 template <int DBM, int DBN, int WBM, int WBN>
-__global__ __launch_bounds__((waves_m<DBM, DBN>() * 128), (DBM >= 256 ? 1 : 2)) void bwd_pair_kernel(
+__global__ __launch_bounds__(waves_m<DBM>() * 128, DBM >= 256 ? 1 : 2) void bwd_pair_kernel(
     ConvGemmParams pd, WgradParams pw, int nd, int nw) {
   __shared__ __attribute__((aligned(16))) __bf16 smem[PairCfg<DBM, DBN, WBM, WBN>::kSmem];
   const int b = blockIdx.x;

@@ -16,22 +16,20 @@
 
 namespace cdp {
 
-// Wave grid: WM x 2 waves, each owning (BM/WM) x (BN/2): WM = 4 for the 256x128 tile (8 waves, two
-// per SIMD, 64x64 each), else 2 (the 256x256 tile: 4 waves, one per SIMD, 128x128 each -- half the
-// operand-split VALU per MFMA of the 256x128 tile, at up to 512 registers per lane).
-template <int BM, int BN = 128>
-constexpr int waves_m() { return (BM >= 256 && BN <= 128) ? 4 : 2; }
+// Wave grid: WM x 2 waves (WM = 4 for BM = 256, else 2), each owning (BM/WM) x (BN/2).
+template <int BM>
+constexpr int waves_m() { return BM >= 256 ? 4 : 2; }
 
 template <int BM, int BN>
 __device__ __forceinline__ void conv_tile_stats(const ConvGemmParams& p,
-                                                const f32x16 (&acc)[BM / waves_m<BM, BN>() / 32][BN / 64], float* red,
+                                                const f32x16 (&acc)[BM / waves_m<BM>() / 32][BN / 64], float* red,
                                                 int m0, int n0, int tm_idx);
 
 template <int BM, int BN>
 __device__ __forceinline__ void conv_epilogue(const ConvGemmParams& p,
-                                              f32x16 (&acc)[BM / waves_m<BM, BN>() / 32][BN / 64], float* red, int m0,
+                                              f32x16 (&acc)[BM / waves_m<BM>() / 32][BN / 64], float* red, int m0,
                                               int n0, int tm_idx, int split) {
-  constexpr int WM = waves_m<BM, BN>();
+  constexpr int WM = waves_m<BM>();
   constexpr int TM = BM / WM / 32, TN = BN / 64;
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -75,9 +73,6 @@ __device__ __forceinline__ void conv_epilogue(const ConvGemmParams& p,
           const float av = p.addend[ok ? remap_row(p.rr, m) * p.Nout + n : 0];
           acc[a][b][r] += ok ? av : 0.f;
         }
-        // one 32x32 accumulator tile's 16 loads in flight at a time: the 256x256 tile holds 256
-        // accumulators per lane, and loading all their addends first would need as many registers
-        if constexpr (TM * TN > 4) __builtin_amdgcn_sched_barrier(0);
       }
   }
   float bias_v[TN];
@@ -115,9 +110,9 @@ __device__ __forceinline__ void conv_epilogue(const ConvGemmParams& p,
 // BN partials (mean, M2) of the tile's columns over its valid rows -> p.part[tm_idx]
 template <int BM, int BN>
 __device__ __forceinline__ void conv_tile_stats(const ConvGemmParams& p,
-                                                const f32x16 (&acc)[BM / waves_m<BM, BN>() / 32][BN / 64], float* red,
+                                                const f32x16 (&acc)[BM / waves_m<BM>() / 32][BN / 64], float* red,
                                                 int m0, int n0, int tm_idx) {
-  constexpr int WM = waves_m<BM, BN>();
+  constexpr int WM = waves_m<BM>();
   constexpr int TM = BM / WM / 32, TN = BN / 64;
   const int tid = threadIdx.x;
   const int lane = tid & 63;

@@ -30,7 +30,7 @@ namespace {
 using namespace x3conv;
 
 template <int BM, int BN, int MODE, bool DGRAD, int NP = 3>
-__global__ __launch_bounds__((waves_m<BM, BN>() * 128), ((NP == 2 && BM + BN <= 256) ? 2 : (BM + BN >= 256) ? 1 : 2)) void
+__global__ __launch_bounds__(waves_m<BM>() * 128, (NP == 2 && BM + BN <= 256) ? 2 : (BM + BN >= 256) ? 1 : 2) void
 conv_x3_kernel(ConvGemmParams p) {
   __shared__ __attribute__((aligned(16))) __bf16 smem[conv_x3_smem_elems<BM, BN, NP>()];
   conv_x3_body<BM, BN, MODE, DGRAD, NP>(p, smem, blockIdx.x, gridDim.x);
@@ -38,7 +38,7 @@ conv_x3_kernel(ConvGemmParams p) {
 
 template <int BM, int BN, int MODE, bool DGRAD>
 void launch_x3(const ConvGemmParams& p, int ntiles, int np, hipStream_t st) {
-  const dim3 blk(waves_m<BM, BN>() * 128), grd(ntiles * p.splits);
+  const dim3 blk(waves_m<BM>() * 128), grd(ntiles * p.splits);
   if (np == 1) hipLaunchKernelGGL((conv_x3_kernel<BM, BN, MODE, DGRAD, 1>), grd, blk, 0, st, p);
   else if (np == 2) hipLaunchKernelGGL((conv_x3_kernel<BM, BN, MODE, DGRAD, 2>), grd, blk, 0, st, p);
   else hipLaunchKernelGGL((conv_x3_kernel<BM, BN, MODE, DGRAD, 3>), grd, blk, 0, st, p);
@@ -48,10 +48,7 @@ template <int MODE, bool DGRAD>
 void dispatch_x3(const ConvGemmParams& p, int bm, int bn, int np, hipStream_t st) {
   const int ntm = (p.M + bm - 1) / bm, ntn = (p.Nout + bn - 1) / bn;
   const int nt = ntm * ntn;
-  if (bm == 256 && bn == 256 && MODE == 0 && np == 2)  // the f16x2 256x256 tile (4 waves, 128x128 each)
-    hipLaunchKernelGGL((conv_x3_kernel<256, 256, 0, DGRAD, 2>), dim3(nt * p.splits), dim3(waves_m<256, 256>() * 128), 0,
-                       st, p);
-  else if (bm == 256) launch_x3<256, 128, MODE, DGRAD>(p, (bn == 256 ? ntm * ((p.Nout + 127) / 128) : nt), np, st);
+  if (bm == 256) launch_x3<256, 128, MODE, DGRAD>(p, nt, np, st);
   else if (bm == 128 && bn == 128) launch_x3<128, 128, MODE, DGRAD>(p, nt, np, st);
   else if (bm == 128 && bn == 64) launch_x3<128, 64, MODE, DGRAD>(p, nt, np, st);
   else if (bm == 64 && bn == 128) launch_x3<64, 128, MODE, DGRAD>(p, nt, np, st);

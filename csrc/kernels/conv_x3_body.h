@@ -67,7 +67,7 @@ template <int BM, int BN, int MODE, bool DGRAD, int NP = 3>
 __device__ __forceinline__ void conv_x3_body(const ConvGemmParams& p, __bf16* __restrict__ smem, int vbid, int nvb) {
   static_assert(NP >= 1 && NP <= 3, "planes");
   constexpr unsigned ES = 2u;  // log2 bytes per element of the (fp32) global operands
-  constexpr int WM = waves_m<BM, BN>();  // waves along M (2 x WM waves)
+  constexpr int WM = waves_m<BM>();  // waves along M (2 x WM waves)
   constexpr int NT = WM * 128;       // threads
   constexpr int RS = NT / 4;         // rows covered by one pass of the loaders
   constexpr int TM = BM / WM / 32;
@@ -365,32 +365,8 @@ __device__ __forceinline__ void conv_x3_body(const ConvGemmParams& p, __bf16* __
 
   // Software pipeline, one barrier per K-tile: while the MFMAs consume stage t&1, tile t+1
   // (loaded into registers one iteration earlier) is split into stage (t+1)&1 and tile t+2 is
-  // being fetched into the other register set. The 256x256 tile (128x128 per wave, 256
-  // accumulator registers) keeps ONE register set: tile t+1 is fetched while the MFMAs consume
-  // tile t and split into the other stage right after them.
-  constexpr bool kTwoSets = !(BM >= 256 && BN >= 256);
-  if constexpr (!kTwoSets) {
-    if (kt_begin < kt_end) {
-    load_tile(kt_begin, va0, vb0, true);
-    if constexpr (NP == 2) {
-      sa = amax_finish(p.amax_a, p.amax_na, amx_a);
-      sb = amax_finish(p.amax_b, p.amax_nb, amx_b);
-    }
-    store_tile(va0, vb0, smem);
-    __syncthreads();
-    int cur = 0;
-    for (int kt = kt_begin; kt < kt_end; ++kt) {
-      load_tile(kt + 1, va0, vb0, kt + 1 < kt_end);
-      compute(smem + cur * STAGE);
-      store_tile(va0, vb0, smem + (cur ^ 1) * STAGE);  // past the last tile: a stage nothing reads
-      __syncthreads();
-      cur ^= 1;
-    }
-    } else if constexpr (NP == 2) {
-      sa = amax_finish(p.amax_a, p.amax_na, amx_a);
-      sb = amax_finish(p.amax_b, p.amax_nb, amx_b);
-    }
-  } else if (kt_begin < kt_end) {
+  // being fetched into the other register set.
+  if (kt_begin < kt_end) {
     load_tile(kt_begin, va0, vb0, true);
     load_tile(kt_begin + 1, va1, vb1, kt_begin + 1 < kt_end);
     if constexpr (NP == 2) {

@@ -562,10 +562,7 @@ GemmPlan plan_gemm(long long M, int Nout, int Kdim) {
   if (o.bn) g.bn = o.bn;
   if (o.splits) g.splits = std::max(1, std::min(o.splits, g.ktiles));
   if (g.bm == 256 && !x3_family()) g.bm = 128;
-  // 256-row conv tiles: 256x128, or 256x256 (f16x2, C % 32 == 0 gathers only; dispatch_x3 falls back
-  // to 256x128 otherwise)
-  if (g.bm == 256 && !(g.bn == 256 && f16x2_mode())) g.bn = 128;
-  if (g.bm != 256 && g.bn == 256) g.bn = 128;
+  if (g.bm == 256) g.bn = 128;  // the only 256-row conv tile (dispatch_x3)
   return g;
 }
 
@@ -650,9 +647,8 @@ at::Tensor pad_channels4(const at::Tensor& t, at::Tensor* amax = nullptr) {
 void set_gemm_override(const std::string& kind, int64_t bm, int64_t bn, int64_t splits) {
   TORCH_CHECK(kind == "conv" || kind == "wgrad", "set_gemm_override: kind must be 'conv' or 'wgrad'");
   TORCH_CHECK(bm == 0 || bm == 64 || bm == 128 || bm == 256, "bm must be 0, 64, 128 or 256");
-  TORCH_CHECK(bn == 0 || bn == 64 || bn == 128 || (bn == 256 && bm == 256 && kind == "conv"),
-              "bn must be 0, 64 or 128 (256: the 256x256 conv tile)");
-  TORCH_CHECK(bm != 256 || bn == 128 || bn == 256, "256-row tiles are 256x128 or 256x256");
+  TORCH_CHECK(bn == 0 || bn == 64 || bn == 128, "bn must be 0, 64 or 128");
+  TORCH_CHECK(bm != 256 || bn == 128, "256-row tiles are 256x128");
   PlanOverride& o = kind == "conv" ? conv_override() : wgrad_override();
   o.bm = (int)bm;
   o.bn = (int)bn;

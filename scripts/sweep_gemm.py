@@ -24,7 +24,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 VGG = [(3, 64, 32), (64, 128, 16), (128, 256, 8), (256, 256, 8), (256, 512, 4), (512, 512, 4), (512, 512, 2),
        (512, 512, 2)]
-CONV_TILES = [(256, 256), (256, 128), (128, 128), (128, 64), (64, 128), (64, 64)]
+CONV_TILES = [(256, 128), (128, 128), (128, 64), (64, 128), (64, 64)]
 WGRAD_TILES = [(256, 128), (128, 128), (128, 64), (64, 128), (64, 64)]
 SPLITS = [1, 2, 3, 4, 5, 6, 8, 10, 12, 16, 20, 24, 32, 48, 64]
 
@@ -64,7 +64,6 @@ def main():
     ap.add_argument("--layers", default="1,2,3,4,5,6,7")
     ap.add_argument("--ops", default="fwd,dgrad,wgrad")
     ap.add_argument("--out", default="gpurun_out/sweep_gemm.json")
-    ap.add_argument("--tiles", default=None, help="restrict conv tiles, e.g. 256x256,256x128")
     args = ap.parse_args()
     import cs744_distributed_data_parallel_amd as cdp
 
@@ -86,14 +85,10 @@ def main():
                     kind, shape = "conv", (M, Co, 9 * Ci)
                     fn = lambda: C.conv2d_fwd(x, w, b, 1, 1, True, xa, wa)  # noqa: E731
                     tiles = CONV_TILES
-                    if args.tiles:
-                        tiles = [tuple(int(v) for v in t.split("x")) for t in args.tiles.split(",")]
                 elif op == "dgrad":
                     kind, shape = "conv", (M, Ci, 9 * Co)
                     fn = lambda: C.conv2d_dgrad(gy, w, list(x.shape), 1, 1, None, ga, wa, wt)  # noqa: E731
                     tiles = CONV_TILES
-                    if args.tiles:
-                        tiles = [tuple(int(v) for v in t.split("x")) for t in args.tiles.split(",")]
                 else:
                     kind, shape = "wgrad", (M, Co, 9 * Ci)
                     fn = lambda: C.conv2d_wgrad(gy, x, list(w.shape), 1, 1, None, False, ga, xa)  # noqa: E731
