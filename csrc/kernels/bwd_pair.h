@@ -40,10 +40,7 @@ __global__ __launch_bounds__(waves_m<DBM>() * 128, DBM >= 256 ? 1 : 2) void bwd_
 }
 
 template <int DBM, int DBN, int WBM, int WBN>
-void launch_pair(const ConvGemmParams& pd0, const WgradParams& pw0, hipStream_t st) {
-  ConvGemmParams pd = pd0;
-  WgradParams pw = pw0;
-  pd.stagger = pw.stagger = stagger_flag();
+void launch_pair(const ConvGemmParams& pd, const WgradParams& pw, hipStream_t st) {
   const int nd = ((pd.M + DBM - 1) / DBM) * ((pd.Nout + DBN - 1) / DBN) * pd.splits;
   const int nw = ((pw.Cout + WBM - 1) / WBM) * ((pw.Kdim + WBN - 1) / WBN) * pw.splits;
   hipLaunchKernelGGL((bwd_pair_kernel<DBM, DBN, WBM, WBN>), dim3(nd + nw), dim3(PairCfg<DBM, DBN, WBM, WBN>::kThreads),

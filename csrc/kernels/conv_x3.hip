@@ -57,9 +57,7 @@ void dispatch_x3(const ConvGemmParams& p, int bm, int bn, int np, hipStream_t st
 
 }  // namespace
 
-void conv_x3_launch(const ConvGemmParams& p0, int bm, int bn, bool dgrad, hipStream_t st, int np) {
-  ConvGemmParams p = p0;
-  p.stagger = stagger_flag();
+void conv_x3_launch(const ConvGemmParams& p, int bm, int bn, bool dgrad, hipStream_t st, int np) {
   if ((p.C % BK) == 0 && (p.Kdim % BK) == 0) {
     if (dgrad) dispatch_x3<0, true>(p, bm, bn, np, st);
     else dispatch_x3<0, false>(p, bm, bn, np, st);

@@ -376,37 +376,17 @@ __device__ __forceinline__ void conv_x3_body(const ConvGemmParams& p, __bf16* __
     store_tile(va0, vb0, smem);
     __syncthreads();
     int kt = kt_begin;
-    // Stagger (8-wave tiles): waves w and w + 4 share a SIMD. With every wave running
-    // [MFMAs on tile t, then split + store of tile t+1] between two barriers, both waves of a SIMD
-    // want the matrix pipe at the same time and then the vector ALU at the same time. Waves 4-7
-    // store first and compute second, so on every SIMD one wave's split overlaps the other's
-    // MFMAs. Legal either way: tile t+1 goes to the stage that compute(t-1) -- finished before the
-    // last barrier -- read, and compute(t) reads the stage stored before it.
-    const bool late = NT == 512 && p.stagger && wid >= 4;
-    if (late) {
-      for (; kt + 1 < kt_end; kt += 2) {
-        load_tile(kt + 2, va0, vb0, kt + 2 < kt_end);
-        store_tile(va1, vb1, smem + STAGE);
-        compute(smem);
-        __syncthreads();
-        load_tile(kt + 3, va1, vb1, kt + 3 < kt_end);
-        store_tile(va0, vb0, smem);
-        compute(smem + STAGE);
-        __syncthreads();
-      }
-    } else {
-      for (; kt + 1 < kt_end; kt += 2) {
-        load_tile(kt + 2, va0, vb0, kt + 2 < kt_end);
-        compute(smem);
-        store_tile(va1, vb1, smem + STAGE);
-        __syncthreads();
-        load_tile(kt + 3, va1, vb1, kt + 3 < kt_end);
-        compute(smem + STAGE);
-        // unconditional (past the last tile it stores stale registers into a stage nothing reads),
-        // so the split can interleave with the MFMAs above
-        store_tile(va0, vb0, smem);
-        __syncthreads();
-      }
+    for (; kt + 1 < kt_end; kt += 2) {
+      load_tile(kt + 2, va0, vb0, kt + 2 < kt_end);
+      compute(smem);
+      store_tile(va1, vb1, smem + STAGE);
+      __syncthreads();
+      load_tile(kt + 3, va1, vb1, kt + 3 < kt_end);
+      compute(smem + STAGE);
+      // unconditional (past the last tile it stores stale registers into a stage nothing reads),
+      // so the split can interleave with the MFMAs above
+      store_tile(va0, vb0, smem);
+      __syncthreads();
     }
     if (kt < kt_end) compute(smem);  // odd tile count: the last tile sits in stage 0
   } else if constexpr (NP == 2) {  // no K-tiles: the (zero) accumulators still get unscaled

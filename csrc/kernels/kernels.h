@@ -4,8 +4,6 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
-#include <cstdlib>
-
 namespace cdp {
 
 // Exact division by a runtime-invariant divisor for dividends in [0, 2^31):
@@ -51,16 +49,6 @@ __device__ __forceinline__ long long remap_row(const RowRemap& r, int m) {
 }
 #endif
 
-// CDP_STAGGER=0: every wave of an 8-wave GEMM tile computes before it stores (A/B of the stagger,
-// see conv_x3_body); the launchers stamp it into the parameter block
-inline int stagger_flag() {
-  static const int on = [] {
-    const char* e = std::getenv("CDP_STAGGER");
-    return (e && e[0] == '0') ? 0 : 1;
-  }();
-  return on;
-}
-
 struct ConvGemmParams {
   const float* x;     // gather source, NHWC [N][H][W][C]
   const float* w;     // B^T rows [Nout][Kdim], Kdim ordered (kh, kw, c)
@@ -80,9 +68,6 @@ struct ConvGemmParams {
   const float* amax_a;
   const float* amax_b;
   int amax_na, amax_nb;
-  // 8-wave tiles: waves 4-7 split + store the next K-tile BEFORE their MFMAs on the current one,
-  // waves 0-3 after (set by the launcher from CDP_STAGGER; see conv_x3_body)
-  int stagger;
 };
 
 struct WgradParams {
@@ -95,7 +80,6 @@ struct WgradParams {
   const float* amax_dy;  // f16x2 engine: partial |max| values of dY and of x
   const float* amax_x;
   int amax_ndy, amax_nx;
-  int stagger;  // as ConvGemmParams::stagger (the 512-thread pipelined tile)
 };
 
 // conv_igemm.hip (exact fp32-input MFMA)

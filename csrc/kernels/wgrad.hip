@@ -293,9 +293,7 @@ void wgrad_launch_t(const WgradParams& p, bool x3, hipStream_t st, int np) {
   }
 }
 
-void wgrad_launch(const WgradParams& p0, int bm, int bn, bool x3, hipStream_t st, int np) {
-  WgradParams p = p0;
-  p.stagger = stagger_flag();
+void wgrad_launch(const WgradParams& p, int bm, int bn, bool x3, hipStream_t st, int np) {
   if (bm == 256 && bn == 128 && x3 && np == 2 && (p.C % 4) == 0 && (p.Cout % 4) == 0) {
     // host plan only picks 256 for the pipelined f16x2 path (plan_wgrad)
     hipLaunchKernelGGL((wgrad_x3_kernel<256, 128, true, 2, true>), dim3(((p.Cout + 255) / 256) * ((p.Kdim + 127) / 128) * p.splits),

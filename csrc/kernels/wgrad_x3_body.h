@@ -286,31 +286,15 @@ __device__ __forceinline__ void wgrad_x3_body(const WgradParams& p, __bf16* __re
       store_tile(ra, rb, smem);
       __syncthreads();
       int kt = kt_begin;
-      // waves 4-7 store first (see conv_x3_body's stagger): one wave of each SIMD splits while the
-      // other runs its MFMAs
-      const bool late = NT == 512 && p.stagger && wid >= 4;
-      if (late) {
-        for (; kt + 1 < kt_end; kt += 2) {
-          load_tile(kt + 2, ra, rb, kt + 2 < kt_end);
-          store_tile(ra1, rb1, smem + STAGE);
-          compute(smem);
-          __syncthreads();
-          load_tile(kt + 3, ra1, rb1, kt + 3 < kt_end);
-          store_tile(ra, rb, smem);
-          compute(smem + STAGE);
-          __syncthreads();
-        }
-      } else {
-        for (; kt + 1 < kt_end; kt += 2) {
-          load_tile(kt + 2, ra, rb, kt + 2 < kt_end);
-          compute(smem);
-          store_tile(ra1, rb1, smem + STAGE);
-          __syncthreads();
-          load_tile(kt + 3, ra1, rb1, kt + 3 < kt_end);
-          compute(smem + STAGE);
-          store_tile(ra, rb, smem);  // past the last tile: stale registers into a stage nothing reads
-          __syncthreads();
-        }
+      for (; kt + 1 < kt_end; kt += 2) {
+        load_tile(kt + 2, ra, rb, kt + 2 < kt_end);
+        compute(smem);
+        store_tile(ra1, rb1, smem + STAGE);
+        __syncthreads();
+        load_tile(kt + 3, ra1, rb1, kt + 3 < kt_end);
+        compute(smem + STAGE);
+        store_tile(ra, rb, smem);  // past the last tile: stale registers into a stage nothing reads
+        __syncthreads();
       }
       if (kt < kt_end) compute(smem);
     } else {
