@@ -1,5 +1,6 @@
 set -o pipefail
 mkdir -p gpurun_out
-for lb in 32 256; do bash scripts/ab_env.sh CDP_BN_BWD_FIN "0 1" 2 --local-batch $lb || exit 1; done
-PMC_MIX=1 bash scripts/pmc_layers.sh pm256 256 || exit 1
-bash scripts/prof_bench.sh b32m 10 --local-batch 32 || exit 1
+PMC_MEM=1 bash scripts/pmc_layers.sh pmem256 256 > /dev/null || exit 1
+python scripts/pmc_layers_summary.py gpurun_out/pmem256 256 | tail -20
+bash scripts/prof_bench.sh b32f 10 --local-batch 32 || exit 1
+bash scripts/prof_bench.sh b256f 6 || exit 1

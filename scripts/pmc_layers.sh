@@ -22,5 +22,11 @@ if [ -n "$PMC_MIX" ]; then
     --output-format csv -d gpurun_out/$TAG/mix -o run -- \
     python bench.py --no-graph --no-extra --steps 2 --warmup 1 --local-batch $LB > gpurun_out/$TAG/mix.log 2>&1 || exit $?
 fi
+# optional third pass: L2 hits / misses and memory-side requests of the same dispatches
+if [ -n "$PMC_MEM" ]; then
+  timeout -s KILL 200 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum TCC_EA0_WRREQ_sum GRBM_GUI_ACTIVE \
+    --output-format csv -d gpurun_out/$TAG/mem -o run -- \
+    python bench.py --no-graph --no-extra --steps 2 --warmup 1 --local-batch $LB > gpurun_out/$TAG/mem.log 2>&1 || exit $?
+fi
 python scripts/pmc_layers_summary.py gpurun_out/$TAG $LB > gpurun_out/$TAG/layers.md
 cat gpurun_out/$TAG/layers.md

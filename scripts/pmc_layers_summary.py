@@ -108,3 +108,28 @@ def main(d, B):
 
 if __name__ == "__main__":
     main(sys.argv[1], sys.argv[2] if len(sys.argv) > 2 else 256)
+
+
+def mem_table(d):
+    mem = rows_of(os.path.join(d, "mem", "*counter_collection.csv"))
+    if not mem:
+        return
+    byd = collections.defaultdict(dict)
+    nm = {}
+    for r in mem:
+        did = int(r.get("Dispatch_Id") or r.get("Correlation_Id"))
+        byd[did][r["Counter_Name"]] = byd[did].get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
+        nm[did] = r["Kernel_Name"]
+    md = [(did, nm[did]) for did in sorted(byd) if kind(nm[did])]
+    ml = max(i for i, (_, n) in enumerate(md) if kind(n) == "fwd0")
+    print("\n| # | GEMM | L2 hit % | L2 requests (M) | memory-side read requests (M) | write requests (M) | wall us (GRBM/8 @ 2.1 GHz) |")
+    print("|---|---|---|---|---|---|---|")
+    for i, (did, n) in enumerate(md[ml:]):
+        c = byd[did]
+        h, m = c.get("TCC_HIT_sum", 0), c.get("TCC_MISS_sum", 0)
+        print(f"| {i} | {kind(n)} | {100 * h / max(1, h + m):.1f} | {(h + m) / 1e6:.2f} | {c.get('TCC_EA0_RDREQ_sum', 0) / 1e6:.2f} | "
+              f"{c.get('TCC_EA0_WRREQ_sum', 0) / 1e6:.2f} | {c.get('GRBM_GUI_ACTIVE', 0) / 8 / 2.1e3:.1f} |")
+
+
+if __name__ == "__main__" and len(sys.argv) > 1:
+    mem_table(sys.argv[1])
