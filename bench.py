@@ -206,7 +206,10 @@ class _Run:
         dbg("eager warmup done")
         # gloo executes its collectives on the host, which no stream capture survives (and a rank
         # failing mid-capture would leave its peer blocked in the collective): eager steps
-        if self.args.no_graph or not cuda or self.args.dist_backend == "gloo":
+        # (a no-sync step of the per-tensor strategies has no collective in it: those are captured
+        # under gloo too, which lets the one-GPU rehearsal exercise the capture agreement)
+        no_coll = not self.sync_grads and self.args.strategy in ("allreduce_blocking", "gather_scatter")
+        if self.args.no_graph or not cuda or (self.args.dist_backend == "gloo" and not no_coll):
             return
         from cs744_distributed_data_parallel_amd import distributed as D
 

@@ -93,3 +93,27 @@ def test_two_ranks_on_one_gpu_strategy_equivalence():
     info = outs["ddp"][0][2]
     assert info["native_reducer"], info
     assert info["rebuilt_buckets"], info
+
+
+def test_capture_failure_on_one_rank_makes_every_rank_eager():
+    """Two ranks on the one GPU (gloo): in the collective-free no-sync step that bench.py also times,
+    rank 1's hipGraph capture is broken on purpose (CDP_BENCH_BREAK_CAPTURE=1), rank 0's succeeds.
+    The ranks agree BEFORE any replay, so both time eager steps, nobody replays a graph the other
+    cannot match, and the run finishes with one record and identical replicas."""
+    import json
+    import os
+    import subprocess
+    import sys
+
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, PYTHONPATH=repo, CDP_BENCH_BREAK_CAPTURE="1", HSA_ENABLE_IPC_MODE_LEGACY="0")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT"):
+        env.pop(k, None)
+    r = subprocess.run([sys.executable, os.path.join(repo, "bench.py"), "--gpus", "2", "--dist-backend", "gloo",
+                        "--strategy", "allreduce_blocking", "--steps", "2", "--warmup", "1", "--local-batch", "8",
+                        "--dataset-size", "64"], env=env, capture_output=True, text=True, timeout=240, cwd=repo)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    assert "hipGraph capture failed" in r.stderr, r.stderr[-3000:]
+    assert "another rank could not capture; all ranks time eager steps" in r.stderr, r.stderr[-3000:]
+    rec = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    assert rec["replicas_identical"] is True and rec["ranks_seen"] == 2
