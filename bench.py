@@ -164,6 +164,7 @@ class _Run:
         self.order = self.loader._order()
         self.nb = max(1, self.order.numel() // local_batch)
         self.graph = None
+        self.seed = None
         self.graph_collectives = None  # native-communicator collectives recorded in the captured step
         # test hooks: CDP_BENCH_BREAK_CAPTURE=1 (every rank) or =r (rank r only) invalidates the capture;
         # CDP_BENCH_CORRUPT_RANK=r perturbs rank r's gradient after the sync (replicas then diverge)
@@ -183,7 +184,9 @@ class _Run:
             if self.sync is not None and self.sync_grads:
                 self.sync.prepare(out)
             loss = self.crit(out, y)
-            loss.backward()
+            if self.seed is None:  # persistent d(loss)/d(loss): no fill kernel in the captured step
+                self.seed = self.torch.ones_like(loss)
+            loss.backward(self.seed)
         if self.sync_grads and strategy == "allreduce_blocking":
             cdp.parallel.average_gradients_allreduce(self.model)
         elif self.sync_grads and strategy == "gather_scatter":
