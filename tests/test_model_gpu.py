@@ -306,3 +306,52 @@ def test_graph_capture_training_step():
         losses.append(static_loss.item())
     assert all(torch.isfinite(torch.tensor(losses)))
     assert losses[-1] < losses[0]  # same batch repeatedly: loss must go down
+
+
+@pytest.mark.parametrize("batch", [32, 256])
+def test_vgg11_chan_fusion_matches_unfused(monkeypatch, batch):
+    """Channel-owner fusion (chan_fuse.hip: one launch per small layer reduces the split-K slabs and
+    runs the whole BatchNorm, forward and backward) vs the row-blocked reduction + finalize/apply
+    launches: loss, every gradient and the running statistics agree to the rounding of the
+    reordered fp64 statistics merges, and the fused path is really taken."""
+    import cs744_distributed_data_parallel_amd as cdp
+
+    C = cdp._native.lib()
+    torch.manual_seed(0)
+    model = cdp.VGG11().cuda()
+    init = {k: v.clone() for k, v in model.state_dict().items()}
+    x = torch.randn(batch, 3, 32, 32, device="cuda").contiguous(memory_format=torch.channels_last)
+    t = torch.randint(0, 10, (batch,), device="cuda")
+    crit = cdp.CrossEntropyLoss()
+
+    def run():
+        model.load_state_dict(init)
+        model.zero_grad(set_to_none=True)
+        loss = crit(model(x), t)
+        loss.backward()
+        torch.cuda.synchronize()
+        bufs = [b.detach().clone().double() for n, b in model.named_buffers() if "running" in n]
+        return loss.detach().clone(), [p.grad.detach().clone() for p in model.parameters()], bufs
+
+    monkeypatch.setenv("CDP_CHAN", "1")
+    f0, b0 = C.chan_launches()
+    l_c, g_c, r_c = run()
+    f1, b1 = C.chan_launches()
+    # B=32: the six split-K forward layers, and every backward hand-off but the stem's and layer 1's
+    assert f1 - f0 >= (4 if batch == 256 else 6) and b1 - b0 >= (3 if batch == 256 else 5), (f1 - f0, b1 - b0)
+    monkeypatch.setenv("CDP_CHAN", "0")
+    l_s, g_s, r_s = run()
+    assert C.chan_launches() == [f1, b1]
+    assert abs(l_c.item() - l_s.item()) <= 1e-6 * abs(l_s.item())
+    for a, b in zip(r_c, r_s):
+        assert ((a - b).norm() / b.norm().clamp_min(1e-30)).item() < 1e-6
+    named = dict(zip([n for n, _ in model.named_parameters()], zip(g_c, g_s)))
+    for name, (a, b) in named.items():
+        conv_bias = name.startswith("layers.") and name.endswith(".bias") and \
+            isinstance(model.layers[int(name.split(".")[1])], torch.nn.Conv2d)
+        if conv_bias:  # analytically zero before training-mode BN: rounding noise
+            beta = named[name.split(".")[0] + "." + str(int(name.split(".")[1]) + 1) + ".bias"][1]
+            assert (a - b).norm() <= 1e-5 * beta.norm(), name
+            continue
+        err = ((a - b).norm() / b.norm().clamp_min(1e-30)).item()
+        assert err < 1e-5, (name, err)
