@@ -210,7 +210,7 @@ class _ConvBNAct(torch.autograd.Function):
         chan = (False, None, None, None)
         if li is not None and li.consumers == 1 and nig[0] and not park_dx and addend is None:
             prev = (li.y, li.stats, li.pool, li.relu, li.ps)
-            if li.chan:
+            if li.chan and _chan_on():
                 pg, pb, pbias = li.params
                 need = [t is not None and t.requires_grad for t in li.params]
                 dbs = _slot(pbias, need[2])

@@ -8,9 +8,11 @@
 // reduction sums them and emits per-row-block statistics partials, and a finalize+apply launch
 // merges the partials and writes the activation. A device-wide barrier is not cheaper than a
 // launch on MI355X (docs/PERF.md: every block has to write back / invalidate its XCD's L2).
-// Here a workgroup instead owns one channel quad for ALL rows (512 threads, up to 16 rows each in
-// registers), so the whole reduction -> statistics -> apply chain is block-local: one launch
-// after the GEMM instead of two. Channels are independent, so there is no cross-block traffic.
+// Here a workgroup instead owns 16 channels for ALL rows (512 threads = 4 channel quads x 128 row
+// lanes, up to 16 rows each in registers), so the whole reduction -> statistics -> apply chain is
+// block-local: one launch after the GEMM instead of two. Channels are independent, so there is no
+// cross-block traffic. (16 channels = 64 B per row and lane group: with one quad per block (16 B
+// per row, 64 rows = 64 cache lines per wave instruction) the same launches ran 3x slower.)
 //
 //   chan_fwd_kernel:  y = sum_z slab[z] + bias (saved for backward); mean / var over the block's
 //                     rows (two-pass, fp64 merge); running statistics; out = [pool2](relu(BN(y)));
@@ -33,6 +35,9 @@ namespace {
 
 constexpr int NT = 512;  // threads per block (8 waves)
 constexpr int NW = NT / 64;
+constexpr int CQ = 4;         // channel quads per block
+constexpr int CB = 4 * CQ;    // channels per block
+constexpr int RL = NT / CQ;   // row lanes
 
 __device__ __forceinline__ float4 f4add4(float4 a, float4 b) {
   return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
@@ -53,8 +58,9 @@ __device__ __forceinline__ float amax4(float4 z) {
   return fmaxf(fmaxf(fabsf(z.x), fabsf(z.y)), fmaxf(fabsf(z.z), fabsf(z.w)));
 }
 
-// Block-wide fp64 sums of K per-thread float4 values: component j of value k -> red[k * 4 + j]
-// (LDS, visible to every thread on return). red: (NW + 1) x K x 4 doubles.
+// Block-wide fp64 sums over the row lanes of K per-thread float4 values: channel quad q = tid % CQ,
+// component j of value k -> red[k * CB + 4 q + j] (LDS, visible to every thread on return).
+// red: (NW + 1) x K x CB doubles.
 template <int K>
 __device__ __forceinline__ void block_sum4(const float4 (&v)[K], double* red) {
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -62,16 +68,18 @@ __device__ __forceinline__ void block_sum4(const float4 (&v)[K], double* red) {
   for (int k = 0; k < K; ++k)
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const double s = wave_sum_d((double)f4c(v[k], j));
-      if (lane == 0) red[(K * 4) + (wv * K + k) * 4 + j] = s;
+      double s = (double)f4c(v[k], j);
+#pragma unroll
+      for (int o = 32; o >= CQ; o >>= 1) s += __shfl_xor(s, o, 64);
+      if (lane < CQ) red[K * CB + (wv * K + k) * CB + 4 * lane + j] = s;
     }
   __syncthreads();
-  if (threadIdx.x < K * 4) {
-    const int k = threadIdx.x >> 2, j = threadIdx.x & 3;
+  if (threadIdx.x < K * CB) {
+    const int k = threadIdx.x / CB, e = threadIdx.x % CB;
     double s = 0.0;
 #pragma unroll
-    for (int w = 0; w < NW; ++w) s += red[(K * 4) + (w * K + k) * 4 + j];
-    red[k * 4 + j] = s;
+    for (int w = 0; w < NW; ++w) s += red[K * CB + (w * K + k) * CB + e];
+    red[threadIdx.x] = s;
   }
   __syncthreads();
 }
@@ -101,19 +109,20 @@ template <int RT, bool POOL>
 __global__ __launch_bounds__(NT) void chan_fwd_kernel(ChanFwdArgs a) {
   constexpr int RPU = POOL ? 4 : 1;
   constexpr int UPT = RT / RPU;
-  constexpr int ZB = RT >= 16 ? 1 : RT >= 8 ? 2 : RT >= 4 ? 4 : 8;
-  __shared__ double red[(NW + 1) * 4];
+  constexpr int ZB = 16 / RT;  // 16 slab loads in flight per lane
+  __shared__ double red[(NW + 1) * CB];
   __shared__ float fred[NW];
-  __shared__ float4 s_sc, s_sh;
+  __shared__ float s_sc[CB], s_sh[CB];
   const int tid = threadIdx.x;
-  const int C = a.C, n0 = blockIdx.x * 4;
+  const int q = tid % CQ, rl = tid / CQ;
+  const int C = a.C, n0 = blockIdx.x * CB + 4 * q;
   const int Ho = POOL ? a.H / 2 : a.H, Wo = POOL ? a.W / 2 : a.W;
   const int U = a.N * Ho * Wo;
   const int M = a.N * a.H * a.W;
   unsigned off[RT];  // byte offsets of the rows (kOOB for slots past the last unit)
 #pragma unroll
   for (int i = 0; i < UPT; ++i) {
-    const int u = tid + NT * i;
+    const int u = rl + RL * i;
 #pragma unroll
     for (int k = 0; k < RPU; ++k)
       off[i * RPU + k] = u < U ? unit_row<POOL>(u, k, a.H, a.W, Ho, Wo, C, n0) * 4u : kOOB;
@@ -151,29 +160,29 @@ __global__ __launch_bounds__(NT) void chan_fwd_kernel(ChanFwdArgs a) {
     block_sum4<1>(sv, red);
   }
   const double invM = 1.0 / (double)M;
-  const float4 mf = make_float4((float)(red[0] * invM), (float)(red[1] * invM), (float)(red[2] * invM),
-                                (float)(red[3] * invM));
-  const double tot = tid < 4 ? red[tid] : 0.0;
+  const float4 mf = make_float4((float)(red[4 * q] * invM), (float)(red[4 * q + 1] * invM),
+                                (float)(red[4 * q + 2] * invM), (float)(red[4 * q + 3] * invM));
+  const double tot = tid < CB ? red[tid] : 0.0;
   __syncthreads();  // red is reused below
-  float4 q = f4zero();
+  float4 sq = f4zero();
 #pragma unroll
   for (int r = 0; r < RT; ++r) {
     if (off[r] == kOOB) continue;
     const float dx = v[r].x - mf.x, dy = v[r].y - mf.y, dz = v[r].z - mf.z, dw = v[r].w - mf.w;
-    q.x = fmaf(dx, dx, q.x);
-    q.y = fmaf(dy, dy, q.y);
-    q.z = fmaf(dz, dz, q.z);
-    q.w = fmaf(dw, dw, q.w);
+    sq.x = fmaf(dx, dx, sq.x);
+    sq.y = fmaf(dy, dy, sq.y);
+    sq.z = fmaf(dz, dz, sq.z);
+    sq.w = fmaf(dw, dw, sq.w);
   }
   {
-    const float4 qv[1] = {q};
+    const float4 qv[1] = {sq};
     block_sum4<1>(qv, red);
   }
-  if (tid < 4) {
-    const int c = n0 + tid;
+  if (tid < CB) {
+    const int c = blockIdx.x * CB + tid;
     const double mean = tot * invM;
     // the deviations were taken from the fp32-rounded mean: remove that offset's contribution
-    const double dm = mean - (double)f4c(mf, tid);
+    const double dm = mean - (double)(float)mean;
     const double M2 = fmax(0.0, red[tid] - (double)M * dm * dm);
     const double var = M2 * invM;
     const float invstd = (float)(1.0 / sqrt(var + (double)a.eps));
@@ -181,8 +190,8 @@ __global__ __launch_bounds__(NT) void chan_fwd_kernel(ChanFwdArgs a) {
     const float bb = a.beta ? a.beta[c] : 0.f;
     const float scale = g * invstd;
     const float shift = bb - (float)mean * scale;
-    f4set(s_sc, tid, scale);
-    f4set(s_sh, tid, shift);
+    s_sc[tid] = scale;
+    s_sh[tid] = shift;
     a.stats[c] = (float)mean;
     a.stats[C + c] = invstd;
     a.stats[2 * C + c] = scale;
@@ -198,11 +207,12 @@ __global__ __launch_bounds__(NT) void chan_fwd_kernel(ChanFwdArgs a) {
   __syncthreads();
   if (blockIdx.x == 0 && tid == 0 && a.nbt) a.nbt[0] += 1;
   // apply: [pool2](relu(y * scale + shift))
-  const float4 sc = s_sc, sh = s_sh;
+  const float4 sc = make_float4(s_sc[4 * q], s_sc[4 * q + 1], s_sc[4 * q + 2], s_sc[4 * q + 3]);
+  const float4 sh = make_float4(s_sh[4 * q], s_sh[4 * q + 1], s_sh[4 * q + 2], s_sh[4 * q + 3]);
   float am = 0.f;
 #pragma unroll
   for (int i = 0; i < UPT; ++i) {
-    const int u = tid + NT * i;
+    const int u = rl + RL * i;
     if (u >= U) continue;
     float4 z = act4(v[i * RPU], sc, sh, a.relu);
     if (POOL) {
@@ -256,12 +266,13 @@ template <int RT, bool POOL>
 __device__ __forceinline__ void chan_bwd_d(const ChanBwdArgs& a) {
   constexpr int RPU = POOL ? 4 : 1;
   constexpr int UPT = RT / RPU;
-  constexpr int ZB = UPT >= 8 ? 1 : UPT >= 4 ? 2 : 8;
-  __shared__ double red[(NW + 1) * 3 * 4];
+  constexpr int ZB = UPT >= 8 ? 1 : 8 / UPT;
+  __shared__ double red[(NW + 1) * 3 * CB];
   __shared__ float fred[NW];
-  __shared__ float4 s_k1, s_k2;
+  __shared__ float s_k1[CB], s_k2[CB];
   const int tid = threadIdx.x;
-  const int C = a.C, n0 = blockIdx.x * 4;
+  const int q = tid % CQ, rl = tid / CQ;
+  const int C = a.C, n0 = blockIdx.x * CB + 4 * q;
   const int Ho = POOL ? a.H / 2 : a.H, Wo = POOL ? a.W / 2 : a.W;
   const int U = a.N * Ho * Wo;
   const int M = a.N * a.H * a.W;
@@ -270,7 +281,7 @@ __device__ __forceinline__ void chan_bwd_d(const ChanBwdArgs& a) {
   unsigned go[UPT];  // byte offsets of the dX rows
 #pragma unroll
   for (int i = 0; i < UPT; ++i) {
-    const int u = tid + NT * i;
+    const int u = rl + RL * i;
     go[i] = u < U ? ((unsigned)u * (unsigned)C + (unsigned)n0) * 4u : kOOB;
 #pragma unroll
     for (int k = 0; k < RPU; ++k) yo[i * RPU + k] = u < U ? unit_row<POOL>(u, k, a.H, a.W, Ho, Wo, C, n0) * 4u : kOOB;
@@ -323,19 +334,20 @@ __device__ __forceinline__ void chan_bwd_d(const ChanBwdArgs& a) {
       }
   }
   block_sum4<3>(acc, red);
-  if (tid < 4) {
-    const int c = n0 + tid;
+  if (tid < CB) {
+    const int c = blockIdx.x * CB + tid;
     const double invM = 1.0 / (double)M;
-    const double t0 = red[tid], t1 = red[4 + tid], t2 = red[8 + tid];
-    f4set(s_k1, tid, (float)t0 * (float)invM);
-    f4set(s_k2, tid, (float)t1 * (float)invM);
+    const double t0 = red[tid], t1 = red[CB + tid], t2 = red[2 * CB + tid];
+    s_k1[tid] = (float)t0 * (float)invM;
+    s_k2[tid] = (float)t1 * (float)invM;
     if (a.gbeta) a.gbeta[c] = (float)t0;
     if (a.ggamma) a.ggamma[c] = (float)t1;
     // conv-bias gradient sum(dy) = -scale * sum(xhat) * sum(dz * xhat) / M
     if (a.gdb) a.gdb[c] = (float)(-(double)a.stats[2 * C + c] * t2 * t1 * invM);
   }
   __syncthreads();
-  const float4 k1 = s_k1, k2 = s_k2;
+  const float4 k1 = make_float4(s_k1[4 * q], s_k1[4 * q + 1], s_k1[4 * q + 2], s_k1[4 * q + 3]);
+  const float4 k2 = make_float4(s_k2[4 * q], s_k2[4 * q + 1], s_k2[4 * q + 2], s_k2[4 * q + 3]);
   // re-read after the barrier: the compiler must then recompute dz / xhat here instead of keeping
   // the first pass's values live across the reduction (which spilled at 16 rows per thread)
   const float4 mu2 = ld4(a.stats + n0), is2 = ld4(a.stats + C + n0);
@@ -367,9 +379,9 @@ __device__ __forceinline__ void chan_bwd_d(const ChanBwdArgs& a) {
 __device__ __forceinline__ void chan_bwd_w(const ChanBwdArgs& a, int bw) {
   __shared__ float4 wred[NT];
   const int tid = threadIdx.x;
-  const int CB = a.w_cb, SL = NT / CB;
-  const int cl = tid % CB, sl = tid / CB;
-  const long long i = (long long)bw * CB + cl;
+  const int wcb = a.w_cb, SL = NT / wcb;
+  const int cl = tid % wcb, sl = tid / wcb;
+  const long long i = (long long)bw * wcb + cl;
   float4 s = f4zero();
   if (i < a.w_n4) {
     int z = sl;
@@ -385,7 +397,7 @@ __device__ __forceinline__ void chan_bwd_w(const ChanBwdArgs& a, int bw) {
     wred[tid] = s;
     __syncthreads();
     if (sl != 0) return;
-    for (int k = 1; k < SL; ++k) s = f4add4(s, wred[k * CB + cl]);
+    for (int k = 1; k < SL; ++k) s = f4add4(s, wred[k * wcb + cl]);
   }
   if (i < a.w_n4) a.w_dst[i] = s;
 }
@@ -398,7 +410,7 @@ __global__ __launch_bounds__(NT) void chan_bwd_kernel(ChanBwdArgs a) {
 
 // rows held per thread for `units` units of rpu rows: 1, 2, 4, 8 or 16 (0: too many)
 int chan_rt(long long units, int rpu) {
-  const long long upt = (units + NT - 1) / NT;
+  const long long upt = (units + RL - 1) / RL;
   long long rt = upt * rpu;
   int p = 1;
   while (p < rt) p <<= 1;
@@ -410,25 +422,36 @@ long long chan_max_rows() {
   const char* off = std::getenv("CDP_CHAN");
   if (off && off[0] == '0') return 0;
   const char* e = std::getenv("CDP_CHAN_MAXROWS");
-  return e ? std::atoll(e) : 8192LL;
+  return e ? std::atoll(e) : 2048LL;
 }
 
 }  // namespace
 
-bool chan_fwd_ok(int N, int H, int W, int C, bool pool) {
-  const long long M = (long long)N * H * W;
-  if ((C % 4) != 0 || M > chan_max_rows() || M < 1) return false;
-  if (pool && ((H & 1) || (W & 1))) return false;
-  const long long units = pool ? M / 4 : M;
-  return chan_rt(units, pool ? 4 : 1) != 0 && M * C * 16LL < (1LL << 31);
+// Rows held per lane above which the fusion loses to the two-launch path (measured on MI355X,
+// VGG-11 at 32 images per GPU, eager rocprofv3, us per layer, fused vs reduction + finalize/apply):
+// forward 9.7 vs 11.5 at 1 row per lane, 15.2 vs 11.5 at 4, 26-30 vs ~12 at 16; backward 9.8 vs
+// 16.7 at 1, 11.4-15.8 vs 16.7 at 4, 31-33 vs 16.7 at 16. A block's rows are a serial chain of
+// split-K load batches, and 16 channels per block leave few blocks for the larger maps.
+int chan_rt_limit(bool bwd) {
+  const char* e = std::getenv(bwd ? "CDP_CHAN_BWD_RT" : "CDP_CHAN_FWD_RT");
+  return e ? std::atoi(e) : (bwd ? 4 : 1);
 }
 
-int chan_amax_parts(int C) { return C / 4; }
+bool chan_fwd_ok(int N, int H, int W, int C, bool pool, bool bwd) {
+  const long long M = (long long)N * H * W;
+  if ((C % CB) != 0 || M > chan_max_rows() || M < 1) return false;
+  if (pool && ((H & 1) || (W & 1))) return false;
+  const long long units = pool ? M / 4 : M;
+  const int rt = chan_rt(units, pool ? 4 : 1);
+  return rt != 0 && rt <= chan_rt_limit(bwd) && M * C * 16LL < (1LL << 31);
+}
+
+int chan_amax_parts(int C) { return C / CB; }
 
 void chan_fwd_launch(const ChanFwdArgs& a, hipStream_t st) {
   const long long M = (long long)a.N * a.H * a.W;
   const int rt = chan_rt(a.pool ? M / 4 : M, a.pool ? 4 : 1);
-  const dim3 grid(a.C / 4), blk(NT);
+  const dim3 grid(a.C / CB), blk(NT);
   if (a.pool) {
     if (rt <= 4) hipLaunchKernelGGL((chan_fwd_kernel<4, true>), grid, blk, 0, st, a);
     else if (rt == 8) hipLaunchKernelGGL((chan_fwd_kernel<8, true>), grid, blk, 0, st, a);
@@ -445,7 +468,7 @@ void chan_fwd_launch(const ChanFwdArgs& a, hipStream_t st) {
 void chan_bwd_launch(ChanBwdArgs a, hipStream_t st) {
   const long long M = (long long)a.N * a.H * a.W;
   const int rt = chan_rt(a.pool ? M / 4 : M, a.pool ? 4 : 1);
-  a.nbd = a.C / 4;
+  a.nbd = a.C / CB;
   int nbw = 0;
   if (a.w_slab) {
     a.w_cb = (a.w_n4 >= 256LL * 1024 || a.w_S <= 1) ? 512 : (a.w_n4 >= 64LL * 1024 || a.w_S <= 4) ? 128 : 32;

@@ -167,7 +167,7 @@ void bwd_reduce_launch(BwdReduceArgs a, hipStream_t st);
 int bwd_reduce_rows_per_part();
 
 // chan_fuse.hip: channel-owner fusion of a split-K reduction with the training-mode BatchNorm around
-// it, for layers with few rows (see the file header). One block per channel quad.
+// it, for layers with few rows (see the file header). One block per 16 channels.
 struct ChanFwdArgs {
   const float* slab;  // [S][M][C] split-K slabs of the conv output, M = N*H*W
   int S;
@@ -207,8 +207,9 @@ struct ChanBwdArgs {
   long long w_n4;
   int nbd, w_cb;  // set by the launcher
 };
-// (N, H, W, C) fits one block per channel quad (CDP_CHAN_MAXROWS rows, default 8192; 0 disables)
-bool chan_fwd_ok(int N, int H, int W, int C, bool pool);
+// (N, H, W, C) fits one block per 16 channels (<= 2048 rows, CDP_CHAN_MAXROWS; CDP_CHAN=0 disables)
+// (bwd: the backward kernel's limits, which differ)
+bool chan_fwd_ok(int N, int H, int W, int C, bool pool, bool bwd = false);
 int chan_amax_parts(int C);
 void chan_fwd_launch(const ChanFwdArgs& a, hipStream_t st);
 void chan_bwd_launch(ChanBwdArgs a, hipStream_t st);

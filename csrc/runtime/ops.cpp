@@ -1235,7 +1235,8 @@ std::vector<at::Tensor> conv_bn_act_bwd(const at::Tensor& gout_, const at::Tenso
                         : at::empty({C, cin, w.size(2), w.size(3)}, opts.memory_format(at::MemoryFormat::ChannelsLast));
     TORCH_CHECK(dw.is_contiguous(at::MemoryFormat::ChannelsLast), "stem dW slot must be channels_last");
     slab_sum_strided_launch(slab.data_ptr<float>(), nb, (long long)C * 36, 4, cin, dw.data_ptr<float>(), false, st);
-    return {at::Tensor(), dw, db, dgamma, dbeta, at::Tensor(), at::Tensor()};
+    return {at::Tensor(), dw, db, dgamma, dbeta, at::Tensor(), at::Tensor(), at::Tensor(), at::Tensor(), at::Tensor(),
+            at::Tensor(), at::Tensor()};
   }
   at::Tensor dy = have_dy ? *dy_in : at::empty({N, C, H, W}, opts.memory_format(at::MemoryFormat::ChannelsLast));
   at::Tensor dbpart;
@@ -1302,7 +1303,7 @@ std::vector<at::Tensor> conv_bn_act_bwd(const at::Tensor& gout_, const at::Tenso
   if (dr.d_on && has_prev && prev_chan && !(dx_addend.has_value() && dx_addend->defined())) {
     const at::Tensor py = nhwc(*prev_y);
     const int pN = py.size(0), pC = py.size(1), pH = py.size(2), pW = py.size(3);
-    chan = chan_fwd_ok(pN, pH, pW, pC, prev_pool) && dr.d_Nout == pC &&
+    chan = chan_fwd_ok(pN, pH, pW, pC, prev_pool, true) && dr.d_Nout == pC &&
            (long long)dr.d_S * dr.d_M * pC * 4 < (1LL << 31) &&
            (long long)dr.d_M == (long long)pN * (prev_pool ? (pH / 2) * (pW / 2) : pH * pW);
     if (chan) {

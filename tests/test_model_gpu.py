@@ -308,12 +308,18 @@ def test_graph_capture_training_step():
     assert losses[-1] < losses[0]  # same batch repeatedly: loss must go down
 
 
-@pytest.mark.parametrize("batch", [32, 256])
+@pytest.mark.parametrize("batch", [32, 64])
 def test_vgg11_chan_fusion_matches_unfused(monkeypatch, batch):
     """Channel-owner fusion (chan_fuse.hip: one launch per small layer reduces the split-K slabs and
     runs the whole BatchNorm, forward and backward) vs the row-blocked reduction + finalize/apply
-    launches: loss, every gradient and the running statistics agree to the rounding of the
-    reordered fp64 statistics merges, and the fused path is really taken."""
+    launches, and the fused paths are really taken.
+
+    Forward: loss and running statistics agree to the rounding of the reordered fp64 statistics
+    merges. Backward, on ONE forward (retain_graph, so both see the same ReLU masks and pool
+    argmaxes): every gradient agrees to 1e-5. (Two separate forwards are not comparable per
+    gradient: a statistic differing in its last bit moves an activation within rounding of 0 or of
+    its window's max to the other side, which reroutes gradient; the fused and unfused paths then
+    each differ from fp64 by ~1e-3 at 32 images, in different layers.)"""
     import cs744_distributed_data_parallel_amd as cdp
 
     C = cdp._native.lib()
@@ -324,27 +330,36 @@ def test_vgg11_chan_fusion_matches_unfused(monkeypatch, batch):
     t = torch.randint(0, 10, (batch,), device="cuda")
     crit = cdp.CrossEntropyLoss()
 
-    def run():
+    def fwd():
         model.load_state_dict(init)
         model.zero_grad(set_to_none=True)
         loss = crit(model(x), t)
-        loss.backward()
         torch.cuda.synchronize()
         bufs = [b.detach().clone().double() for n, b in model.named_buffers() if "running" in n]
-        return loss.detach().clone(), [p.grad.detach().clone() for p in model.parameters()], bufs
+        return loss, bufs
 
+    def grads(loss, chan):
+        monkeypatch.setenv("CDP_CHAN", "1" if chan else "0")
+        model.zero_grad(set_to_none=True)
+        loss.backward(retain_graph=True)
+        torch.cuda.synchronize()
+        return [p.grad.detach().clone() for p in model.parameters()]
+
+    monkeypatch.setenv("CDP_CHAN", "0")
+    l_s, r_s = fwd()
     monkeypatch.setenv("CDP_CHAN", "1")
     f0, b0 = C.chan_launches()
-    l_c, g_c, r_c = run()
-    f1, b1 = C.chan_launches()
-    # B=32: the six split-K forward layers, and every backward hand-off but the stem's and layer 1's
-    assert f1 - f0 >= (4 if batch == 256 else 6) and b1 - b0 >= (3 if batch == 256 else 5), (f1 - f0, b1 - b0)
-    monkeypatch.setenv("CDP_CHAN", "0")
-    l_s, g_s, r_s = run()
-    assert C.chan_launches() == [f1, b1]
+    l_c, r_c = fwd()
+    f1, _ = C.chan_launches()
+    assert f1 - f0 >= (1 if batch == 32 else 0), f1 - f0  # unpooled split-K layers with <= 128 rows
     assert abs(l_c.item() - l_s.item()) <= 1e-6 * abs(l_s.item())
     for a, b in zip(r_c, r_s):
         assert ((a - b).norm() / b.norm().clamp_min(1e-30)).item() < 1e-6
+    g_c = grads(l_c, True)
+    b1 = C.chan_launches()[1]
+    assert b1 - b0 >= (3 if batch == 32 else 1), b1 - b0  # hand-offs on maps of <= 512 rows
+    g_s = grads(l_c, False)
+    assert C.chan_launches()[1] == b1
     named = dict(zip([n for n, _ in model.named_parameters()], zip(g_c, g_s)))
     for name, (a, b) in named.items():
         conv_bias = name.startswith("layers.") and name.endswith(".bias") and \
