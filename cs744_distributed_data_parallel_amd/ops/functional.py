@@ -207,16 +207,19 @@ class _ConvBNAct(torch.autograd.Function):
             lo.clear()
         li = ctx.link_in
         prev = (None, None, False, False, 2)
-        chan = (False, None, None, None)
+        chan, claimed = (False, None, None, None), ()
         if li is not None and li.consumers == 1 and nig[0] and not park_dx and addend is None:
             prev = (li.y, li.stats, li.pool, li.relu, li.ps)
             if li.chan and _chan_on():
-                pg, pb, pbias = li.params
-                need = [t is not None and t.requires_grad for t in li.params]
-                dbs = _slot(pbias, need[2])
-                if need[2] and dbs is None:
-                    dbs = torch.empty_like(pbias)
-                chan = (True, _slot(pg, need[0]), _slot(pb, need[1]), dbs)
+                # block L's gradient slots, claimed before it is known whether the native side takes
+                # the hand-off (it decides by the map size); given back below if it does not
+                slots = [_slot(t, t is not None and t.requires_grad) for t in li.params]
+                claimed = [t for t, v in zip(li.params, slots) if v is not None]
+                pbias = li.params[2]
+                dbs = slots[2]
+                if dbs is None and pbias is not None and pbias.requires_grad:
+                    dbs = torch.empty_like(pbias)  # (the kernel needs somewhere to write the bias gradient)
+                chan = (True, slots[0], slots[1], dbs)
         (dx, dw, db, dgamma, dbeta, dres, prev_part, prev_dy, prev_dy_amax, pdg, pdb,
          pdbias) = C.conv_bn_act_bwd(
             gout, x, w, y, stats, stride, pad, pool, relu, nig[0], has_bias, zout, training,
@@ -233,6 +236,8 @@ class _ConvBNAct(torch.autograd.Function):
             if prev_dy is not None and dx is not None:
                 li.dy, li.dy_amax, li.grads = prev_dy, prev_dy_amax, (pdg, pdb, pdbias)
             else:
+                for t in claimed:  # no hand-off (map too large): block L claims its own slots
+                    t._cdp_arena.unclaim(t)
                 li.part = prev_part if (prev_part is not None and dx is not None) else None
             got = li.dy is not None or li.part is not None
             li.gptr = dx.data_ptr() if got else None

@@ -98,11 +98,13 @@ __global__ __launch_bounds__(256) void bwd_reduce_kernel(BwdReduceArgs a) {
         s.w += ((t[i][0].w + t[i][1].w) + (t[i][2].w + t[i][3].w)) + ((t[i][4].w + t[i][5].w) + (t[i][6].w + t[i][7].w));
       }
     }
+    // (one "slab" that is dX itself, read in place: nothing to write back)
+    const bool in_place = a.d_slab == a.d_y && !a.d_addend;
 #pragma unroll
     for (int i = 0; i < RBD / 16; ++i) {
       const int m = y0 + rl + 16 * i;
       float4 s = g[i];
-      if (m < a.d_M && nok) {
+      if (m < a.d_M && nok && !in_place) {
         const long long o = (long long)m * C + n;
         if (a.d_addend) {
           const float4 ad = ld4(a.d_addend + o);

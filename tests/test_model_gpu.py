@@ -370,3 +370,26 @@ def test_vgg11_chan_fusion_matches_unfused(monkeypatch, batch):
             continue
         err = ((a - b).norm() / b.norm().clamp_min(1e-30)).item()
         assert err < 1e-5, (name, err)
+
+
+@pytest.mark.parametrize("batch", [32, 256])
+def test_vgg11_every_gradient_lands_in_its_arena_slot(batch):
+    """After zero_grad(set_to_none), every gradient of a VGG-11 step is written straight into its
+    flat-arena slot and adopted by autograd (FlatArena.claim), including the gamma / beta / bias
+    gradients a consumer block writes for its producer (channel-owner hand-off) and the slots it
+    claims and gives back when the hand-off is not taken: no copy into the arena before SGD."""
+    import cs744_distributed_data_parallel_amd as cdp
+
+    torch.manual_seed(0)
+    model = cdp.VGG11().cuda()
+    opt = cdp.SGD(model.parameters(), lr=0.1, momentum=0.9, weight_decay=1e-4)
+    crit = cdp.CrossEntropyLoss()
+    x = torch.randn(batch, 3, 32, 32, device="cuda").contiguous(memory_format=torch.channels_last)
+    t = torch.randint(0, 10, (batch,), device="cuda")
+    for _ in range(2):
+        opt.zero_grad()
+        crit(model(x), t).backward()
+        views = opt._arena.grad_views()
+        bad = [n for n, p in model.named_parameters() if p.grad.data_ptr() != views[p._cdp_index].data_ptr()]
+        assert not bad, bad
+        opt.step()
