@@ -23,8 +23,7 @@ EXT_SUFFIX = sysconfig.get_config_var("EXT_SUFFIX") or ".so"
 OUTPUT = os.path.join(PKG_DIR, "_C" + EXT_SUFFIX)
 
 KERNELS = ["conv_igemm.hip", "conv_x3.hip", "wgrad.hip", "bn.hip", "misc.hip", "stem.hip", "bwd_fuse.hip", "bwd_pair.hip",
-           "bwd_pair_d128x128.hip", "bwd_pair_d128x64.hip", "bwd_pair_d64x128.hip", "bwd_pair_d64x64.hip",
-           "chan_fuse.hip"]
+           "bwd_pair_d128x128.hip", "bwd_pair_d128x64.hip", "bwd_pair_d64x128.hip", "bwd_pair_d64x64.hip"]
 RUNTIME = ["ops.cpp", "rccl_comm.cpp", "reducer.cpp", "torch_ops.cpp", "bindings.cpp"]
 
 

@@ -118,27 +118,14 @@ class _BNLink:
     statistics pass. ``gptr`` / ``gver`` pin the hand-off to that exact gradient tensor, unmodified
     (autograd accumulating a second consumer's gradient into it in place bumps its version), and
     ``consumers`` counts the fused blocks that read the tagged output: with two, neither takes the
-    link and the producer reduces its own statistics.
+    link and the producer reduces its own statistics."""
 
-    ``chan`` (training-mode BN, not the RGB stem): on a small map block L+1's backward runs block L's
-    whole BatchNorm backward in its reduction launch (csrc/kernels/chan_fuse.hip) and hands over
-    ``dy`` (the gradient at block L's conv output), its f16x2 maxima and the gamma / beta / bias
-    gradients (``grads``, written straight into block L's arena slots when free), instead of
-    ``part``; block L's backward then runs only its two GEMMs."""
+    __slots__ = ("y", "stats", "pool", "relu", "ps", "part", "gptr", "gver", "consumers")
 
-    __slots__ = ("y", "stats", "pool", "relu", "ps", "part", "gptr", "gver", "consumers", "chan", "params", "dy",
-                 "dy_amax", "grads")
-
-    def __init__(self, y, stats, pool, relu, ps, chan=False, params=(None, None, None)):
+    def __init__(self, y, stats, pool, relu, ps):
         self.y, self.stats, self.pool, self.relu, self.ps = y, stats, pool, relu, ps
         self.part, self.gptr, self.gver = None, None, None
         self.consumers = 0
-        self.chan, self.params = chan, params
-        self.dy = self.dy_amax = self.grads = None
-
-    def clear(self):
-        self.part = self.gptr = self.gver = None
-        self.dy = self.dy_amax = self.grads = None
 
 
 LINK_HANDOFFS = [0]  # BN statistics reductions taken from the consumer block's backward (tests read it)
@@ -176,8 +163,7 @@ class _ConvBNAct(torch.autograd.Function):
         if bn_link and residual is None and _bwd_fuse_on():
             odd_pool = pool and (y.shape[2] % 2 == 1 or y.shape[3] % 2 == 1)
             ps = 3 if (b is not None and not odd_pool and training) else 2  # as conv_bn_act_bwd's
-            chan = training and x.shape[1] > 4 and _chan_on()  # (the RGB stem's backward needs gout itself)
-            ctx.link_out = _BNLink(y, stats, pool, relu, ps, chan, (gamma, beta, b))
+            ctx.link_out = _BNLink(y, stats, pool, relu, ps)
             out._cdp_bnlink = (ctx.link_out, out._version)
         return out
 
@@ -195,53 +181,27 @@ class _ConvBNAct(torch.autograd.Function):
                 park_dx = True
             else:
                 addend, dx_sink.grad = dx_sink.grad, None
-        part_in, dy_in, dy_amax_in, lgrads, lo = None, None, None, None, ctx.link_out
+        part_in, lo = None, ctx.link_out
         if lo is not None:
-            if lo.consumers == 1 and lo.gptr == gout.data_ptr() and lo.gver == gout._version:
-                if lo.dy is not None:
-                    dy_in, dy_amax_in, lgrads = lo.dy, lo.dy_amax, lo.grads
-                    LINK_HANDOFFS[0] += 1
-                elif lo.part is not None:
-                    part_in = lo.part
-                    LINK_HANDOFFS[0] += 1
-            lo.clear()
+            if (lo.part is not None and lo.consumers == 1 and lo.gptr == gout.data_ptr()
+                    and lo.gver == gout._version):
+                part_in = lo.part
+                LINK_HANDOFFS[0] += 1
+            lo.part = lo.gptr = lo.gver = None
         li = ctx.link_in
         prev = (None, None, False, False, 2)
-        chan, claimed = (False, None, None, None), ()
         if li is not None and li.consumers == 1 and nig[0] and not park_dx and addend is None:
             prev = (li.y, li.stats, li.pool, li.relu, li.ps)
-            if li.chan and _chan_on():
-                # block L's gradient slots, claimed before it is known whether the native side takes
-                # the hand-off (it decides by the map size); given back below if it does not
-                slots = [_slot(t, t is not None and t.requires_grad) for t in li.params]
-                claimed = [t for t, v in zip(li.params, slots) if v is not None]
-                pbias = li.params[2]
-                dbs = slots[2]
-                if dbs is None and pbias is not None and pbias.requires_grad:
-                    dbs = torch.empty_like(pbias)  # (the kernel needs somewhere to write the bias gradient)
-                chan = (True, slots[0], slots[1], dbs)
-        (dx, dw, db, dgamma, dbeta, dres, prev_part, prev_dy, prev_dy_amax, pdg, pdb,
-         pdbias) = C.conv_bn_act_bwd(
+        dx, dw, db, dgamma, dbeta, dres, prev_part = C.conv_bn_act_bwd(
             gout, x, w, y, stats, stride, pad, pool, relu, nig[0], has_bias, zout, training,
-            _slot(wp, nig[1]),
-            None if dy_in is not None else _slot(bp, nig[2] and has_bias),
-            None if dy_in is not None else _slot(gp, nig[3]),
-            None if dy_in is not None else _slot(betap, nig[4]), addend,
-            *ctx.amax, ctx.w_t, part_in, *prev, bp, dy_in, dy_amax_in, *chan,
+            _slot(wp, nig[1]), _slot(bp, nig[2] and has_bias), _slot(gp, nig[3]), _slot(betap, nig[4]), addend,
+            *ctx.amax, ctx.w_t, part_in, *prev, bp,
         )
-        if lgrads is not None:
-            dgamma, dbeta, db = lgrads
         ctx.w_t = None
         if li is not None:
-            if prev_dy is not None and dx is not None:
-                li.dy, li.dy_amax, li.grads = prev_dy, prev_dy_amax, (pdg, pdb, pdbias)
-            else:
-                for t in claimed:  # no hand-off (map too large): block L claims its own slots
-                    t._cdp_arena.unclaim(t)
-                li.part = prev_part if (prev_part is not None and dx is not None) else None
-            got = li.dy is not None or li.part is not None
-            li.gptr = dx.data_ptr() if got else None
-            li.gver = dx._version if got else None
+            li.part = prev_part if (prev_part is not None and dx is not None) else None
+            li.gptr = dx.data_ptr() if li.part is not None else None
+            li.gver = dx._version if li.part is not None else None
             ctx.link_in = None
         if park_dx:
             dx_sink.grad, dx = dx, None
@@ -267,13 +227,6 @@ def _bwd_fuse_on() -> bool:
     import os
 
     return os.environ.get("CDP_BWD_FUSE", "1") != "0"
-
-
-def _chan_on() -> bool:
-    """CDP_CHAN=0: no channel-owner hand-off of a block's BN backward (A/B; read per forward)."""
-    import os
-
-    return os.environ.get("CDP_CHAN", "1") != "0"
 
 
 def conv_bn_act(x, conv, bn, relu: bool = True, pool: bool = False, residual=None, res_sink=None, dx_sink=None,

@@ -103,10 +103,6 @@ class FlatArena:
         self.claimed[i] = True
         return _view_like(self.grad, self.offsets[i], p.data)
 
-    def unclaim(self, p):
-        """Give back a slot claimed for a kernel that ended up not writing it (a speculative claim)."""
-        self.claimed[p._cdp_index] = False
-
     def reset_claims(self):
         self.claimed = [False] * len(self.params)
 

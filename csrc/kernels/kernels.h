@@ -166,54 +166,6 @@ struct BwdReduceArgs {
 void bwd_reduce_launch(BwdReduceArgs a, hipStream_t st);
 int bwd_reduce_rows_per_part();
 
-// chan_fuse.hip: channel-owner fusion of a split-K reduction with the training-mode BatchNorm around
-// it, for layers with few rows (see the file header). One block per 16 channels.
-struct ChanFwdArgs {
-  const float* slab;  // [S][M][C] split-K slabs of the conv output, M = N*H*W
-  int S;
-  const float* bias;  // conv bias [C] or nullptr
-  float* y;           // conv output (saved for backward) [M][C]
-  float* out;         // [N][Ho][Wo][C]
-  float* stats;       // [4][C] = (mean, invstd, scale, shift)
-  const float* gamma;
-  const float* beta;
-  float* running_mean;
-  float* running_var;
-  long long* nbt;
-  float momentum, eps;
-  float* amax_part;  // optional, chan_amax_parts(C) entries: |max| of out per block
-  int N, H, W, C, pool, relu;
-};
-struct ChanBwdArgs {
-  // job D: dX = sum_z d_slab[z] ([N][H/2][W/2][C] under pooling), written to d_y unless d_y == d_slab
-  const float* d_slab;
-  int d_S;
-  float* d_y;
-  // the BatchNorm whose (pooled) activation dX is the gradient of: its saved conv output y
-  // [N][H][W][C] and stats [4][C]
-  const float* y;
-  const float* stats;
-  int N, H, W, C, pool, relu;
-  // outputs: dy [N][H][W][C], dbeta / dgamma / conv-bias gradient [C] (each optional), |max| of dy
-  float* dy;
-  float* gbeta;
-  float* ggamma;
-  float* gdb;
-  float* amax_part;  // optional, chan_amax_parts(C) entries
-  // job W: w_dst[i] = sum_z w_slab[z][i] over w_n4 float4s (optional)
-  const float4* w_slab;
-  float4* w_dst;
-  int w_S;
-  long long w_n4;
-  int nbd, w_cb;  // set by the launcher
-};
-// (N, H, W, C) fits one block per 16 channels (<= 2048 rows, CDP_CHAN_MAXROWS; CDP_CHAN=0 disables)
-// (bwd: the backward kernel's limits, which differ)
-bool chan_fwd_ok(int N, int H, int W, int C, bool pool, bool bwd = false);
-int chan_amax_parts(int C);
-void chan_fwd_launch(const ChanFwdArgs& a, hipStream_t st);
-void chan_bwd_launch(ChanBwdArgs a, hipStream_t st);
-
 // bn.hip
 int bn_bwd_grid(int N, int H, int W, int C, bool pool);
 void bn_finalize_launch(const float* part, int nparts, int rpp, int M, int C, const float* gamma, const float* beta,

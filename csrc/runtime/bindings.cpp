@@ -44,17 +44,10 @@ PYBIND11_MODULE(_C, m) {
         py::arg("dx_addend") = py::none(), py::arg("x_amax") = py::none(), py::arg("w_amax") = py::none(),
         py::arg("w_t") = py::none(), py::arg("part_in") = py::none(), py::arg("prev_y") = py::none(),
         py::arg("prev_stats") = py::none(), py::arg("prev_pool") = false, py::arg("prev_relu") = false,
-        py::arg("prev_ps") = 2, py::arg("bias") = py::none(), py::arg("dy_in") = py::none(),
-        py::arg("dy_amax_in") = py::none(), py::arg("prev_chan") = false, py::arg("prev_dgamma") = py::none(),
-        py::arg("prev_dbeta") = py::none(), py::arg("prev_db") = py::none(),
-        "fused block backward; returns (dx, dw, db, dgamma, dbeta, dres, prev_part, prev_dy, prev_dy_amax, "
-        "prev_dgamma, prev_dbeta, prev_db). prev_* describe the BN whose output is x: its statistics reduction is "
-        "then fused into this block's data-gradient reduction and returned as prev_part (undefined when not fused), "
-        "which that block's backward takes as part_in; with prev_chan and a small map, that BN's whole backward "
-        "runs in the same launch instead (prev_dy, its |max| partials and the gamma / beta / bias gradients, "
-        "written into prev_dgamma / prev_dbeta / prev_db when given), which that block's backward takes as dy_in / "
-        "dy_amax_in");
-  m.def("chan_launches", &chan_launches, "(forward, backward) channel-owner BN launches issued by this process");
+        py::arg("prev_ps") = 2, py::arg("bias") = py::none(),
+        "fused block backward; returns (dx, dw, db, dgamma, dbeta, dres, prev_part). prev_* describe the BN whose "
+        "output is x: its statistics reduction is then fused into this block's data-gradient reduction and returned "
+        "as prev_part (undefined when not fused), which that block's backward takes as part_in");
   m.def("weight_prep", &weight_prep, py::arg("weights"), py::arg("want_t"),
         "one launch per step: conv weights' |max| partials (f16x2; else empty) and W^T [Ci, KH*KW*Co] per weight "
         "with want_t (the data-gradient operand)");

@@ -17,7 +17,6 @@
 
 #include <algorithm>
 #include <array>
-#include <atomic>
 #include <cstdlib>
 #include <functional>
 #include <mutex>
@@ -679,16 +678,9 @@ std::string get_conv_gemm() {
 // ---------------------------------------------------------------- conv forward
 // Returns y (channels_last [N, Cout, P, Q]). When `part` is requested the per-tile BatchNorm
 // partials are returned in a second tensor [nparts, Cout, 2] together with rows-per-part.
-// channel-owner launches (chan_fuse.hip) issued so far: forward, backward (tests check the path is taken)
-std::atomic<long long> g_chan_fwd{0}, g_chan_bwd{0};
-std::vector<int64_t> chan_launches() { return {g_chan_fwd.load(), g_chan_bwd.load()}; }
-
-// slab_out (internal): when given and the plan splits K, the GEMM writes its fp32 split-K slabs
-// [S][M][Co] there and no reduction is launched (y is returned unwritten, for chan_fwd_launch)
-std::vector<at::Tensor> conv2d_fwd_impl(const at::Tensor& x_, const at::Tensor& w_,
-                                        const c10::optional<at::Tensor>& bias, int64_t stride, int64_t pad,
-                                        bool want_stats, const c10::optional<at::Tensor>& x_amax,
-                                        const c10::optional<at::Tensor>& w_amax, at::Tensor* slab_out) {
+std::vector<at::Tensor> conv2d_fwd(const at::Tensor& x_, const at::Tensor& w_, const c10::optional<at::Tensor>& bias,
+                                   int64_t stride, int64_t pad, bool want_stats, const c10::optional<at::Tensor>& x_amax,
+                                   const c10::optional<at::Tensor>& w_amax) {
   check_f32_cuda(x_, "x");
   check_f32_cuda(w_, "weight");
   TORCH_CHECK(x_.dim() == 4 && w_.dim() == 4, "conv2d_fwd expects 4-D input and weight");
@@ -726,24 +718,11 @@ std::vector<at::Tensor> conv2d_fwd_impl(const at::Tensor& x_, const at::Tensor& 
       part = at::empty({(M + rows_pp - 1) / rows_pp, Co, 2}, opts);
       return part.data_ptr<float>();
     };
-  if (slab_out && g.splits > 1) {
-    *slab_out = at::empty({g.splits, M, Co}, opts);
-    p.y = slab_out->data_ptr<float>();
-    p.bias = nullptr;
-    conv_launch(p, g.bm, g.bn, false, st);
-    return {y};
-  }
   std::vector<at::Tensor> keep;
   const int rb = conv_gemm_splitk(p, g, false, st, opts, keep, alloc_part);
   if (want_stats) rpp = at::full({1}, rb, opts.dtype(at::kInt).device(at::kCPU));
   if (want_stats) return {y, part, rpp};
   return {y};
-}
-
-std::vector<at::Tensor> conv2d_fwd(const at::Tensor& x_, const at::Tensor& w_, const c10::optional<at::Tensor>& bias,
-                                   int64_t stride, int64_t pad, bool want_stats, const c10::optional<at::Tensor>& x_amax,
-                                   const c10::optional<at::Tensor>& w_amax) {
-  return conv2d_fwd_impl(x_, w_, bias, stride, pad, want_stats, x_amax, w_amax, nullptr);
 }
 
 // ---------------------------------------------------------------- conv data gradient
@@ -1048,50 +1027,14 @@ std::vector<at::Tensor> conv_bn_act_fwd(const at::Tensor& x, const at::Tensor& w
   const at::Tensor xa = amax_parts(xin, pad_amax.defined() ? c10::optional<at::Tensor>(pad_amax) : x_amax,
                                    cur_stream());
   const at::Tensor wa = amax_parts(win, w_amax, cur_stream());
-  const bool has_res = residual.has_value() && residual->defined();
-  // few output rows and a split-K plan: one channel-owner launch reduces the slabs, finalizes the
-  // statistics and applies BN / ReLU / pool (chan_fuse.hip) instead of a reduction and a
-  // finalize + apply launch
-  const int Ho_ = (int)((x.size(2) + 2 * pad - w.size(2)) / stride + 1), Wo_ = (int)((x.size(3) + 2 * pad - w.size(3)) / stride + 1);
-  const bool chan = training && !has_res && momentum >= 0.0 && chan_fwd_ok((int)x.size(0), Ho_, Wo_, (int)w.size(0), pool);
-  at::Tensor slab;
-  std::vector<at::Tensor> r = conv2d_fwd_impl(xin, win, b, stride, pad, training, xa, wa, chan ? &slab : nullptr);
+  std::vector<at::Tensor> r = conv2d_fwd(xin, win, b, stride, pad, training, xa, wa);
   at::Tensor y = r[0];
   const int N = y.size(0), C = y.size(1), H = y.size(2), W = y.size(3);
   TORCH_CHECK(C % 4 == 0, "BatchNorm channel count must be a multiple of 4");
   auto opts = y.options();
   at::Tensor stats = at::empty({4, C}, opts);
   hipStream_t st = cur_stream();
-  if (slab.defined()) {
-    at::Tensor out = at::empty({N, C, pool ? H / 2 : H, pool ? W / 2 : W}, opts.memory_format(at::MemoryFormat::ChannelsLast));
-    at::Tensor out_amax;
-    if (f16x2_mode()) out_amax = at::empty({chan_amax_parts(C)}, opts);
-    ChanFwdArgs a{};
-    a.slab = slab.data_ptr<float>();
-    a.S = (int)slab.size(0);
-    a.bias = fptr(b);
-    a.y = y.data_ptr<float>();
-    a.out = out.data_ptr<float>();
-    a.stats = stats.data_ptr<float>();
-    a.gamma = fptr(gamma);
-    a.beta = fptr(beta);
-    a.running_mean = fptr_mut(running_mean);
-    a.running_var = fptr_mut(running_var);
-    if (num_batches_tracked.has_value() && num_batches_tracked->defined()) {
-      TORCH_CHECK(num_batches_tracked->scalar_type() == at::kLong, "num_batches_tracked must be int64");
-      a.nbt = reinterpret_cast<long long*>(num_batches_tracked->data_ptr<int64_t>());
-    }
-    a.momentum = (float)momentum;
-    a.eps = (float)eps;
-    a.amax_part = out_amax.defined() ? out_amax.data_ptr<float>() : nullptr;
-    a.N = N; a.H = H; a.W = W; a.C = C;
-    a.pool = pool ? 1 : 0;
-    a.relu = relu ? 1 : 0;
-    TORCH_CHECK((long long)a.S * N * H * W * C * 4 < (1LL << 31), "chan_fwd: slab too large");
-    chan_fwd_launch(a, st);
-    ++g_chan_fwd;
-    return {out, y, stats, xin, out_amax, xa, wa};
-  }
+  const bool has_res = residual.has_value() && residual->defined();
   // few statistics partials (the deep layers): finalize and apply in one launch (bn_fin_act_kernel)
   bool fused_fin = false;
   int nparts = 0, rpp = 0;
@@ -1153,12 +1096,7 @@ std::vector<at::Tensor> conv_bn_act_bwd(const at::Tensor& gout_, const at::Tenso
                                         const c10::optional<at::Tensor>& part_in,
                                         const c10::optional<at::Tensor>& prev_y,
                                         const c10::optional<at::Tensor>& prev_stats, bool prev_pool, bool prev_relu,
-                                        int64_t prev_ps, const c10::optional<at::Tensor>& bias,
-                                        const c10::optional<at::Tensor>& dy_in,
-                                        const c10::optional<at::Tensor>& dy_amax_in, bool prev_chan,
-                                        const c10::optional<at::Tensor>& prev_dgamma,
-                                        const c10::optional<at::Tensor>& prev_dbeta,
-                                        const c10::optional<at::Tensor>& prev_db) {
+                                        int64_t prev_ps, const c10::optional<at::Tensor>& bias) {
   check_f32_cuda(gout_, "grad_output");
   const at::Tensor gout = nhwc(gout_);
   const int N = y.size(0), C = y.size(1), H = y.size(2), W = y.size(3);
@@ -1170,13 +1108,6 @@ std::vector<at::Tensor> conv_bn_act_bwd(const at::Tensor& gout_, const at::Tenso
   };
   at::Tensor zout;
   if (zout_.has_value() && zout_->defined()) zout = nhwc(*zout_);
-  // this block's BN backward already done by the consumer block's chan_bwd launch (dy_in, and the
-  // gamma / beta / bias gradients it wrote into the slots the caller holds): only the GEMMs remain
-  const bool have_dy = dy_in.has_value() && dy_in->defined();
-  if (have_dy)
-    TORCH_CHECK(!zout.defined() && dy_in->is_contiguous(at::MemoryFormat::ChannelsLast) && dy_in->size(0) == N &&
-                    dy_in->size(1) == C && dy_in->size(2) == H && dy_in->size(3) == W,
-                "conv_bn_act_bwd: dy_in must be a channels_last [N, C, H, W] tensor (no residual)");
   const int nblk = bn_bwd_grid(N, H, W, C, pool);
   // The conv-bias gradient sum(dy) comes out of the finalize of the statistics reduction
   // (chan_finalize dbmode): in training mode from one extra partial, sum(xhat); in eval mode as
@@ -1188,8 +1119,7 @@ std::vector<at::Tensor> conv_bn_act_bwd(const at::Tensor& gout_, const at::Tenso
   // the statistics reduction: from the consumer block's fused backward reduction when it made it
   // (part_in, see prev_* below), else a launch of its own
   at::Tensor part;
-  if (have_dy) {
-  } else if (part_in.has_value() && part_in->defined()) {
+  if (part_in.has_value() && part_in->defined()) {
     part = *part_in;
     TORCH_CHECK(part.dim() == 3 && part.size(1) == C && part.size(2) == ps && !zout.defined(),
                 "conv_bn_act_bwd: part_in must be [nparts, C, ", ps, "] (no residual)");
@@ -1199,31 +1129,28 @@ std::vector<at::Tensor> conv_bn_act_bwd(const at::Tensor& gout_, const at::Tenso
                          part.data_ptr<float>(), nblk, N, H, W, C, pool, relu,
                          zout.defined() ? zout.data_ptr<float>() : nullptr, st, ps == 3);
   }
-  const int nparts = have_dy ? 0 : (int)part.size(0);
+  const int nparts = (int)part.size(0);
   at::Tensor sums = at::empty({2, C}, opts);
   // gradients go straight into the caller's slots (flat-arena views) when provided
-  at::Tensor dgamma, dbeta, db;
-  if (!have_dy) {
-    dgamma = slot(dgamma_out, {C}, false);
-    dbeta = slot(dbeta_out, {C}, false);
-    if (has_bias) db = slot(db_out, {C}, false);
-  }
+  at::Tensor dgamma = slot(dgamma_out, {C}, false), dbeta = slot(dbeta_out, {C}, false);
+  at::Tensor db;
+  if (has_bias) db = slot(db_out, {C}, false);
   // eval-mode BatchNorm is a fixed affine map: dy = scale * dz (no batch-statistics terms)
   const int dbmode = fused_db ? (training ? 1 : 2) : 0;
   // RGB stem without an input gradient (VGG layer 0): the weight-gradient kernel applies the
   // BN / ReLU / pool backward on the fly, so dy is never materialised (stem.hip)
   const int cin = (int)x.size(1);
-  const bool stem_path = !have_dy && stem_enabled() && !need_dx && training && pool && relu && !zout.defined() && fused_db &&
+  const bool stem_path = stem_enabled() && !need_dx && training && pool && relu && !zout.defined() && fused_db &&
                          C == 64 && stem_ok(cin, (int)w.size(2), (int)w.size(3), stride, pad, C) &&
                          cin == (int)w.size(1) && (H % 2) == 0 && (W % 2) == 0;
   // few statistics partials (the deep layers): finalize and apply in one launch (bn_bwd_fin_apply_kernel)
-  const bool fused_fin = !have_dy && bn_fin_enabled(true) && training && !stem_path && !zout.defined() &&
-                         (!has_bias || fused_db) && bn_bwd_fin_apply_ok(nparts, C, H, W, pool);
-  if (!fused_fin && !have_dy)
+  const bool fused_fin = bn_fin_enabled(true) && training && !stem_path && !zout.defined() && (!has_bias || fused_db) &&
+                         bn_bwd_fin_apply_ok(nparts, C, H, W, pool);
+  if (!fused_fin)
     chan_finalize_launch(part.data_ptr<float>(), nparts, C, sums.data_ptr<float>(), dbeta.data_ptr<float>(),
                          dgamma.data_ptr<float>(), false, st, ps, fused_db ? db.data_ptr<float>() : nullptr,
                          stats.data_ptr<float>() + 2 * C, (long long)N * H * W, dbmode);
-  if (!training && dbmode != 2 && !have_dy) sums.zero_();
+  if (!training && dbmode != 2) sums.zero_();
   if (stem_path) {
     const at::Tensor xin = nhwc(x);
     const int nb = stem_wgrad_blocks(N, H, W);
@@ -1235,23 +1162,17 @@ std::vector<at::Tensor> conv_bn_act_bwd(const at::Tensor& gout_, const at::Tenso
                         : at::empty({C, cin, w.size(2), w.size(3)}, opts.memory_format(at::MemoryFormat::ChannelsLast));
     TORCH_CHECK(dw.is_contiguous(at::MemoryFormat::ChannelsLast), "stem dW slot must be channels_last");
     slab_sum_strided_launch(slab.data_ptr<float>(), nb, (long long)C * 36, 4, cin, dw.data_ptr<float>(), false, st);
-    return {at::Tensor(), dw, db, dgamma, dbeta, at::Tensor(), at::Tensor(), at::Tensor(), at::Tensor(), at::Tensor(),
-            at::Tensor(), at::Tensor()};
+    return {at::Tensor(), dw, db, dgamma, dbeta, at::Tensor(), at::Tensor()};
   }
-  at::Tensor dy = have_dy ? *dy_in : at::empty({N, C, H, W}, opts.memory_format(at::MemoryFormat::ChannelsLast));
+  at::Tensor dy = at::empty({N, C, H, W}, opts.memory_format(at::MemoryFormat::ChannelsLast));
   at::Tensor dbpart;
-  const bool sep_db = has_bias && !fused_db && !have_dy;
+  const bool sep_db = has_bias && !fused_db;
   if (sep_db) dbpart = at::empty({nblk, C, 2}, opts);
   at::Tensor dres;
   if (zout.defined()) dres = at::empty({N, C, H, W}, opts.memory_format(at::MemoryFormat::ChannelsLast));
   at::Tensor dy_amax;  // dy's |max| partials: operand scale of both gradient GEMMs (f16x2)
-  if (have_dy) {
-    if (dy_amax_in.has_value() && dy_amax_in->defined()) dy_amax = *dy_amax_in;
-  } else if (f16x2_mode()) {
-    dy_amax = at::empty({fused_fin ? bn_fin_act_grid(N, H, W, C, pool) : nblk}, opts);
-  }
-  if (have_dy) {
-  } else if (fused_fin)
+  if (f16x2_mode()) dy_amax = at::empty({fused_fin ? bn_fin_act_grid(N, H, W, C, pool) : nblk}, opts);
+  if (fused_fin)
     bn_bwd_fin_apply_launch(part.data_ptr<float>(), nparts, ps, y.data_ptr<float>(), gout.data_ptr<float>(),
                             stats.data_ptr<float>(), dy.data_ptr<float>(), dbeta.data_ptr<float>(),
                             dgamma.data_ptr<float>(), has_bias ? db.data_ptr<float>() : nullptr, N, H, W, C, pool,
@@ -1296,58 +1217,8 @@ std::vector<at::Tensor> conv_bn_act_bwd(const at::Tensor& gout_, const at::Tenso
     }
   }
   pend.flush(st);  // no data-gradient GEMM took it: launch the weight gradient alone
-  at::Tensor prev_part, prev_dy, prev_dy_amax, pdg, pdb, pdbias;
-  // the previous block's whole BN backward in this block's reduction launch (chan_fuse.hip): one
-  // block per channel quad of dX when its map is small enough
-  bool chan = false;
-  if (dr.d_on && has_prev && prev_chan && !(dx_addend.has_value() && dx_addend->defined())) {
-    const at::Tensor py = nhwc(*prev_y);
-    const int pN = py.size(0), pC = py.size(1), pH = py.size(2), pW = py.size(3);
-    chan = chan_fwd_ok(pN, pH, pW, pC, prev_pool, true) && dr.d_Nout == pC &&
-           (long long)dr.d_S * dr.d_M * pC * 4 < (1LL << 31) &&
-           (long long)dr.d_M == (long long)pN * (prev_pool ? (pH / 2) * (pW / 2) : pH * pW);
-    if (chan) {
-      TORCH_CHECK(pN == x.size(0) && pC == x.size(1) &&
-                      (prev_pool ? (pH / 2 == x.size(2) && pW / 2 == x.size(3)) : (pH == x.size(2) && pW == x.size(3))) &&
-                      prev_stats->numel() == 4 * pC,
-                  "conv_bn_act_bwd: prev_y / prev_stats do not describe the BN that produced x");
-      auto pslot = [&](const c10::optional<at::Tensor>& o) {
-        if (o.has_value() && o->defined()) {
-          TORCH_CHECK(o->numel() == pC && o->is_contiguous(), "conv_bn_act_bwd: prev gradient slot must be [C]");
-          return *o;
-        }
-        return at::empty({pC}, opts);
-      };
-      pdg = pslot(prev_dgamma);
-      pdb = pslot(prev_dbeta);
-      if (prev_db.has_value() && prev_db->defined()) pdbias = pslot(prev_db);
-      prev_dy = at::empty({pN, pC, pH, pW}, opts.memory_format(at::MemoryFormat::ChannelsLast));
-      if (f16x2_mode()) prev_dy_amax = at::empty({chan_amax_parts(pC)}, opts);
-      ChanBwdArgs a{};
-      a.d_slab = dr.d_src;
-      a.d_S = dr.d_S;
-      a.d_y = dr.d_y;
-      a.y = py.data_ptr<float>();
-      a.stats = prev_stats->data_ptr<float>();
-      a.N = pN; a.H = pH; a.W = pW; a.C = pC;
-      a.pool = prev_pool ? 1 : 0;
-      a.relu = prev_relu ? 1 : 0;
-      a.dy = prev_dy.data_ptr<float>();
-      a.gbeta = pdb.data_ptr<float>();
-      a.ggamma = pdg.data_ptr<float>();
-      a.gdb = pdbias.defined() ? pdbias.data_ptr<float>() : nullptr;
-      a.amax_part = prev_dy_amax.defined() ? prev_dy_amax.data_ptr<float>() : nullptr;
-      if (dr.w_slab.defined()) {
-        a.w_slab = reinterpret_cast<const float4*>(dr.w_slab.data_ptr<float>());
-        a.w_dst = reinterpret_cast<float4*>(dr.w_dst);
-        a.w_S = dr.w_S;
-        a.w_n4 = dr.w_n / 4;
-      }
-      chan_bwd_launch(a, st);
-      ++g_chan_bwd;
-    }
-  }
-  if (!chan && (dr.w_slab.defined() || dr.d_on)) {
+  at::Tensor prev_part;
+  if (dr.w_slab.defined() || dr.d_on) {
     BwdReduceArgs a{};
     if (dr.d_on) {
       a.d_slab = dr.d_src;
@@ -1385,7 +1256,7 @@ std::vector<at::Tensor> conv_bn_act_bwd(const at::Tensor& gout_, const at::Tenso
     }
     bwd_reduce_launch(a, st);
   }
-  return {dx, dw, db, dgamma, dbeta, dres, prev_part, prev_dy, prev_dy_amax, pdg, pdb, pdbias};
+  return {dx, dw, db, dgamma, dbeta, dres, prev_part};
 }
 
 // ---------------------------------------------------------------- linear

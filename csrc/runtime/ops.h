@@ -56,14 +56,7 @@ std::vector<at::Tensor> conv_bn_act_bwd(const at::Tensor& gout, const at::Tensor
                                         const c10::optional<at::Tensor>& prev_y = c10::nullopt,
                                         const c10::optional<at::Tensor>& prev_stats = c10::nullopt,
                                         bool prev_pool = false, bool prev_relu = false, int64_t prev_ps = 2,
-                                        const c10::optional<at::Tensor>& bias = c10::nullopt,
-                                        const c10::optional<at::Tensor>& dy_in = c10::nullopt,
-                                        const c10::optional<at::Tensor>& dy_amax_in = c10::nullopt,
-                                        bool prev_chan = false,
-                                        const c10::optional<at::Tensor>& prev_dgamma = c10::nullopt,
-                                        const c10::optional<at::Tensor>& prev_dbeta = c10::nullopt,
-                                        const c10::optional<at::Tensor>& prev_db = c10::nullopt);
-std::vector<int64_t> chan_launches();
+                                        const c10::optional<at::Tensor>& bias = c10::nullopt);
 at::Tensor linear_fwd(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tensor>& b);
 std::vector<at::Tensor> linear_bwd(const at::Tensor& gy, const at::Tensor& x, const at::Tensor& w, bool need_dx,
                                    bool has_bias, const c10::optional<at::Tensor>& dw_out,

@@ -505,59 +505,3 @@ def test_weight_prep_transposes_and_maxima():
     b = C().conv2d_dgrad(cl(gy), w, [2, 512, 8, 8], 1, 1, None, None, None, wts[2])
     assert torch.equal(a, b)
     del x
-
-
-@pytest.mark.parametrize("pool", [False, True])
-@pytest.mark.parametrize("N", [2, 8, 32])
-def test_linked_chain_channel_owner_matches_torch(monkeypatch, pool, N):
-    """Two chained blocks A -> B (A's output feeds only B, bn_link) on a small map: B's backward runs
-    A's whole BatchNorm backward in its reduction launch (chan_fuse.hip: one block per channel
-    quad) and A's backward only its GEMMs; the forward BN of both blocks runs in the channel-owner
-    forward launch. Every gradient and running statistic against fp64 torch."""
-    import cs744_distributed_data_parallel_amd as cdp
-    from cs744_distributed_data_parallel_amd.ops import functional as CF
-
-    C = cdp._native.lib()
-    # every row count the kernels support (1-16 rows per lane), not only the defaults' (<= 4)
-    monkeypatch.setenv("CDP_CHAN_FWD_RT", "16")
-    monkeypatch.setenv("CDP_CHAN_BWD_RT", "16")
-    torch.manual_seed(4)
-    convs = [torch.nn.Conv2d(64, 128, 3, 1, 1).cuda(), torch.nn.Conv2d(128, 128, 3, 1, 1).cuda()]
-    bns = [torch.nn.BatchNorm2d(128).cuda(), torch.nn.BatchNorm2d(128).cuda()]
-    with torch.no_grad():
-        for bn in bns:
-            bn.weight.uniform_(0.5, 1.5)
-            bn.bias.uniform_(-0.5, 0.5)
-    convs_r = [torch.nn.Conv2d(64, 128, 3, 1, 1).double(), torch.nn.Conv2d(128, 128, 3, 1, 1).double()]
-    bns_r = [torch.nn.BatchNorm2d(128).double(), torch.nn.BatchNorm2d(128).double()]
-    for a, b in zip(convs + bns, convs_r + bns_r):
-        b.load_state_dict(a.state_dict())
-    for c in convs:
-        c.weight.data = cl(c.weight.data)
-    x = torch.randn(N, 64, 8, 8, device="cuda")
-    xn = cl(x).requires_grad_()
-    f0, b0 = C.chan_launches()
-    h = CF.conv_bn_act(xn, convs[0], bns[0], relu=True, pool=pool, bn_link=True)
-    out = CF.conv_bn_act(h, convs[1], bns[1], relu=True, pool=True)
-    g = torch.randn_like(out)
-    out.backward(g)
-    torch.cuda.synchronize()
-    f1, b1 = C.chan_launches()
-    assert b1 - b0 == 1, (f1 - f0, b1 - b0)  # (the forward GEMMs may plan no split-K)
-    xr = x.double().cpu().requires_grad_()
-    hr = F.relu(bns_r[0](convs_r[0](xr)))
-    if pool:
-        hr = F.max_pool2d(hr, 2, 2)
-    ref = F.max_pool2d(F.relu(bns_r[1](convs_r[1](hr))), 2, 2)
-    ref.backward(g.double().cpu())
-    assert rel_err(out, ref) < 5e-5
-    assert rel_err(xn.grad, xr.grad) < 5e-4
-    for a, b in zip(convs + bns, convs_r + bns_r):
-        assert rel_err(a.weight.grad, b.weight.grad) < 5e-4
-    for a, b in zip(bns, bns_r):
-        assert rel_err(a.bias.grad, b.bias.grad) < 5e-4
-        assert rel_err(a.running_mean, b.running_mean) < 1e-5
-        assert rel_err(a.running_var, b.running_var) < 1e-5
-    for a, b, bn in zip(convs, convs_r, bns_r):  # conv bias before training BN: analytically zero
-        assert (a.bias.grad.double().cpu() - b.bias.grad).abs().max().item() < 1e-3 * (
-            bn.bias.grad.abs().max().item())
