@@ -223,6 +223,9 @@ void wtrans_sub_launch(const float* w, float* wt, int Co, int KH, int KW, int Ci
 // NHWC channel padding C (<= 4) -> 4 with zeros; amax_part (optional, pad_c4_grid entries): per-block |max|
 int pad_c4_grid(long long npix);
 void pad_c4_launch(const float* x, long long npix, int C, float* out, float* amax_part, hipStream_t st);
+// dst = mean of k <= kMaxStackSrcs tensors; srcs is a HOST array (the pointers travel in the kernel
+// arguments: no pointer-table upload, so nothing can race with a host buffer's lifetime)
+constexpr int kMaxStackSrcs = 128;
 void stack_mean_launch(const float* const* srcs, int k, long long n, float* dst, hipStream_t st);
 void scale_launch(float* x, long long n, float a, hipStream_t st);
 void delay_scale_launch(float* x, long long n, float a, double delay_us, hipStream_t st);

@@ -323,12 +323,14 @@ __global__ __launch_bounds__(256) void pad_c4_kernel(const float* __restrict__ x
 }
 
 // ------------------------------------------------------------------ stack mean / scale / colsum
-__global__ __launch_bounds__(256) void stack_mean_kernel(const float* const* __restrict__ srcs, int k, long long n,
-                                                         float* __restrict__ dst) {
+struct StackSrcs {
+  const float* p[kMaxStackSrcs];
+};
+__global__ __launch_bounds__(256) void stack_mean_kernel(StackSrcs srcs, int k, long long n, float* __restrict__ dst) {
   const float inv = 1.f / (float)k;
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
     float s = 0.f;
-    for (int j = 0; j < k; ++j) s += srcs[j][i];
+    for (int j = 0; j < k; ++j) s += srcs.p[j][i];
     dst[i] = s * inv;
   }
 }
@@ -612,7 +614,10 @@ void pad_c4_launch(const float* x, long long npix, int C, float* out, float* ama
   hipLaunchKernelGGL(pad_c4_kernel, dim3(pad_c4_grid(npix)), dim3(256), 0, st, x, npix, C, out, amax_part);
 }
 void stack_mean_launch(const float* const* srcs, int k, long long n, float* dst, hipStream_t st) {
-  hipLaunchKernelGGL(stack_mean_kernel, dim3(grid_for(n)), dim3(256), 0, st, srcs, k, n, dst);
+  StackSrcs a{};
+  for (int j = 0; j < k && j < kMaxStackSrcs; ++j) a.p[j] = srcs[j];
+  hipLaunchKernelGGL(stack_mean_kernel, dim3(grid_for(n)), dim3(256), 0, st, a, k < kMaxStackSrcs ? k : kMaxStackSrcs, n,
+                     dst);
 }
 // Test-only post-op (RcclComm::set_test_postop): every wave first idles ~delay_us with s_sleep
 // (no memory traffic), then scales. Used to prove that consumers wait on the collective's event.

@@ -1448,14 +1448,18 @@ void counter_inc(at::Tensor c) { counter_inc_launch(reinterpret_cast<long long*>
 void stack_mean(const std::vector<at::Tensor>& srcs, at::Tensor dst) {
   TORCH_CHECK(!srcs.empty(), "stack_mean: empty list");
   const int k = srcs.size();
-  std::vector<int64_t> ptrs(k);
+  TORCH_CHECK(k <= kMaxStackSrcs, "stack_mean: at most ", kMaxStackSrcs, " tensors");
+  // The pointers go in the kernel arguments. (They used to be uploaded as a device table by a
+  // non-blocking copy from a temporary pageable host tensor, freed when the statement ended: now
+  // and then the copy read reused host memory and the mean read a stale buffer -- the gather /
+  // scatter strategy was not reproducible run to run.)
+  std::vector<const float*> ptrs(k);
   for (int i = 0; i < k; ++i) {
-    TORCH_CHECK(srcs[i].is_contiguous() && srcs[i].numel() == dst.numel(), "stack_mean: shape mismatch");
-    ptrs[i] = reinterpret_cast<int64_t>(srcs[i].data_ptr<float>());
+    TORCH_CHECK(srcs[i].is_contiguous() && srcs[i].numel() == dst.numel() && srcs[i].device() == dst.device(),
+                "stack_mean: shape / device mismatch");
+    ptrs[i] = srcs[i].data_ptr<float>();
   }
-  at::Tensor dptrs = at::tensor(ptrs, at::TensorOptions().dtype(at::kLong)).to(dst.device(), /*non_blocking=*/true);
-  stack_mean_launch(reinterpret_cast<const float* const*>(dptrs.data_ptr<int64_t>()), k, dst.numel(),
-                    dst.data_ptr<float>(), cur_stream());
+  stack_mean_launch(ptrs.data(), k, dst.numel(), dst.data_ptr<float>(), cur_stream());
 }
 
 void scale_(at::Tensor x, double a) {
