@@ -218,22 +218,40 @@ class TorchCommunicator(Communicator):
         w = tdist.reduce(t, dst, op=_TORCH_OPS[_norm_op(op)], group=self.group, async_op=async_op)
         return Work(torch_work=w) if async_op else None
 
-    def _gloo_device_fence(self, t):
-        # gloo on device tensors (the one-GPU multi-rank rehearsal): its host staging copies run on
-        # gloo's own streams; a device-wide sync around the blocking gather / scatter keeps the
-        # consumer kernels (stack_mean, SGD) from ever seeing a buffer before its copy lands
-        if t.is_cuda and tdist.get_backend(self.group) == "gloo":
-            torch.cuda.synchronize(t.device)
+    def _gloo_device(self, t) -> bool:
+        return t.is_cuda and tdist.get_backend(self.group) == "gloo"
 
+    # gloo on device tensors (the one-GPU multi-rank rehearsal; production GPU runs use the RCCL
+    # communicator): the gather / scatter are staged through host tensors here, with blocking copies.
+    # torch's own device-tensor path for these two collectives (host staging on gloo's streams) was
+    # not reproducible run to run on ROCm: two ranks training VGG-11 with the gather/scatter strategy
+    # differed after step 3 in 4 of 9 repeats (relative L2 up to 1e-4, step 1 always bitwise equal),
+    # even with a device-wide sync around every call; staged by hand, 9 of 9 repeats were bitwise
+    # equal (scripts/diag/gs_repeat.py, gs_repeat_cpu_staged.py). all_reduce / broadcast reproduce
+    # bitwise on the device path and keep it.
     def gather(self, t, gather_list=None, dst=0):
-        self._gloo_device_fence(t)
-        tdist.gather(t, gather_list if self.rank == dst else None, dst=dst, group=self.group)
-        self._gloo_device_fence(t)
+        if not self._gloo_device(t):
+            tdist.gather(t, gather_list if self.rank == dst else None, dst=dst, group=self.group)
+            return
+        torch.cuda.synchronize(t.device)
+        tc = t.cpu()
+        lst = [torch.empty_like(tc) for _ in range(self.size)] if self.rank == dst else None
+        tdist.gather(tc, lst, dst=dst, group=self.group)
+        if self.rank == dst:
+            for o, h in zip(gather_list, lst):
+                o.copy_(h)
+        torch.cuda.synchronize(t.device)
 
     def scatter(self, t, scatter_list=None, src=0):
-        self._gloo_device_fence(t)
-        tdist.scatter(t, scatter_list if self.rank == src else None, src=src, group=self.group)
-        self._gloo_device_fence(t)
+        if not self._gloo_device(t):
+            tdist.scatter(t, scatter_list if self.rank == src else None, src=src, group=self.group)
+            return
+        torch.cuda.synchronize(t.device)
+        tc = torch.empty(t.shape, dtype=t.dtype)
+        lst = [h.cpu() for h in scatter_list] if self.rank == src else None
+        tdist.scatter(tc, lst, src=src, group=self.group)
+        t.copy_(tc)
+        torch.cuda.synchronize(t.device)
 
     def all_gather(self, out, t, async_op=False):
         w = tdist.all_gather_into_tensor(out, t, group=self.group, async_op=async_op)
