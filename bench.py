@@ -56,6 +56,9 @@ def parse(argv=None):
                    help="fp32 (default, the reference's precision; conv GEMMs fp32-accurate via the f16x2 "
                         "split, or CDP_CONV_GEMM=x3|f32) or bf16 (conv GEMM operands rounded to bf16, fp32 "
                         "accumulation: the non-parity fast mode)")
+    p.add_argument("--global-batch", type=int, default=REF_GLOBAL_BATCH,
+                   help="global batch of the strong-scaling rule, int(global/N) per rank (the reference's 256, "
+                        "/root/reference/src/Part 2a/main.py:22)")
     p.add_argument("--bucket-cap-mb", type=float, default=None)
     p.add_argument("--dataset-size", type=int, default=50000)
     p.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
@@ -117,7 +120,7 @@ def launch(args) -> int:
 class _Run:
     """Builds model/optimizer/data for one (local batch, sync on/off) point and times it."""
 
-    def __init__(self, args, world, rank, dev, local_batch, sync_grads=True, model_name=None):
+    def __init__(self, args, world, rank, dev, local_batch, sync_grads=True, model_name=None, strategy=None):
         import torch
 
         import cs744_distributed_data_parallel_amd as cdp
@@ -142,7 +145,7 @@ class _Run:
             ds = synthetic_cifar10(size, seed=0, device=dev)
         sampler = DistributedSampler(ds, num_replicas=world, rank=rank) if world > 1 else None
         self.loader = DeviceLoader(ds, local_batch, sampler=sampler, shuffle=(world == 1), train=True)
-        strategy = args.strategy
+        self.strategy = strategy = strategy or args.strategy
         self.sync = None
         if args.backend == "native":
             model = cdp.get_model(model_name).to(dev)
@@ -175,7 +178,7 @@ class _Run:
     def body(self):
         import contextlib
 
-        cdp, strategy = self.cdp, self.args.strategy
+        cdp, strategy = self.cdp, self.strategy
         x, y = self.loader.batch(self.order, 0, self.local_batch, nbatches=self.nb)
         self.opt.zero_grad()
         nosync = (not self.sync_grads and self.world > 1 and hasattr(self.model, "no_sync"))
@@ -211,7 +214,7 @@ class _Run:
         # failing mid-capture would leave its peer blocked in the collective): eager steps
         # (a no-sync step of the per-tensor strategies has no collective in it: those are captured
         # under gloo too, which lets the one-GPU rehearsal exercise the capture agreement)
-        no_coll = not self.sync_grads and self.args.strategy in ("allreduce_blocking", "gather_scatter")
+        no_coll = not self.sync_grads and self.strategy in ("allreduce_blocking", "gather_scatter")
         if self.args.no_graph or not cuda or (self.args.dist_backend == "gloo" and not no_coll):
             return
         from cs744_distributed_data_parallel_amd import distributed as D
@@ -311,6 +314,24 @@ class _Run:
             dist.all_reduce(el_t, "max")  # the slowest rank defines the step
         return float(el_t.item()) / steps * 1e3
 
+    def replicas_identical(self, dist):
+        """True when every rank's parameters + momentum are bit-identical (None at one rank)."""
+        if self.world == 1:
+            return None
+        torch = self.torch
+        dg = self.replica_digest()
+        allg = [torch.empty_like(dg) for _ in range(self.world)]
+        dist.all_gather(allg, dg)
+        return all(torch.equal(allg[0].cpu(), a.cpu()) for a in allg)
+
+    def bucket_plan(self):
+        """The gradient buckets of this point's reducer in launch order (None without one)."""
+        red = getattr(self.model, "reducer", None) or getattr(self.sync, "reducer", None)
+        if red is None or not hasattr(red, "plan_summary"):
+            return None
+        mod = getattr(self.model, "module", self.model)
+        return red.plan_summary({id(p): n for n, p in mod.named_parameters()})
+
     def replica_digest(self):
         """Exact digest of this replica's training state: the int64 sum of the parameters' and the
         momentum buffers' fp32 bit patterns (order-independent, bit-exact) and their fp64 sum. DDP's
@@ -343,15 +364,51 @@ class _Run:
             self.sync = None
 
 
-def _measure(args, world, rank, dev, lb, dbg, dist, steps=None, warmup=None, **kw):
-    """ms/step of one more (local batch, model, sync) point, measured like the headline."""
+def _measure(args, world, rank, dev, lb, dbg, dist, steps=None, warmup=None, full=False, **kw):
+    """ms/step of one more (local batch, model, sync) point, measured like the headline. With
+    ``full``: (ms, hipgraph, replicas_identical, bucket plan)."""
     r = _Run(args, world, rank, dev, lb, **kw)
     r.prepare(args.warmup if warmup is None else warmup, dbg)
     ms = r.time(args.steps if steps is None else steps, dist)
     hg = r.graph is not None
+    rep = r.replicas_identical(dist) if full else None
+    plan = r.bucket_plan() if full else None
     r.release()
     del r
-    return ms, hg
+    return (ms, hg, rep, plan) if full else (ms, hg)
+
+
+# The reference's three multi-process stages and the hook-driven bucketed strategy, in the order
+# BASELINE.md lists them (its per-strategy rows map one-to-one onto these keys)
+STRATEGY_REF = {
+    "gather_scatter": "Part 2a: rank-0 gather -> mean -> scatter per parameter (src/Part 2a/main.py:117-127)",
+    "allreduce_blocking": "Part 2b: blocking per-tensor all_reduce(SUM) / W after backward (src/Part 2b/main.py:116-119)",
+    "bucketed_overlap": "backward-hook bucketed all-reduce overlapped with backward (BASELINE.json config #3)",
+    "ddp": "Part 3: DistributedDataParallel wrapper (src/Part 3/main.py:61)",
+}
+
+
+def _strategies_block(args, world, rank, dev, dbg, dist, lb, known=None):
+    """Every gradient-sync strategy at the reference's strong-scaling point (``lb`` = int(256 / W)
+    images per rank): ms/step, the sync time the step exposes (vs the same step without gradient
+    sync), ``scaling_eff`` = ms_no_sync / ms (1.0 = communication fully hidden) and whether the
+    replicas stayed bit-identical. ``known`` = {strategy: (ms, hg, rep, plan)} already measured."""
+    known = known or {}
+    ms0, hg0 = _measure(args, world, rank, dev, lb, dbg, dist, sync_grads=False)
+    out = {"local_batch": lb, "global_batch": lb * world,
+           "no_sync": {"ms_per_step": round(ms0, 4), "value": round(lb * world / ms0 * 1e3, 1), "hipgraph": hg0}}
+    for strat in STRATEGY_REF:
+        if strat in known:
+            ms, hg, rep, plan = known[strat]
+        else:
+            ms, hg, rep, plan = _measure(args, world, rank, dev, lb, dbg, dist, full=True, strategy=strat)
+        ent = {"reference": STRATEGY_REF[strat], "ms_per_step": round(ms, 4), "value": round(lb * world / ms * 1e3, 1),
+               "exposed_sync_ms": round(max(0.0, ms - ms0), 4), "scaling_eff": round(min(1.0, ms0 / ms), 4),
+               "replicas_identical": rep, "hipgraph": hg}
+        if plan is not None:
+            ent["buckets"] = plan
+        out[strat] = ent
+    return out
 
 
 def rank_main(args) -> int:
@@ -407,7 +464,7 @@ def rank_main(args) -> int:
     comm_kind = ("rccl-native" if dist.native_communicator() is not None else
                  ("gloo" if (cpu or args.dist_backend == "gloo") else "torch-nccl")) if world > 1 else "none"
 
-    strong_lb = max(1, REF_GLOBAL_BATCH // world)
+    strong_lb = max(1, args.global_batch // world)
     main_lb = args.local_batch if args.scaling == "weak" else strong_lb
 
     run = _Run(args, world, rank, dev, main_lb, sync_grads=True)
@@ -415,27 +472,33 @@ def rank_main(args) -> int:
     ms = run.time(args.steps, dist)
     hipgraph = run.graph is not None
     graph_collectives = run.graph_collectives
-    replicas_identical = None
-    if world > 1:
-        # every rank's parameters + momentum after the timed steps must be bit-identical
-        dg = run.replica_digest()
-        allg = [torch.empty_like(dg) for _ in range(world)]
-        dist.all_gather(allg, dg)
-        replicas_identical = all(torch.equal(allg[0].cpu(), a.cpu()) for a in allg)
+    # every rank's parameters + momentum after the timed steps must be bit-identical
+    replicas_identical = run.replicas_identical(dist)
+    bucket_plan = run.bucket_plan()
     run.release()
     del run
 
     extra = {}
+    if bucket_plan is not None:
+        extra["buckets"] = bucket_plan
     if world > 1 and not args.no_extra:
         ms_nosync, _ = _measure(args, world, rank, dev, main_lb, dbg, dist, sync_grads=False)
         extra["ms_per_step_no_sync"] = round(ms_nosync, 4)
         extra["exposed_comm_ms"] = round(max(0.0, ms - ms_nosync), 4)
-        other_lb = strong_lb if args.scaling == "weak" else args.local_batch
-        if other_lb != main_lb:
-            ms_o, _ = _measure(args, world, rank, dev, other_lb, dbg, dist)
-            key = "strong" if args.scaling == "weak" else "weak"
-            extra[key] = {"value": round(other_lb * world / ms_o * 1e3, 1), "ms_per_step": round(ms_o, 4),
-                          "global_batch": other_lb * world, "local_batch": other_lb}
+        # the reference's whole multi-process experiment: its four sync strategies at its own
+        # strong-scaling rule (global batch 256 split int(256 / W) per rank)
+        known = {args.strategy: (ms, hipgraph, replicas_identical, bucket_plan)} if main_lb == strong_lb else None
+        blk = _strategies_block(args, world, rank, dev, dbg, dist, strong_lb, known)
+        extra["strategies"] = blk
+        d = blk[args.strategy]
+        eff = {args.scaling: round(min(1.0, ms_nosync / ms), 4)}
+        if args.scaling == "weak":
+            extra["strong"] = {"value": d["value"], "ms_per_step": d["ms_per_step"], "global_batch": strong_lb * world,
+                               "local_batch": strong_lb, "strategy": args.strategy}
+            eff["strong"] = d["scaling_eff"]
+        # ms/step without gradient sync over ms/step with it (1.0 = communication fully hidden); the
+        # driver computes the across-N scaling efficiency from the per-N values itself
+        extra["scaling_eff"] = eff
 
     engine = "reference" if cpu else _conv_gemm_engine(args.backend)
     headline = (world == 1 and not args.no_extra and not cpu and args.backend == "native" and args.precision == "fp32"

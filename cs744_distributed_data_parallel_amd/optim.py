@@ -52,6 +52,7 @@ class SGD(Optimizer):
         self._arena = None
         self._lr_tensor = None
         self._steps = 0
+        self.fused_prep = True  # emit the next step's weight preparation from the step (one arena pass)
         all_params = [p for g in self.param_groups for p in g["params"]]
         if flat and all_params and all_params[0].is_cuda:
             self._arena = arena_for(all_params)
@@ -98,6 +99,8 @@ class SGD(Optimizer):
             params = [p for p in group["params"] if p.grad is not None]
             if not params:
                 continue
+            if self._arena is not None:
+                self._arena.prep_valid = None  # re-marked below only by a fused step
             if params[0].is_cuda and not _native.force_reference():
                 self._step_native(gi, group, params)
             else:
@@ -140,15 +143,14 @@ class SGD(Optimizer):
                 firsts = self._first_flags(params)
             if all(firsts) or not any(firsts):
                 s, e = rng
-                C.sgd_step(arena.data[s:e], arena.grad[s:e], mom[s:e], lr_t, lr, m, damp, wd, 1.0, nest, all(firsts),
-                           maxim)
+                self._flat_step(C, arena, s, e, mom[s:e], lr_t, lr, m, damp, wd, nest, all(firsts), maxim)
                 if all(firsts):
                     for p in params:
                         self.state[p]["momentum_buffer"] = mviews[p._cdp_index]
                 return
         elif rng is not None and m == 0.0:
             s, e = rng
-            C.sgd_step(arena.data[s:e], arena.grad[s:e], None, lr_t, lr, 0.0, damp, wd, 1.0, nest, True, maxim)
+            self._flat_step(C, arena, s, e, None, lr_t, lr, 0.0, damp, wd, nest, True, maxim)
             return
         # general path: one launch per parameter (non-arena / partial groups)
         for p in params:
@@ -174,6 +176,17 @@ class SGD(Optimizer):
                            wd, 1.0, nest, first, maxim)
             if m != 0.0:
                 st["momentum_buffer"] = buf
+
+    def _flat_step(self, C, arena, s, e, mom, lr_t, lr, m, damp, wd, nest, first, maxim):
+        """One launch over the arena range: plain SGD, or SGD that also writes the next forward's
+        weight |max| partials and W^T (FlatArena.prep_plan_for) when a model registered them."""
+        plan = arena.prep_plan_for(s, e) if self.fused_prep else None
+        if plan is None:
+            C.sgd_step(arena.data[s:e], arena.grad[s:e], mom, lr_t, lr, m, damp, wd, 1.0, nest, first, maxim)
+            return
+        C.sgd_step_prep(arena.data[s:e], arena.grad[s:e], mom, lr_t, lr, m, damp, wd, 1.0, nest, first, maxim,
+                        plan["desc"], plan["meta"], plan["amax"])
+        arena.prep_mark_valid()
 
     def _step_reference(self, group, params):
         lr, m, damp, wd = group["lr"], group["momentum"], group["dampening"], group["weight_decay"]

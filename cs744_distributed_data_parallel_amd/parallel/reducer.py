@@ -262,6 +262,25 @@ class GradReducer:
         es = self.arena.data.element_size()
         return [(e - s) * es for s, e in self.bucket_ranges]
 
+    def plan_summary(self, names=None) -> dict:
+        """The bucket plan in launch order (the order backward makes them ready and the comm stream
+        runs them): per bucket its bytes, tensor count and first / last parameter (``names`` maps
+        ``id(param)`` to a name; arena indices otherwise), plus the caps it was planned with."""
+        a = self.arena
+        es = a.data.element_size()
+        n = len(a.params)
+        rows = []
+        for b, (s, e) in enumerate(self.bucket_ranges):
+            lo, hi = sorted((self.bucket_starts[b], self.bucket_starts[b + 1]))
+            idx = list(range(lo, hi))
+            if not self.arena_in_ready_order:
+                idx = idx[::-1]  # model-order arena: the bucket's launch order runs backwards
+            label = (lambda i: names.get(id(a.params[i]), str(i))) if names else str
+            rows.append({"bytes": (e - s) * es, "tensors": len(idx), "first": label(idx[0]) if idx else None,
+                         "last": label(idx[-1]) if idx else None})
+        return {"count": len(rows), "cap_mb": self.cap, "first_cap_mb": self.first_cap,
+                "ready_order_layout": bool(self.arena_in_ready_order), "params": n, "launch_order": rows}
+
     def rebind_if_stream_changed(self) -> bool:
         """Re-create the autograd hooks when the caller switched streams (e.g. hipGraph capture).
 

@@ -57,6 +57,11 @@ class FlatArena:
         self.grad = None
         self.momentum = None
         self.claimed = [False] * len(params)
+        # next-step weight preparation by the optimizer (see prep_lookup / prep_plan_for)
+        self.layout_gen = 0
+        self.prep_request = None  # (weights, want_t) registered by a model's forward
+        self._prep_plan = None  # (key, plan tensors) from _C.sgd_prep_plan
+        self.prep_valid = None  # (key, weight versions) after a fused optimizer step
         if with_grad:
             self.attach_grads()
         for i, p in enumerate(params):
@@ -155,6 +160,69 @@ class FlatArena:
             return None
         return self.range_of(idx[0], idx[-1])
 
+    # ------------------------------------------------------------------ fused weight preparation
+    # The forward of a model with f16x2 / data-gradient GEMMs needs, per conv weight, |max| partials
+    # and W^T (ops.functional.weight_prep). The optimizer's step is the last writer of the weights, so
+    # it can emit both in the same pass (csrc sgd_prep_kernel) instead of a separate launch re-reading
+    # the 37 MB arena at the next forward. The forward registers what it needs (prep_request); the
+    # optimizer plans once per layout (prep_plan_for) and marks the products valid for the weights'
+    # versions at that step (prep_valid); the next forward takes them (prep_lookup) only if no weight
+    # changed since (an in-place edit, load_state_dict or a step without the fused kernel all bump a
+    # version or clear prep_valid) and otherwise prepares the weights itself.
+    def _prep_key(self, weights, want):
+        return (self.layout_gen, tuple(id(w) for w in weights), tuple(bool(f) for f in want))
+
+    def prep_lookup(self, weights, want):
+        """(amax partial views, W^T list) written by the last optimizer step, or None."""
+        v = self.prep_valid
+        if v is None or self._prep_plan is None:
+            return None
+        key, versions = v
+        if key != self._prep_key(weights, want) or key != self._prep_plan[0]:
+            return None
+        if any(w._version != ver for w, ver in zip(weights, versions)):
+            return None
+        plan = self._prep_plan[1]
+        return plan["amax_views"], plan["wts"]
+
+    def prep_plan_for(self, start: int, end: int):
+        """The fused-step plan for the flat range [start, end) if the registered request lies in it."""
+        req = self.prep_request
+        if req is None:
+            return None
+        weights, want = req
+        key = self._prep_key(weights, want)
+        if self._prep_plan is not None and self._prep_plan[0] == key and self._prep_plan[2] == (start, end):
+            return self._prep_plan[1]
+        if any(getattr(w, "_cdp_arena", None) is not self for w in weights):
+            return None
+        offs = [self.offsets[w._cdp_index] for w in weights]
+        if any(o < start or o + w.numel() > end for o, w in zip(offs, weights)):
+            return None
+        if any(w.dim() != 4 or not w.is_contiguous(memory_format=torch.channels_last) for w in weights):
+            return None
+        from .. import _native
+
+        r = _native.lib().sgd_prep_plan(self.data, start, end, [w.data for w in weights], list(want))
+        desc, meta, amax, wts = r[0], r[1], r[2], list(r[3:])
+        nblk = [((w.shape[0] + 31) // 32) * ((w.shape[1] + 31) // 32) for w in weights]
+        views, b0 = [], 0
+        for n in nblk:
+            views.append(amax.narrow(0, b0, n))
+            b0 += n
+        plan = {"desc": desc, "meta": meta, "amax": amax, "amax_views": views,
+                "wts": [t if f else None for t, f in zip(wts, want)], "weights": list(weights)}
+        self._prep_plan = (key, plan, (start, end))
+        return plan
+
+    def prep_mark_valid(self):
+        req = self.prep_request
+        if req is None or self._prep_plan is None:
+            self.prep_valid = None
+            return
+        weights, want = req
+        self.prep_valid = (self._prep_key(weights, want), [w._version for w in weights])
+
     # ------------------------------------------------------------------ relayout
     def relayout(self, new_order: Sequence[int]):
         """Permute the arena into ``new_order`` (indices into the current parameter list).
@@ -186,6 +254,9 @@ class FlatArena:
                 _view_like(self.momentum, n_off, p.data).copy_(_view_like(old_mom, o_off, p.data))
             p._cdp_index = new_i
         self.claimed = [False] * len(params)
+        self.layout_gen += 1  # offsets moved: any fused-step plan / products are stale
+        self._prep_plan = None
+        self.prep_valid = None
         if old_grad is not None:
             for p, off in zip(self.params, self.offsets):
                 if p.grad is not None:

@@ -842,12 +842,8 @@ int bn_bwd_grid(int N, int H, int W, int C, bool pool) {
   const long long rows = b;
   b = (b + 1) / 2;
   if (b < 256) b = rows < 256 ? rows : 256;
-  static const long long cap = [] {  // CDP_BN_BWD_MAXBLK: workgroup cap (partial rows), default 1024
-    const char* e = std::getenv("CDP_BN_BWD_MAXBLK");
-    const long long v = e ? std::atoll(e) : 1024;
-    return v < 256 ? 256 : v > 4096 ? 4096 : v;
-  }();
-  if (b > cap) b = cap;
+  // <= 1024 workgroups (2048 measured slower: the extra partial rows cost more in the finalize)
+  if (b > 1024) b = 1024;
   if (b < 1) b = 1;
   return (int)b;
 }
@@ -865,17 +861,12 @@ void bn_eval_stats_launch(int C, const float* gamma, const float* beta, const fl
                      stats);
 }
 
-// (up to 512 partials: 16-channel blocks above CDP_FIN_CG16 partials, 32 M2-merge loads per thread)
+// (up to 512 partials: 16-channel blocks above 32 partials, 32 M2-merge loads per thread)
 bool bn_fin_act_ok(int nparts, int C, bool residual) { return !residual && nparts <= FIN_MAXP16 && (C % 64) == 0; }
 
-// channels per fused-finalize block: 16 above CDP_FIN_CG16 partials (default 32), else 64
-static int fin_cg(int nparts) {
-  static const int t = [] {
-    const char* e = std::getenv("CDP_FIN_CG16");
-    return e ? std::atoi(e) : 32;
-  }();
-  return nparts > t ? 16 : 64;
-}
+// channels per fused-finalize block: 16 above 32 partials, else 64 (a 64-channel block merges at
+// most FIN_MAXP partials, so past that the 16-channel blocks are the only correct choice)
+static int fin_cg(int nparts) { return nparts > 32 ? 16 : 64; }
 
 int bn_fin_act_grid(int N, int H, int W, int C, bool pool, int nparts) {
   const long long rows = (long long)N * (pool ? (H / 2) * (W / 2) : H * W);

@@ -121,6 +121,23 @@ struct WeightPrepArgs {
   int nseg;
 };
 void weight_prep_launch(const WeightPrepArgs& a, float* part, hipStream_t st);
+// SGD over an arena range fused with the next step's weight preparation (sgd_prep_kernel): one
+// descriptor per conv weight (element offset in the range, W^T destination or null, shape, first
+// |max|-partial block) and one per float4 chunk of the range outside every conv weight
+struct SgdPrepSeg {
+  long long off;
+  float* wt;
+  int co, t, ci, blk0;
+};
+struct SgdPrepChunk {
+  long long start;
+  int n4, pad;
+};
+constexpr int kSgdPrepChunk4 = 1024;  // float4 per rest chunk (one workgroup)
+void sgd_prep_launch(float* p, const float* g, float* buf, const SgdPrepSeg* segs, int nseg, int nblk_w,
+                     const SgdPrepChunk* chunks, int nchunk, float* amax_part, const float* lr_ptr, float lr,
+                     float momentum, float dampening, float wd, float grad_scale, bool nesterov, bool first,
+                     bool maximize, hipStream_t st);
 void slab_sum_launch(const float* slab, int S, long long n, float* dst, bool accumulate, hipStream_t st);
 void slab_sum_strided_launch(const float* slab, int S, long long n_src, int src_cols, int dst_cols, float* dst,
                              bool accumulate, hipStream_t st);

@@ -162,6 +162,109 @@ __global__ __launch_bounds__(256) void sgd_kernel(float* __restrict__ p, const f
   }
 }
 
+// ------------------------------------------------------------------ SGD + next-step weight preparation
+// One pass over the parameter arena per step: the optimizer that writes W also emits what the next
+// forward / backward GEMMs need from it (weight_prep_kernel's products): the f16x2 |max| partial of
+// every 32x32 (co, ci) block and, where asked, W^T [ci][tap][co] (the data-gradient B operand).
+// Blocks [0, nblk_w) own one (conv weight, co32, ci32) tile over all taps: load p / g / buf of the
+// tile (branch-free buffer loads, TG taps per round trip), update exactly as sgd_kernel (same
+// sgd_one), store p / buf in place, then the |max| and the transpose of the NEW p through LDS.
+// Blocks [nblk_w, ...) each run sgd_kernel's float4 update over one chunk of the arena that no conv
+// weight covers (biases, BatchNorm parameters, the classifier).
+__global__ __launch_bounds__(256) void sgd_prep_kernel(float* __restrict__ p, const float* __restrict__ g,
+                                                      float* __restrict__ buf, const SgdPrepSeg* __restrict__ segs,
+                                                      int nseg, int nblk_w, const SgdPrepChunk* __restrict__ chunks,
+                                                      float* __restrict__ part, const float* __restrict__ lr_ptr,
+                                                      float lr_host, float m, float damp, float wd, float gs,
+                                                      int flags) {
+  constexpr int TG = 9;
+  __shared__ float tile[TG][32][33];
+  __shared__ float red[4];
+  const bool nesterov = flags & 1, first = flags & 2, maximize = flags & 4, has_mom = flags & 8;
+  const float lr = lr_ptr ? lr_ptr[0] : lr_host;
+  const int b = blockIdx.x;
+  if (b >= nblk_w) {
+    const SgdPrepChunk ch = chunks[b - nblk_w];
+    for (int i = threadIdx.x; i < ch.n4; i += 256) {
+      const long long e = ch.start + 4LL * i;
+      float4 pv = ld4(p + e);
+      const float4 gv = ld4(g + e);
+      float4 bv = has_mom && !first ? ld4(buf + e) : f4zero();
+      sgd_one(pv.x, gv.x, bv.x, lr, m, damp, wd, gs, nesterov, first, maximize, has_mom);
+      sgd_one(pv.y, gv.y, bv.y, lr, m, damp, wd, gs, nesterov, first, maximize, has_mom);
+      sgd_one(pv.z, gv.z, bv.z, lr, m, damp, wd, gs, nesterov, first, maximize, has_mom);
+      sgd_one(pv.w, gv.w, bv.w, lr, m, damp, wd, gs, nesterov, first, maximize, has_mom);
+      st4(p + e, pv);
+      if (has_mom) st4(buf + e, bv);
+    }
+    return;
+  }
+  int si = 0;
+  while (si + 1 < nseg && segs[si + 1].blk0 <= b) ++si;
+  const SgdPrepSeg sg = segs[si];
+  const int Co = sg.co, T = sg.t, Ci = sg.ci;
+  float* __restrict__ wt = sg.wt;
+  const int local = b - sg.blk0;
+  const int nci = (Ci + 31) / 32;
+  const int co0 = (local / nci) * 32, ci0 = (local % nci) * 32;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 32 x 8
+  const unsigned bytes = (unsigned)((long long)Co * T * Ci * 4);
+  float* const pw = p + sg.off;
+  float* const bw = buf ? buf + sg.off : nullptr;
+  const __amdgpu_buffer_rsrc_t pr = make_rsrc(pw, bytes);
+  const __amdgpu_buffer_rsrc_t gr = make_rsrc(g + sg.off, bytes);
+  const __amdgpu_buffer_rsrc_t br = make_rsrc(has_mom && !first ? bw : pw, bytes);
+  float mx = 0.f;
+  for (int t0 = 0; t0 < T; t0 += TG) {
+    float vp[TG][4], vg[TG][4], vb[TG][4];
+    unsigned off[TG][4];
+#pragma unroll
+    for (int q = 0; q < TG; ++q)
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) {
+        const int co = co0 + ty + 8 * jj, ci = ci0 + tx, tap = t0 + q;
+        off[q][jj] = (co < Co && ci < Ci && tap < T) ? (unsigned)(((co * T + tap) * Ci + ci) * 4) : kOOB;
+        vp[q][jj] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(pr, (int)off[q][jj], 0, 0));
+        vg[q][jj] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(gr, (int)off[q][jj], 0, 0));
+        vb[q][jj] = has_mom && !first ? __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(br, (int)off[q][jj], 0, 0))
+                                      : 0.f;
+      }
+#pragma unroll
+    for (int q = 0; q < TG; ++q)
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) {
+        sgd_one(vp[q][jj], vg[q][jj], vb[q][jj], lr, m, damp, wd, gs, nesterov, first, maximize, has_mom);
+        if (off[q][jj] != kOOB) {
+          pw[off[q][jj] >> 2] = vp[q][jj];
+          if (has_mom) bw[off[q][jj] >> 2] = vb[q][jj];
+          mx = fmaxf(mx, fabsf(vp[q][jj]));
+        }
+      }
+    if (wt) {
+#pragma unroll
+      for (int q = 0; q < TG; ++q)
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) tile[q][ty + 8 * jj][tx] = vp[q][jj];
+      __syncthreads();
+#pragma unroll
+      for (int q = 0; q < TG; ++q) {
+        const int tap = t0 + q;
+        if (tap >= T) break;
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) {
+          const int ci = ci0 + ty + 8 * jj, co = co0 + tx;
+          if (ci < Ci && co < Co) wt[((long long)ci * T + tap) * Co + co] = tile[q][tx][ty + 8 * jj];
+        }
+      }
+      __syncthreads();
+    }
+  }
+  mx = wave_max(mx);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = mx;
+  __syncthreads();
+  if (threadIdx.x == 0) part[b] = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+}
+
 // ------------------------------------------------------------------ augmentation
 __device__ __forceinline__ unsigned long long splitmix64(unsigned long long x) {
   x += 0x9E3779B97F4A7C15ull;
@@ -589,6 +692,15 @@ void sgd_launch(float* p, const float* g, float* buf, long long n, const float* 
   const int flags = (nesterov ? 1 : 0) | (first ? 2 : 0) | (maximize ? 4 : 0) | (momentum != 0.f ? 8 : 0);
   hipLaunchKernelGGL(sgd_kernel, dim3(grid_for((n + 3) / 4)), dim3(256), 0, st, p, g, buf, n, lr_ptr, lr, momentum,
                      dampening, wd, grad_scale, flags);
+}
+void sgd_prep_launch(float* p, const float* g, float* buf, const SgdPrepSeg* segs, int nseg, int nblk_w,
+                     const SgdPrepChunk* chunks, int nchunk, float* amax_part, const float* lr_ptr, float lr,
+                     float momentum, float dampening, float wd, float grad_scale, bool nesterov, bool first,
+                     bool maximize, hipStream_t st) {
+  const int flags = (nesterov ? 1 : 0) | (first ? 2 : 0) | (maximize ? 4 : 0) | (momentum != 0.f ? 8 : 0);
+  if (nblk_w + nchunk <= 0) return;
+  hipLaunchKernelGGL(sgd_prep_kernel, dim3(nblk_w + nchunk), dim3(256), 0, st, p, g, buf, segs, nseg, nblk_w, chunks,
+                     amax_part, lr_ptr, lr, momentum, dampening, wd, grad_scale, flags);
 }
 void augment_launch(const unsigned char* imgs, const long long* idx, long long idx_off, int B, int H, int W, int C,
                     const float* mean, const float* inv_std, int pad, bool flip, const long long* counter,

@@ -277,13 +277,8 @@ void wgrad_launch_t(const WgradParams& p, bool x3, hipStream_t st, int np) {
       if (fast) hipLaunchKernelGGL((wgrad_x3_kernel<BM, BN, true, 1>), grid, dim3(256), 0, st, p);
       else hipLaunchKernelGGL((wgrad_x3_kernel<BM, BN, false, 1>), grid, dim3(256), 0, st, p);
     } else if (np == 2) {
-      static const bool pipe = [] {
-        const char* e = std::getenv("CDP_WGRAD_PIPE");
-        return !(e && e[0] == '0');
-      }();
-      if (fast && pipe)
+      if (fast)
         hipLaunchKernelGGL((wgrad_x3_kernel<BM, BN, true, 2, true>), grid, dim3(wg_threads<BM>()), 0, st, p);
-      else if (fast) hipLaunchKernelGGL((wgrad_x3_kernel<BM, BN, true, 2>), grid, dim3(256), 0, st, p);
       else hipLaunchKernelGGL((wgrad_x3_kernel<BM, BN, false, 2>), grid, dim3(256), 0, st, p);
     } else if (fast) hipLaunchKernelGGL((wgrad_x3_kernel<BM, BN, true>), grid, dim3(256), 0, st, p);
     else hipLaunchKernelGGL((wgrad_x3_kernel<BM, BN, false>), grid, dim3(256), 0, st, p);

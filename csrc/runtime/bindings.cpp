@@ -20,6 +20,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("get_conv_gemm", &get_conv_gemm);
   m.def("set_gemm_override", &set_gemm_override, py::arg("kind"), py::arg("bm") = 0, py::arg("bn") = 0,
         py::arg("splits") = 0, "force the tile / split-K plan of later GEMMs (tuning sweeps; zeros restore the planner)");
+  m.def("pair_launches", &pair_launches, "paired data/weight-gradient launches issued so far");
   m.def("plan_info", &plan_info, py::arg("kind"), py::arg("M"), py::arg("N"), py::arg("K"));
   m.def("clear_hip_error", [] { return std::string(hipGetErrorName(hipGetLastError())); },
         "reset the thread's last HIP error (e.g. after an invalidated stream capture) and return its name");
@@ -57,6 +58,9 @@ PYBIND11_MODULE(_C, m) {
   m.def("xent_fwd", &xent_fwd, py::arg("logits"), py::arg("target"), py::arg("correct") = py::none());
   m.def("xent_bwd", &xent_bwd);
   m.def("sgd_step", &sgd_step);
+  m.def("sgd_prep_plan", &sgd_prep_plan, py::arg("flat"), py::arg("start"), py::arg("end"), py::arg("weights"),
+        py::arg("want_t"), "plan of the fused SGD + weight-preparation step over an arena range");
+  m.def("sgd_step_prep", &sgd_step_prep, "SGD over an arena range that also emits the next step's weight |max| / W^T");
   m.def("augment", &augment, py::arg("images"), py::arg("indices"), py::arg("idx_offset"), py::arg("batch"),
         py::arg("mean"), py::arg("std"), py::arg("pad"), py::arg("flip"), py::arg("counter"), py::arg("seed"),
         py::arg("out") = py::none(), py::arg("nbatches") = 0, py::arg("labels") = py::none(),

@@ -17,7 +17,9 @@
 
 #include <algorithm>
 #include <array>
+#include <atomic>
 #include <cstdlib>
+#include <cstring>
 #include <functional>
 #include <mutex>
 #include <string>
@@ -241,10 +243,15 @@ struct PendingWgrad {
   WgradParams p{};
   int bm = 0, bn = 0;
   std::function<void()> after;
+  // owners of every buffer p points into (dy / x may be channels_last copies and their |max|
+  // partials measured in wgrad_impl): without them the caching allocator could hand a freed block
+  // to dX before the held launch reads it
+  std::vector<at::Tensor> keep;
   void run_after() {
     set = false;
     if (after) after();
     after = nullptr;
+    keep.clear();
   }
   // launch it alone (no data-gradient GEMM took it)
   void flush(hipStream_t st) {
@@ -273,11 +280,17 @@ bool bwd_fuse_enabled() {
 // the GEMM is enqueued and the reduction left to the caller's bwd_reduce launch.
 // The conv GEMM launch, or -- a pending weight gradient of the same block given and both GEMMs
 // being f16x2 256x128 tiles -- both GEMMs in one bwd_pair launch.
+std::atomic<long long>& pair_counter() {
+  static std::atomic<long long> n{0};
+  return n;
+}
+
 void conv_launch_or_pair(const ConvGemmParams& p, const GemmPlan& g, bool dgrad, hipStream_t st,
                          PendingWgrad* pending) {
   if (pending && pending->set && dgrad && f16x2_mode() && x3_ok(p, true) && p.amax_a && p.amax_b &&
       bwd_pair_ok(p, g.bm, g.bn, pending->p, pending->bm, pending->bn, split_planes())) {
     bwd_pair_launch(p, g.bm, g.bn, pending->p, pending->bm, pending->bn, st);
+    pair_counter().fetch_add(1, std::memory_order_relaxed);
     pending->run_after();
     return;
   }
@@ -342,31 +355,18 @@ int conv_blocks_per_cu(int bm, int bn) {
   if (x3_family()) return (bm + bn) >= 256 ? 1 : (bm + bn) >= 192 ? 2 : 3;  // 2 x 3 x (bm+bn) x 64 B
   return std::max(1, std::min(4, (160 * 1024) / (2 * (bm + bn) * 36 * 4)));
 }
+// Split-K cost model constants (MFMA rate per engine, fp32-equivalent; slab round-trip bandwidth).
+// Round 2 swept the rate x0.6-x1.6 and the slab bandwidth 2-8 TB/s: every VGG-11 layer's plan and
+// the step stayed within +-2 % (docs/PERF.md), so they are fixed.
 double conv_mfma_rate() {
-  static const double scale = [] {  // tuning knob for the split-K cost model (CDP_MFMA_RATE_SCALE)
-    const char* e = std::getenv("CDP_MFMA_RATE_SCALE");
-    return e ? std::atof(e) : 1.0;
-  }();
   const int m = conv_gemm_mode();
-  return scale * (m == 1 ? 250.0e12 : m == 2 ? 800.0e12 : m == 3 ? 450.0e12 : 120.0e12);
+  return m == 1 ? 250.0e12 : m == 2 ? 800.0e12 : m == 3 ? 450.0e12 : 120.0e12;
 }
-double slab_bw() {
-  static const double bw = [] {  // modelled split-K slab round-trip bandwidth (CDP_SLAB_BW, B/s)
-    const char* e = std::getenv("CDP_SLAB_BW");
-    return e ? std::atof(e) : 4.0e12;
-  }();
-  return bw;
-}
+double slab_bw() { return 4.0e12; }
 int wgrad_blocks_per_cu(int bm, int bn) {
-  // f16x2, two-stage pipeline (default, CDP_WGRAD_PIPE=0 for one stage): 2 stages x 2 planes x
-  // (bm+bn) x 80 B of LDS, 214 / 153 / 110 VGPRs (128x128 / 128x64 / 64x64); one stage: half the
-  // LDS, 156 / 114 / 70 VGPRs
-  static const bool pipe = [] {
-    const char* e = std::getenv("CDP_WGRAD_PIPE");
-    return !(e && e[0] == '0');
-  }();
-  if (f16x2_mode() && pipe) return bm >= 256 ? 1 : (bm + bn) >= 192 ? 2 : 3;
-  if (f16x2_mode()) return (bm + bn) >= 256 ? 3 : (bm + bn) >= 192 ? 4 : 6;
+  // f16x2 (two-stage pipeline): 2 stages x 2 planes x (bm+bn) x 80 B of LDS, 214 / 153 / 110 VGPRs
+  // (128x128 / 128x64 / 64x64)
+  if (f16x2_mode()) return bm >= 256 ? 1 : (bm + bn) >= 192 ? 2 : 3;
   if (x3_family()) return (bm + bn) >= 256 ? 2 : (bm + bn) >= 192 ? 3 : 5;
   return std::max(1, std::min(4, (160 * 1024) / (2 * 32 * (bm + bn + 8) * 4)));
 }
@@ -456,26 +456,9 @@ double model_time(const GemmCostModel& m, int residency, long long P, long long 
 // per GPU: heuristic 0.638 / 0.757 / 0.970 / 1.409 (one box); model everywhere 0.551 / 0.698 /
 // 0.985 / 1.454 (same box); a single threshold of 0.95 / 0.87 / 0.80 (another box):
 // 0.552 / 0.731 / 0.981 / 1.377, 0.588 / 0.733 / 0.967 / 1.366, 0.616 / 0.743 / 0.987 / 1.363.
-double model_gain(double flops) {
-  static const double g_small = [] {
-    const char* e = std::getenv("CDP_PLANNER_GAIN_SMALL");
-    return e ? std::atof(e) : 0.95;
-  }();
-  static const double g_large = [] {
-    const char* e = std::getenv("CDP_PLANNER_GAIN");
-    return e ? std::atof(e) : 0.85;
-  }();
-  return flops < 3.2e9 ? g_small : g_large;
-}
+double model_gain(double flops) { return flops < 3.2e9 ? 0.95 : 0.85; }
 
-// CDP_PLANNER=legacy: the previous heuristic (A/B)
-bool model_planner_on() {
-  static const bool on = [] {
-    const char* e = std::getenv("CDP_PLANNER");
-    return !(e && std::string(e) == "legacy");
-  }();
-  return on && f16x2_mode();
-}
+bool model_planner_on() { return f16x2_mode(); }
 
 struct PlanKey {
   int kind, mode;
@@ -536,18 +519,11 @@ GemmPlan plan_gemm(long long M, int Nout, int Kdim) {
   // on VGG-11 B=256 they beat 128x128 / 64x128 on every layer, split-K making up the grid
   // (127.5k vs 124.5k img/s with 256 only for M >= 8192)
   if (x3_family() && g.bn == 128) g.bm = 256;
-  static const int force_bm = [] {
-    const char* e = std::getenv("CDP_TILE_BM");
-    return e ? std::atoi(e) : 0;
-  }();
-  if (force_bm == 64 || force_bm == 128) g.bm = force_bm;
-  if (force_bm == 256 && g.bn == 128 && x3_family()) g.bm = 256;
-  if (force_bm == 128 && g.bm == 256) g.bm = 128;
   const long long tiles = ((M + g.bm - 1) / g.bm) * ((Nout + g.bn - 1) / g.bn);
   const int slots = conv_blocks_per_cu(g.bm, g.bn) * num_cus();
   g.splits = std::min(16, choose_splits(tiles, g.ktiles, slots, 4, 2.0 * M * Nout * Kdim, 4.0 * M * Nout,
                                         conv_mfma_rate()));
-  if (model_planner_on() && force_bm == 0) {
+  if (model_planner_on()) {
     const auto m = model_plan(false, M, Nout, Kdim);
     const double t_model = model_time(kConvCost, conv_blocks_per_cu(m[0], m[1]), M, Nout, Kdim, m[0], m[1], m[2]);
     const double t_heur = model_time(kConvCost, conv_blocks_per_cu(g.bm, g.bn), M, Nout, Kdim, g.bm, g.bn, g.splits);
@@ -575,21 +551,10 @@ WgradPlan plan_wgrad(int Cout, int Kdim, long long M) {
   w.bm = Cout >= 128 ? 128 : 64;
   // 128-wide k tiles also when Kdim is an odd multiple of 64 and >= 512 (e.g. 576 = 9 x 64: 4.5
   // tiles, the last one half padding). Measured on VGG-11 layer 1 (B=256): 70.7 -> 61.9 us.
-  // CDP_WGRAD_BN=64 restores the exact 64-wide tiling.
-  static const int force_bn = [] {
-    const char* e = std::getenv("CDP_WGRAD_BN");
-    return e ? std::atoi(e) : 128;
-  }();
-  w.bn = (Kdim % 128 == 0 || (force_bn == 128 && Kdim >= 512)) ? 128 : 64;
-  // 256x128 f16x2 tiles, 8 waves, one workgroup per CU (pipelined kernel only; CDP_WGRAD_BM=128
-  // for the 128-wide tiles). Measured on MI355X, VGG-11 B=256: 156.0k -> 161.7k img/s (the x
-  // gather and split are shared by four co waves instead of two)
-  static const bool wide = [] {
-    const char* e = std::getenv("CDP_WGRAD_BM");
-    const char* q = std::getenv("CDP_WGRAD_PIPE");
-    return !(e && std::atoi(e) != 256) && !(q && q[0] == '0');
-  }();
-  if (wide && f16x2_mode() && Cout >= 256 && Cout % 4 == 0 && w.bn == 128) w.bm = 256;
+  w.bn = (Kdim % 128 == 0 || Kdim >= 512) ? 128 : 64;
+  // 256x128 f16x2 tiles, 8 waves, one workgroup per CU. Measured on MI355X, VGG-11 B=256:
+  // 156.0k -> 161.7k img/s (the x gather and split are shared by four co waves instead of two)
+  if (f16x2_mode() && Cout >= 256 && Cout % 4 == 0 && w.bn == 128) w.bm = 256;
   const long long tiles = (long long)((Cout + w.bm - 1) / w.bm) * ((Kdim + w.bn - 1) / w.bn);
   const int mt = (int)std::min<long long>((M + 31) / 32, 1 << 30);
   const int slots = wgrad_blocks_per_cu(w.bm, w.bn) * num_cus();
@@ -643,6 +608,9 @@ at::Tensor pad_channels4(const at::Tensor& t, at::Tensor* amax = nullptr) {
 }
 
 }  // namespace
+
+// paired gradient launches (bwd_pair) issued by this process so far (tests check the pair is taken)
+int64_t pair_launches() { return pair_counter().load(std::memory_order_relaxed); }
 
 void set_gemm_override(const std::string& kind, int64_t bm, int64_t bn, int64_t splits) {
   TORCH_CHECK(kind == "conv" || kind == "wgrad", "set_gemm_override: kind must be 'conv' or 'wgrad'");
@@ -733,14 +701,6 @@ std::vector<at::Tensor> conv2d_fwd(const at::Tensor& x_, const at::Tensor& w_, c
 // masked full-resolution gather (which spends 3/4 of its MACs on taps that cannot contribute).
 // Classes without taps (e.g. the odd pixels of a 1x1 stride-2 conv) get zeros from a K-less
 // launch. Returns false when a shape is outside the x3 kernels' addressing limits.
-bool subpixel_enabled() {
-  static const bool on = [] {
-    const char* e = std::getenv("CDP_DGRAD_SUBPIXEL");
-    return !(e && e[0] == '0');
-  }();
-  return on;
-}
-
 bool conv2d_dgrad_subpixel(const at::Tensor& dy, const at::Tensor& w, at::Tensor& dx, int pad, hipStream_t st,
                            const float* addend, const at::Tensor& dya, const at::Tensor& wa) {
   const int N = dx.size(0), C = dx.size(1), H = dx.size(2), W = dx.size(3);
@@ -809,7 +769,7 @@ at::Tensor dgrad_impl(const at::Tensor& dy_, const at::Tensor& w_, std::vector<i
                 "dgrad addend must be a channels_last fp32 tensor of the input's shape");
   const float* addp = has_add ? addend->data_ptr<float>() : nullptr;
   const at::Tensor dya = amax_parts(dy, dy_amax, st), wa = amax_parts(w, w_amax, st);  // |max| W^T = |max| W
-  if (stride == 2 && x3_family() && subpixel_enabled()) {
+  if (stride == 2 && x3_family()) {
     at::Tensor dx = has_add ? *addend : at::empty({N, C, H, W}, opts.memory_format(at::MemoryFormat::ChannelsLast));
     if (conv2d_dgrad_subpixel(dy, w, dx, (int)pad, st, addp, dya, wa)) return dx;
   }
@@ -902,6 +862,7 @@ at::Tensor wgrad_impl(const at::Tensor& dy_, const at::Tensor& x_, std::vector<i
       pending->bm = wp.bm;
       pending->bn = wp.bn;
       pending->after = std::move(after);
+      pending->keep = {dy, x, dya, xa};
       return;
     }
     wgrad_launch(p, wp.bm, wp.bn, x3_family() && x3_ok(p), st, split_planes());
@@ -939,13 +900,7 @@ at::Tensor conv2d_wgrad_keep(const at::Tensor& dy, const at::Tensor& x, std::vec
 }
 
 // ---------------------------------------------------------------- RGB stem (stem.hip)
-bool stem_enabled() {
-  static const bool on = [] {
-    const char* e = std::getenv("CDP_STEM");
-    return !(e && e[0] == '0');
-  }();
-  return on;
-}
+bool stem_enabled() { return true; }
 
 // Training-mode conv + BN + act [+ pool] of a Cin <= 4 stem; same outputs as conv_bn_act_fwd with
 // x saved unpadded (xsave = x) and no f16x2 maxima for x / W (the stem kernels need none).
@@ -1387,6 +1342,89 @@ void sgd_step(at::Tensor p, const at::Tensor& g, c10::optional<at::Tensor> buf, 
   }
   sgd_launch(p.data_ptr<float>(), g.data_ptr<float>(), bp, p.numel(), fptr(lr_t), (float)lr, (float)momentum,
              (float)dampening, (float)wd, (float)grad_scale, nesterov, first, maximize, cur_stream());
+}
+
+// ---------------------------------------------------------------- SGD + next-step weight preparation
+// Plan of the fused optimizer step over the flat range [s, e) of `flat` (an arena's parameter
+// storage): one segment per conv weight (a channels_last view inside the range), the W^T
+// destinations where want_t, and float4 chunks for everything else in the range. Returns
+// {descriptor (device bytes), meta (cpu int64: nseg, nblk_w, nchunk), amax partials (device; one per
+// 32x32 (co, ci) block, weight i's at [blk0_i, blk0_{i+1}) as weight_prep lays them out),
+// W^T per weight (undefined where not wanted)}. Built once per arena layout, outside any capture.
+std::vector<at::Tensor> sgd_prep_plan(const at::Tensor& flat, int64_t s, int64_t e, const std::vector<at::Tensor>& ws,
+                                      const std::vector<bool>& want_t) {
+  check_f32_cuda(flat, "arena");
+  TORCH_CHECK(ws.size() == want_t.size() && !ws.empty(), "sgd_prep_plan: one want_t flag per weight");
+  TORCH_CHECK(0 <= s && s < e && e <= flat.numel() && (s % 4) == 0, "sgd_prep_plan: bad range");
+  const float* base = flat.data_ptr<float>() + s;
+  std::vector<SgdPrepSeg> segs;
+  std::vector<std::pair<long long, long long>> covered;
+  std::vector<at::Tensor> outs;
+  int blk = 0;
+  for (size_t i = 0; i < ws.size(); ++i) {
+    const at::Tensor& w = ws[i];
+    check_f32_cuda(w, "sgd_prep weight");
+    TORCH_CHECK(w.dim() == 4 && w.is_contiguous(at::MemoryFormat::ChannelsLast),
+                "sgd_prep_plan: conv weights must be channels_last [Co, Ci, KH, KW]");
+    const long long off = w.data_ptr<float>() - base;
+    TORCH_CHECK(off >= 0 && off + w.numel() <= e - s && (off % 4) == 0, "sgd_prep_plan: weight outside the range");
+    const int Co = w.size(0), Ci = w.size(1), T = w.size(2) * w.size(3);
+    TORCH_CHECK((long long)Co * T * Ci * 4 < (1LL << 31), "sgd_prep_plan: weight too large");
+    at::Tensor wt;
+    if (want_t[i]) wt = at::empty({Ci, (long long)T * Co}, flat.options());
+    outs.push_back(wt);
+    segs.push_back(SgdPrepSeg{off, wt.defined() ? wt.data_ptr<float>() : nullptr, Co, T, Ci, blk});
+    blk += ((Co + 31) / 32) * ((Ci + 31) / 32);
+    covered.push_back({off, off + (w.numel() + 3) / 4 * 4});
+  }
+  std::sort(covered.begin(), covered.end());
+  std::vector<SgdPrepChunk> chunks;
+  long long cur = 0;
+  auto add_gap = [&](long long a, long long b) {
+    for (long long x = a; x < b; x += 4LL * kSgdPrepChunk4)
+      chunks.push_back(SgdPrepChunk{x, (int)(std::min<long long>(b - x, 4LL * kSgdPrepChunk4) / 4), 0});
+  };
+  for (const auto& c : covered) {
+    TORCH_CHECK(c.first >= cur, "sgd_prep_plan: overlapping weights");
+    add_gap(cur, c.first);
+    cur = c.second;
+  }
+  TORCH_CHECK(((e - s) % 4) == 0, "sgd_prep_plan: range must be whole float4s");
+  add_gap(cur, e - s);
+  const size_t seg_bytes = segs.size() * sizeof(SgdPrepSeg);
+  const size_t bytes = seg_bytes + chunks.size() * sizeof(SgdPrepChunk);
+  at::Tensor host = at::empty({(long long)std::max<size_t>(bytes, 16)}, at::TensorOptions().dtype(at::kByte));
+  std::memcpy(host.data_ptr<uint8_t>(), segs.data(), seg_bytes);
+  if (!chunks.empty()) std::memcpy(host.data_ptr<uint8_t>() + seg_bytes, chunks.data(), bytes - seg_bytes);
+  at::Tensor desc = host.to(flat.device());
+  at::Tensor meta = at::tensor({(int64_t)segs.size(), (int64_t)blk, (int64_t)chunks.size()}, at::kLong);
+  at::Tensor amax = at::empty({std::max(blk, 1)}, flat.options());
+  std::vector<at::Tensor> r = {desc, meta, amax};
+  for (auto& t : outs) r.push_back(t);
+  return r;
+}
+
+void sgd_step_prep(at::Tensor p, const at::Tensor& g, c10::optional<at::Tensor> buf, const c10::optional<at::Tensor>& lr_t,
+                   double lr, double momentum, double dampening, double wd, double grad_scale, bool nesterov, bool first,
+                   bool maximize, const at::Tensor& desc, const at::Tensor& meta, at::Tensor amax) {
+  check_f32_cuda(p, "param");
+  TORCH_CHECK(p.is_contiguous() && g.is_contiguous() && p.numel() == g.numel(), "sgd: flat contiguous tensors required");
+  float* bp = nullptr;
+  if (momentum != 0.0) {
+    TORCH_CHECK(buf.has_value() && buf->numel() == p.numel(), "sgd: momentum buffer required");
+    bp = buf->data_ptr<float>();
+  }
+  TORCH_CHECK(meta.device().is_cpu() && meta.numel() == 3 && desc.is_cuda(), "sgd_step_prep: plan from sgd_prep_plan");
+  const int64_t* mt = meta.data_ptr<int64_t>();
+  const int nseg = (int)mt[0], nblk = (int)mt[1], nchunk = (int)mt[2];
+  TORCH_CHECK(desc.numel() >= (int64_t)(nseg * sizeof(SgdPrepSeg) + nchunk * sizeof(SgdPrepChunk)) &&
+                  amax.numel() >= nblk,
+              "sgd_step_prep: descriptor / amax smaller than the plan");
+  const uint8_t* d = desc.data_ptr<uint8_t>();
+  sgd_prep_launch(p.data_ptr<float>(), g.data_ptr<float>(), bp, reinterpret_cast<const SgdPrepSeg*>(d), nseg, nblk,
+                  reinterpret_cast<const SgdPrepChunk*>(d + nseg * sizeof(SgdPrepSeg)), nchunk,
+                  amax.data_ptr<float>(), fptr(lr_t), (float)lr, (float)momentum, (float)dampening, (float)wd,
+                  (float)grad_scale, nesterov, first, maximize, cur_stream());
 }
 
 // ---------------------------------------------------------------- data augmentation

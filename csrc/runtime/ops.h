@@ -9,6 +9,7 @@ namespace cdp {
 void set_conv_gemm(const std::string& mode);
 // tuning sweeps: force the tile / split-K plan of later conv ('conv') or weight-gradient ('wgrad')
 // GEMMs (0 = planner's choice); plan_info returns the planner's {bm, bn, splits}
+int64_t pair_launches();
 void set_gemm_override(const std::string& kind, int64_t bm, int64_t bn, int64_t splits);
 std::vector<int64_t> plan_info(const std::string& kind, int64_t M, int64_t N, int64_t K);
 std::string get_conv_gemm();
@@ -63,6 +64,11 @@ std::vector<at::Tensor> linear_bwd(const at::Tensor& gy, const at::Tensor& x, co
                                    const c10::optional<at::Tensor>& db_out);
 at::Tensor xent_fwd(const at::Tensor& logits, const at::Tensor& target, const c10::optional<at::Tensor>& correct);
 at::Tensor xent_bwd(const at::Tensor& gloss, const at::Tensor& logits, const at::Tensor& target);
+std::vector<at::Tensor> sgd_prep_plan(const at::Tensor& flat, int64_t s, int64_t e, const std::vector<at::Tensor>& ws,
+                                      const std::vector<bool>& want_t);
+void sgd_step_prep(at::Tensor p, const at::Tensor& g, c10::optional<at::Tensor> buf, const c10::optional<at::Tensor>& lr_t,
+                   double lr, double momentum, double dampening, double wd, double grad_scale, bool nesterov, bool first,
+                   bool maximize, const at::Tensor& desc, const at::Tensor& meta, at::Tensor amax);
 void sgd_step(at::Tensor p, const at::Tensor& g, c10::optional<at::Tensor> buf, const c10::optional<at::Tensor>& lr_t,
               double lr, double momentum, double dampening, double wd, double grad_scale, bool nesterov, bool first,
               bool maximize);

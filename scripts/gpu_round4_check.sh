@@ -1,0 +1,9 @@
+# Round-4 GPU check: smoke, the GPU test suite, the default 1-GPU bench (the driver's steps)
+set -o pipefail
+mkdir -p gpurun_out
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || { tail -20 gpurun_out/smoke.log; exit 1; }
+tail -1 gpurun_out/smoke.log
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread ${PYTEST_ARGS} > gpurun_out/gputest.log 2>&1 || { tail -40 gpurun_out/gputest.log; exit 1; }
+tail -3 gpurun_out/gputest.log
+timeout -k 10 300 python bench.py --gpus 1 --steps 20 --warmup 5 > gpurun_out/bench_driver.log 2>&1 || { tail -20 gpurun_out/bench_driver.log; exit 1; }
+tail -1 gpurun_out/bench_driver.log

@@ -1,0 +1,117 @@
+"""The paired gradient launch (csrc/kernels/bwd_pair.h: a block's data- and weight-gradient GEMMs in
+one grid) against the two separate launches (CDP_BWD_PAIR=0, read on every call) and against fp64.
+
+* At the VGG-11 layer shapes of the bench (256 images) and of the reference's 8-rank strong-scaling
+  point (32 images, /root/reference/src/Part 2a/main.py:22), the pair is really taken (the
+  runtime's launch counter moves), and dX / dW equal the unpaired launches' and torch fp64's.
+* An NCHW-contiguous input that needs a gradient: the weight-gradient GEMM held back for the pair
+  reads a channels_last copy of x and |max| partials made inside the backward call; both must stay
+  alive until the paired launch is enqueued (else dX, allocated in between, may reuse their memory).
+"""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+VGG_LAYERS = [(64, 128, 16), (128, 256, 8), (256, 256, 8), (256, 512, 4), (512, 512, 4), (512, 512, 2),
+              (512, 512, 2)]
+POOL_AFTER = {1, 3, 5, 7}  # VGG-11 blocks followed by 'M' (cfg, models/vgg.py)
+
+
+def _lib():
+    import cs744_distributed_data_parallel_amd as cdp
+
+    return cdp._native.lib()
+
+
+def _block(Ci, Co, seed):
+    torch.manual_seed(seed)
+    conv = torch.nn.Conv2d(Ci, Co, 3, padding=1).cuda()
+    conv.weight.data = conv.weight.data.contiguous(memory_format=torch.channels_last)
+    bn = torch.nn.BatchNorm2d(Co).cuda()
+    with torch.no_grad():
+        bn.weight.uniform_(0.5, 1.5)
+        bn.bias.uniform_(-0.2, 0.2)
+    return conv, bn
+
+
+def _grads(monkeypatch, pair, x, conv, bn, pool, gy):
+    from cs744_distributed_data_parallel_amd.ops import functional as CF
+
+    monkeypatch.setenv("CDP_BWD_PAIR", "1" if pair else "0")
+    xr = x.detach().clone().requires_grad_()
+    for p in (conv.weight, conv.bias, bn.weight, bn.bias):
+        p.grad = None
+    n0 = _lib().pair_launches()
+    out = CF.conv_bn_act(xr, conv, bn, relu=True, pool=pool)
+    out.backward(gy)
+    torch.cuda.synchronize()
+    return xr.grad.clone(), conv.weight.grad.clone(), _lib().pair_launches() - n0
+
+
+def _fp64(x, conv, bn, pool, gy):
+    xd = x.double().detach().requires_grad_()
+    wd = conv.weight.double().detach().requires_grad_()
+    y = F.conv2d(xd, wd, conv.bias.double(), 1, 1)
+    y = F.batch_norm(y, None, None, bn.weight.double(), bn.bias.double(), True, 0.0, bn.eps)
+    y = F.relu(y)
+    if pool:
+        y = F.max_pool2d(y, 2, 2)
+    y.backward(gy.double())
+    return xd.grad, wd.grad
+
+
+def _rel(a, b):
+    return ((a.double() - b.double()).norm() / b.double().norm()).item()
+
+
+@pytest.mark.parametrize("B", [256, 32])
+@pytest.mark.parametrize("layer", range(1, 8))
+def test_paired_gradients_match_separate_launches_and_fp64(monkeypatch, B, layer):
+    lib = _lib()
+    orig = lib.get_conv_gemm()
+    try:
+        lib.set_conv_gemm("f16x2")
+        Ci, Co, HW = VGG_LAYERS[layer - 1]
+        conv, bn = _block(Ci, Co, 10 + layer)
+        pool = layer in POOL_AFTER
+        x = torch.relu(torch.randn(B, Ci, HW, HW, device="cuda")).contiguous(memory_format=torch.channels_last)
+        oh = HW // 2 if pool else HW
+        gy = torch.randn(B, Co, oh, oh, device="cuda").contiguous(memory_format=torch.channels_last)
+        dx_p, dw_p, n_pair = _grads(monkeypatch, True, x, conv, bn, pool, gy)
+        dx_s, dw_s, n_sep = _grads(monkeypatch, False, x, conv, bn, pool, gy)
+    finally:
+        lib.set_conv_gemm(orig)
+    assert n_pair == 1 and n_sep == 0, (n_pair, n_sep)
+    # same tiles, same split-K partition, same reduction order: the pair changes only which
+    # workgroup runs which tile
+    assert _rel(dx_p, dx_s) <= 1e-6 and _rel(dw_p, dw_s) <= 1e-6, (_rel(dx_p, dx_s), _rel(dw_p, dw_s))
+    dx_r, dw_r = _fp64(x, conv, bn, pool, gy)
+    e_dx, e_dw = _rel(dx_p, dx_r.cuda()), _rel(dw_p, dw_r.cuda())
+    print(f"B={B} layer {layer}: paired vs fp64 rel-L2 dX {e_dx:.2e} dW {e_dw:.2e}")
+    assert e_dx <= 1e-5 and e_dw <= 1e-5, (e_dx, e_dw)
+
+
+def test_held_weight_gradient_keeps_its_nchw_input_alive(monkeypatch):
+    lib = _lib()
+    orig = lib.get_conv_gemm()
+    try:
+        lib.set_conv_gemm("f16x2")
+        conv, bn = _block(128, 256, 3)
+        x = torch.relu(torch.randn(64, 128, 8, 8, device="cuda"))  # NCHW-contiguous, not channels_last
+        assert not x.is_contiguous(memory_format=torch.channels_last)
+        gy = torch.randn(64, 256, 8, 8, device="cuda")
+        res = []
+        for pair in (True, False):
+            # several rounds so the caching allocator has freed blocks of x's size to hand out
+            for _ in range(3):
+                dx, dw, n = _grads(monkeypatch, pair, x, conv, bn, False, gy)
+            res.append((dx, dw, n))
+    finally:
+        lib.set_conv_gemm(orig)
+    (dx_p, dw_p, n_p), (dx_s, dw_s, n_s) = res
+    assert n_p == 1 and n_s == 0
+    assert _rel(dx_p, dx_s) <= 1e-6 and _rel(dw_p, dw_s) <= 1e-6, (_rel(dx_p, dx_s), _rel(dw_p, dw_s))
+    dx_r, dw_r = _fp64(x, conv, bn, False, gy)
+    assert _rel(dw_p, dw_r.cuda()) <= 1e-5 and _rel(dx_p, dx_r.cuda()) <= 1e-5

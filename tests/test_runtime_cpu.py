@@ -303,20 +303,51 @@ def _bench(args, env_extra=None, timeout=600):
 
 def test_bench_self_launches_ranks_cpu():
     """`bench.py --gpus 2` without WORLD_SIZE starts both ranks itself; rank 0 prints one JSON line
-    with n_gpus == ranks_seen == 2, the strong-scaling point and the exposed-comm estimate."""
+    with n_gpus == ranks_seen == 2, the strong-scaling point, the exposed-comm estimate and the
+    reference's whole multi-process experiment: every sync strategy at its strong-scaling rule
+    (int(global / W) images per rank), each with ms/step, exposed sync, scaling_eff and a
+    bit-identical-replicas check -- BASELINE.md's Part 2a / 2b / 3 rows map onto these keys."""
     r = _bench(["--gpus", "2", "--device", "cpu", "--steps", "2", "--warmup", "1", "--local-batch", "4",
-                "--dataset-size", "64"])
+                "--global-batch", "16", "--dataset-size", "64"])
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, r.stdout
     rec = json.loads(lines[0])
     assert rec["n_gpus"] == 2 and rec["ranks_seen"] == 2
     assert rec["config"]["parallelism"] == "dp2" and rec["config"]["global_batch"] == 8
-    assert rec["strong"]["global_batch"] == 256 and rec["strong"]["local_batch"] == 128
+    assert rec["strong"]["global_batch"] == 16 and rec["strong"]["local_batch"] == 8
     assert rec["exposed_comm_ms"] >= 0 and rec["value"] > 0
     # self-verification: every rank holds the same parameters + momentum after the timed steps
     assert rec["replicas_identical"] is True
     assert rec["config"]["comm_fallback_reason"] is None and rec["config"]["graph_collectives"] is None
+    blk = rec["strategies"]
+    assert blk["local_batch"] == 8 and blk["global_batch"] == 16 and blk["no_sync"]["ms_per_step"] > 0
+    for strat, part in (("gather_scatter", "Part 2a"), ("allreduce_blocking", "Part 2b"),
+                        ("bucketed_overlap", "config #3"), ("ddp", "Part 3")):
+        e = blk[strat]
+        assert part in e["reference"]
+        assert e["ms_per_step"] > 0 and e["value"] > 0 and e["exposed_sync_ms"] >= 0
+        assert 0 < e["scaling_eff"] <= 1.0
+        assert e["replicas_identical"] is True, strat
+    # the bucketed strategies report their plan in launch order
+    for strat in ("bucketed_overlap", "ddp"):
+        b = blk[strat]["buckets"]
+        assert b["count"] == len(b["launch_order"]) >= 2
+        assert sum(x["bytes"] for x in b["launch_order"]) >= 36_924_456  # every VGG-11 gradient
+    assert set(rec["scaling_eff"]) == {"weak", "strong"}
+    assert rec["scaling_eff"]["strong"] == blk["ddp"]["scaling_eff"]
+
+
+def test_bench_launcher_at_eight_ranks_cpu():
+    """The driver's largest point, rehearsed over gloo on the CPU: eight rank processes, one record."""
+    r = _bench(["--gpus", "8", "--device", "cpu", "--steps", "1", "--warmup", "1", "--local-batch", "2",
+                "--dataset-size", "32", "--no-extra"])
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    rec = json.loads(lines[0])
+    assert rec["n_gpus"] == 8 and rec["ranks_seen"] == 8 and rec["config"]["parallelism"] == "dp8"
+    assert rec["config"]["global_batch"] == 16 and rec["replicas_identical"] is True
 
 
 @pytest.mark.parametrize("strategy", ["gather_scatter", "allreduce_blocking", "bucketed_overlap"])

@@ -1,0 +1,117 @@
+"""The optimizer step that also prepares the next forward's weights (csrc sgd_prep_kernel): one pass
+over the parameter arena instead of SGD (sgd_kernel) + a separate weight_prep_kernel at the next
+forward.
+
+* 20 VGG-11 steps with the fused step and 20 with the two-kernel path from the same init give
+  bitwise-identical parameters and momentum buffers (the update is the same sgd_one per element),
+  and the forwards after the first really take the fused products (PREP_HITS).
+* The prepared |max| partials and W^T equal what the standalone weight_prep_kernel makes from the
+  stepped weights.
+* A weight edited in place between steps (``torch.no_grad(): w.add_``, load_state_dict) bumps its
+  version: the next forward prepares the weights itself and its output matches a model that never
+  used the fused path.
+"""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _setup(seed=0):
+    import cs744_distributed_data_parallel_amd as cdp
+
+    torch.manual_seed(seed)
+    model = cdp.VGG11().cuda()
+    opt = cdp.SGD(model.parameters(), lr=0.1, momentum=0.9, weight_decay=1e-4)
+    return cdp, model, opt
+
+
+def _batch(step, B=64):
+    g = torch.Generator(device="cuda").manual_seed(1000 + step)
+    x = torch.randn(B, 3, 32, 32, device="cuda", generator=g).contiguous(memory_format=torch.channels_last)
+    y = torch.randint(0, 10, (B,), device="cuda", generator=g)
+    return x, y
+
+
+def _train(fused, steps=20):
+    from cs744_distributed_data_parallel_amd.ops import functional as CF
+
+    cdp, model, opt = _setup()
+    opt.fused_prep = fused
+    crit = cdp.CrossEntropyLoss()
+    h0 = CF.PREP_HITS[0]
+    for i in range(steps):
+        x, y = _batch(i)
+        opt.zero_grad()
+        crit(model(x), y).backward()
+        opt.step()
+    torch.cuda.synchronize()
+    params = [p.detach().clone() for p in model.parameters()]
+    moms = [opt.state[p]["momentum_buffer"].clone() for p in model.parameters()]
+    return params, moms, CF.PREP_HITS[0] - h0, model, opt
+
+
+def test_fused_step_is_bitwise_the_two_kernel_path():
+    p_f, m_f, hits_f, _, _ = _train(True)
+    p_s, m_s, hits_s, _, _ = _train(False)
+    assert hits_f == 19 and hits_s == 0, (hits_f, hits_s)
+    for a, b in zip(p_f + m_f, p_s + m_s):
+        assert torch.equal(a, b)
+
+
+def test_fused_products_equal_standalone_weight_prep():
+    from cs744_distributed_data_parallel_amd.ops import functional as CF
+
+    _, _, _, model, opt = _train(True, steps=3)
+    weights = [model.layers[ci].weight for ci, _, _ in model._plan]
+    want = [k > 0 for k in range(len(weights))]
+    hit = model.layers[0].weight._cdp_arena.prep_lookup(weights, want)
+    assert hit is not None
+    amax_f, wts_f = hit
+    C = __import__("cs744_distributed_data_parallel_amd")._native.lib()
+    amax_s, wts_s = C.weight_prep(weights, want)
+    for k in range(len(weights)):
+        assert torch.equal(amax_f[k], amax_s[k]), k
+        if want[k]:
+            assert torch.equal(wts_f[k], wts_s[k]), k
+        else:
+            assert wts_f[k] is None
+
+
+@pytest.mark.parametrize("edit", ["inplace", "load_state_dict"])
+def test_weight_edited_between_steps_is_seen_by_the_gemms(edit):
+    from cs744_distributed_data_parallel_amd.ops import functional as CF
+
+    cdp, model, opt = _setup()
+    crit = cdp.CrossEntropyLoss()
+    for i in range(3):
+        x, y = _batch(i)
+        opt.zero_grad()
+        crit(model(x), y).backward()
+        opt.step()
+    w = model.layers[8].weight  # block 2's conv: its W^T and |max| come from the fused step
+    if edit == "inplace":
+        with torch.no_grad():
+            w.mul_(3.0)  # the |max| and W^T the step wrote are now stale
+    else:
+        sd = {k: v.clone() for k, v in model.state_dict().items()}
+        sd["layers.8.weight"] = sd["layers.8.weight"] * 3.0
+        model.load_state_dict(sd)
+    h0 = CF.PREP_HITS[0]
+    x, y = _batch(99)
+    model.train()
+    out = model(x)
+    assert CF.PREP_HITS[0] == h0  # the forward prepared the edited weights itself
+    # a fresh model holding the same (edited) weights, never touched by a fused step
+    _, ref, _ = _setup()
+    ref.load_state_dict(model.state_dict())
+    ref.train()
+    out_ref = ref(x)
+    torch.cuda.synchronize()
+    assert torch.equal(out, out_ref)
+    # and backward uses the edited W^T: same input gradient as the fresh model
+    xa = x.clone().requires_grad_()
+    xb = x.clone().requires_grad_()
+    crit(model(xa), y).backward()
+    crit(ref(xb), y).backward()
+    assert torch.equal(xa.grad, xb.grad)
