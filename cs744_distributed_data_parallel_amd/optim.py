@@ -68,6 +68,15 @@ class SGD(Optimizer):
             if st and st.get("momentum_buffer") is not None:
                 st["momentum_buffer"] = views[p._cdp_index]
 
+    # ------------------------------------------------------------------ fused weight preparation
+    def refresh_weight_prep(self) -> bool:
+        """Re-derive the next forward's weight |max| / W^T from the current weights (in place).
+
+        With ``fused_prep`` (default) the step itself writes them for the next forward. Eager forwards
+        notice weights edited since (a bumped version) and prepare them anew; a replayed hipGraph
+        cannot, so after editing weights between replays of a captured step call this first."""
+        return self._arena.prep_refresh() if self._arena is not None else False
+
     # ------------------------------------------------------------------ device-side LR
     def lr_tensor(self) -> torch.Tensor:
         """A 1-element device tensor holding the LR of param group 0 (graph-capture friendly)."""

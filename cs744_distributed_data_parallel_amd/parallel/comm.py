@@ -222,13 +222,14 @@ class TorchCommunicator(Communicator):
         return t.is_cuda and tdist.get_backend(self.group) == "gloo"
 
     # gloo on device tensors (the one-GPU multi-rank rehearsal; production GPU runs use the RCCL
-    # communicator): the gather / scatter are staged through host tensors here, with blocking copies.
-    # torch's own device-tensor path for these two collectives (host staging on gloo's streams) was
-    # not reproducible run to run on ROCm: two ranks training VGG-11 with the gather/scatter strategy
-    # differed after step 3 in 4 of 9 repeats (relative L2 up to 1e-4, step 1 always bitwise equal),
-    # even with a device-wide sync around every call; staged by hand, 9 of 9 repeats were bitwise
-    # equal (scripts/diag/gs_repeat.py, gs_repeat_cpu_staged.py). all_reduce / broadcast reproduce
-    # bitwise on the device path and keep it.
+    # communicator): the gather / scatter are staged through host tensors here, with blocking copies
+    # and a device-wide sync before and after. What was measured (two ranks training VGG-11 with the
+    # gather/scatter strategy on one GPU, scripts/diag/gs_repeat.py and gs_repeat_cpu_staged.py):
+    # passing device tensors straight to gloo, 4 of 9 repeats differed after step 3 (relative L2 up
+    # to 1e-4; step 1 always bitwise equal); with this staging, 9 of 9 were bitwise equal. The
+    # experiment changed two things at once -- host staging AND the syncs -- so it does not say
+    # which one (or which code path) caused the difference; no cause was found in code. all_reduce /
+    # broadcast reproduced bitwise on the device path and keep it.
     def gather(self, t, gather_list=None, dst=0):
         if not self._gloo_device(t):
             tdist.gather(t, gather_list if self.rank == dst else None, dst=dst, group=self.group)

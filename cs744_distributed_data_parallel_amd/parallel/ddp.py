@@ -89,6 +89,9 @@ class DistributedDataParallel(nn.Module):
             first_bucket_cap_mb if first_bucket_cap_mb is not None else DEFAULT_FIRST_BUCKET_CAP_MB,
             find_unused_parameters,
             average=True,
+            # no explicit cap: the plan is designed at the ready-order rebuild from the measured
+            # backward timeline and communicator (buckets.plan_buckets_timed)
+            timed_plan=bucket_cap_mb is None and first_bucket_cap_mb is None and rebuild_buckets,
         )
         self._rebuild = rebuild_buckets
         self._rebuilt = False

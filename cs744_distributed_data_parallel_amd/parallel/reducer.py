@@ -21,7 +21,7 @@ import torch.distributed as tdist
 
 from .. import _native
 from ..utils.arena import ALIGN, FlatArena
-from .buckets import DEFAULT_BUCKET_CAP_MB, DEFAULT_FIRST_BUCKET_CAP_MB, plan_buckets
+from .buckets import DEFAULT_BUCKET_CAP_MB, DEFAULT_FIRST_BUCKET_CAP_MB, fit_comm_model, plan_buckets, plan_buckets_timed
 from .comm import Communicator, RcclCommunicator, TorchCommunicator
 
 
@@ -194,6 +194,7 @@ class GradReducer:
         find_unused_parameters: bool = False,
         average: bool = True,
         arena_in_ready_order: bool = False,
+        timed_plan: bool = False,
     ):
         self.arena, self.comm = arena, comm
         self.cap, self.first_cap = bucket_cap_mb, first_bucket_cap_mb
@@ -201,7 +202,12 @@ class GradReducer:
         self.arena_in_ready_order = arena_in_ready_order
         self._impl = None
         self._stream = None
+        self._groups_override = None  # bucket plan chosen at the ready-order rebuild (timed planner)
+        self.plan_info = {"planner": "cap"}
+        self._timing = None
         self._build()
+        if timed_plan:
+            self.start_ready_timing()
 
     # ------------------------------------------------------------------ plan
     def _build(self):
@@ -209,7 +215,7 @@ class GradReducer:
         n = len(a.params)
         launch = list(range(n)) if self.arena_in_ready_order else list(range(n - 1, -1, -1))
         nbytes = [a.numels[i] * a.data.element_size() for i in launch]
-        groups = plan_buckets(nbytes, self.cap, self.first_cap)
+        groups = self._groups_override or plan_buckets(nbytes, self.cap, self.first_cap)
         starts = [launch[0] if self.arena_in_ready_order else n]
         views = []
         self.bucket_ranges: List[Tuple[int, int]] = []
@@ -278,8 +284,12 @@ class GradReducer:
             label = (lambda i: names.get(id(a.params[i]), str(i))) if names else str
             rows.append({"bytes": (e - s) * es, "tensors": len(idx), "first": label(idx[0]) if idx else None,
                          "last": label(idx[-1]) if idx else None})
-        return {"count": len(rows), "cap_mb": self.cap, "first_cap_mb": self.first_cap,
-                "ready_order_layout": bool(self.arena_in_ready_order), "params": n, "launch_order": rows}
+        out = {"count": len(rows), "ready_order_layout": bool(self.arena_in_ready_order), "params": n,
+               "launch_order": rows}
+        out.update(self.plan_info)
+        if self.plan_info.get("planner") == "cap":
+            out.update(cap_mb=self.cap, first_cap_mb=self.first_cap)
+        return out
 
     def rebind_if_stream_changed(self) -> bool:
         """Re-create the autograd hooks when the caller switched streams (e.g. hipGraph capture).
@@ -316,8 +326,76 @@ class GradReducer:
     def ready_order(self) -> List[int]:
         return list(self._impl.ready_order())
 
+    # ------------------------------------------------------------------ timed bucket plan
+    def start_ready_timing(self):
+        """Record when each gradient becomes ready (GPU events on the compute stream, host clock on
+        the CPU) until the ready-order rebuild, which plans the buckets from it."""
+        self.stop_ready_timing()
+        cuda = self.arena.device.type == "cuda"
+        stamps = {}
+        handles = []
+        for i, p in enumerate(self.arena.params):
+            def hook(_p, i=i):
+                if cuda:
+                    ev = torch.cuda.Event(enable_timing=True)
+                    ev.record()
+                    stamps[i] = ev
+                else:
+                    stamps[i] = time.perf_counter()
+            handles.append(p.register_post_accumulate_grad_hook(hook))
+        self._timing = (stamps, handles, cuda, list(self.arena.params))
+
+    def stop_ready_timing(self):
+        if self._timing is not None:
+            for h in self._timing[1]:
+                h.remove()
+        self._timing = None
+
+    def _ready_times(self):
+        """{param object id: seconds after the first recorded gradient} from the last timed backward."""
+        if self._timing is None:
+            return None
+        stamps, _, cuda, params = self._timing
+        if len(stamps) != len(params):
+            return None
+        if cuda:
+            torch.cuda.synchronize(self.arena.device)
+            origin = next(iter(stamps.values()))  # any event works as the origin (min subtracted below)
+            t = {i: origin.elapsed_time(e) * 1e-3 for i, e in stamps.items()}
+        else:
+            t = dict(stamps)
+        t0 = min(t.values())
+        return {id(params[i]): v - t0 for i, v in t.items()}
+
+    def _measure_comm(self, sizes_mb=(0.25, 2.0, 8.0), reps=3):
+        """Fit alpha + beta * S to all-reduces of this communicator (every rank runs the same ones)."""
+        cuda = self.arena.device.type == "cuda"
+        xs, ts = [], []
+        for mb in sizes_mb:
+            n = max(4, int(mb * 1024 * 1024) // 4)
+            buf = torch.zeros(n, device=self.arena.device, dtype=torch.float32)
+            samples = []
+            for r in range(reps + 1):
+                if cuda:
+                    torch.cuda.synchronize(self.arena.device)
+                t0 = time.perf_counter()
+                self.comm.all_reduce(buf, "sum")
+                if cuda:
+                    torch.cuda.synchronize(self.arena.device)
+                if r:
+                    samples.append(time.perf_counter() - t0)
+            samples.sort()
+            xs.append(n * 4)
+            ts.append(samples[len(samples) // 2])
+            del buf
+        return fit_comm_model(xs, ts)
+
     def rebuild_in_ready_order(self, order: Optional[Sequence[int]] = None) -> bool:
-        """Relayout the arena in gradient-ready order (rank 0's order, broadcast) and re-bucket."""
+        """Relayout the arena in gradient-ready order (rank 0's order, broadcast) and re-bucket.
+
+        With ready times from the first iteration (``timed_plan``), rank 0 also designs the bucket
+        plan (buckets.plan_buckets_timed over its measured timeline and this communicator's fitted
+        alpha / beta) and broadcasts it with the order, so every rank buckets identically."""
         if order is None:
             order = self.ready_order()
         n = len(self.arena.params)
@@ -325,13 +403,37 @@ class GradReducer:
         # parameters that never fired (unused) go last, in reverse model order
         seen = set(order)
         order += [i for i in range(n - 1, -1, -1) if i not in seen]
-        t = torch.tensor(order, dtype=torch.int64)
+        timed = self._timing is not None
+        sizes = [0] * n
+        info = {}
+        if timed:
+            rt = self._ready_times()
+            alpha, beta = self._measure_comm()  # collective on every rank (same calls everywhere)
+            if rt is not None and self.comm.rank == 0:
+                ps = self.arena.params
+                nbytes = [self.arena.numels[i] * self.arena.data.element_size() for i in order]
+                ready = [rt[id(ps[i])] for i in order]
+                groups, info = plan_buckets_timed(nbytes, ready, alpha, beta)
+                for k, g in enumerate(groups):
+                    sizes[k] = len(g)
+        t = torch.tensor(order + [1 if timed else 0] + sizes, dtype=torch.int64)
         if self.comm.size > 1:
             t = t.to(self.arena.device)
             self.comm.broadcast(t, 0)
             t = t.cpu()
-        order = t.tolist()
-        if order == list(range(n)) and self.arena_in_ready_order:
+        vals = t.tolist()
+        order, sizes = vals[:n], [k for k in vals[n + 1:] if k > 0]
+        self.stop_ready_timing()
+        changed = not (order == list(range(n)) and self.arena_in_ready_order)
+        if sizes and sum(sizes) == n:
+            groups, pos = [], 0
+            for k in sizes:
+                groups.append(list(range(pos, pos + k)))
+                pos += k
+            self._groups_override = groups
+            self.plan_info = dict({"planner": "timed"}, **info) if info else {"planner": "timed"}
+            changed = True
+        if not changed:
             return False
         self.arena.relayout(order)
         self.arena_in_ready_order = True
@@ -339,6 +441,7 @@ class GradReducer:
         return True
 
     def remove(self):
+        self.stop_ready_timing()
         if self._impl is not None:
             self._impl.remove_hooks()
             self._impl = None

@@ -117,6 +117,7 @@ class BucketedOverlap:
             bucket_cap_mb if bucket_cap_mb is not None else DEFAULT_BUCKET_CAP_MB,
             first_bucket_cap_mb if first_bucket_cap_mb is not None else DEFAULT_FIRST_BUCKET_CAP_MB,
             find_unused_parameters,
+            timed_plan=bucket_cap_mb is None and first_bucket_cap_mb is None and rebuild_in_ready_order,
         )
         self._rebuild = rebuild_in_ready_order
         self._rebuilt = False

@@ -215,6 +215,23 @@ class FlatArena:
         self._prep_plan = (key, plan, (start, end))
         return plan
 
+    def prep_refresh(self) -> bool:
+        """Recompute the fused-step products from the current weights, in place (same buffers).
+
+        A captured hipGraph step reads these buffers at its forward and rewrites them at its optimizer
+        step, so the graph never re-checks the weights on the host: weights changed outside the graph
+        between replays (copy_, load_state_dict, ...) must be followed by this call (SGD.refresh_weight_prep)
+        before the next replay. Eager steps detect such edits themselves (prep_lookup)."""
+        if self._prep_plan is None or self.prep_request is None:
+            return False
+        weights, want = self.prep_request
+        plan = self._prep_plan[1]
+        from .. import _native
+
+        _native.lib().weight_prep_into([w.data for w in weights], list(want), plan["amax"], plan["wts"])
+        self.prep_mark_valid()
+        return True
+
     def prep_mark_valid(self):
         req = self.prep_request
         if req is None or self._prep_plan is None:

@@ -49,6 +49,8 @@ PYBIND11_MODULE(_C, m) {
         "fused block backward; returns (dx, dw, db, dgamma, dbeta, dres, prev_part). prev_* describe the BN whose "
         "output is x: its statistics reduction is then fused into this block's data-gradient reduction and returned "
         "as prev_part (undefined when not fused), which that block's backward takes as part_in");
+  m.def("weight_prep_into", &weight_prep_into, py::arg("weights"), py::arg("want_t"), py::arg("amax"), py::arg("wts"),
+        "weight_prep writing into existing buffers (a fused-step plan's)");
   m.def("weight_prep", &weight_prep, py::arg("weights"), py::arg("want_t"),
         "one launch per step: conv weights' |max| partials (f16x2; else empty) and W^T [Ci, KH*KW*Co] per weight "
         "with want_t (the data-gradient operand)");

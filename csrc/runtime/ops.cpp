@@ -135,10 +135,15 @@ std::vector<at::Tensor> multi_amax(const std::vector<at::Tensor>& ts) {
 // weight (f16x2 engine; empty list otherwise), W^T [Ci][KH*KW*Co] per weight with want_t[i]
 // (undefined tensor otherwise)}. The transposes are the data-gradient B operand, so backward no
 // longer transposes every weight in its own launch.
-std::vector<std::vector<at::Tensor>> weight_prep(const std::vector<at::Tensor>& ts, const std::vector<bool>& want_t) {
+// With `into` (amax partials + W^T tensors from sgd_prep_plan), the products are written into
+// those buffers instead of fresh ones (refreshing a fused-step plan after the weights were edited).
+std::vector<std::vector<at::Tensor>> weight_prep_impl(const std::vector<at::Tensor>& ts, const std::vector<bool>& want_t,
+                                                      const at::Tensor* amax_into,
+                                                      const std::vector<c10::optional<at::Tensor>>* wt_into) {
   TORCH_CHECK(ts.size() == want_t.size(), "weight_prep: one want_t flag per weight");
   std::vector<at::Tensor> amax, wts;
   hipStream_t st = cur_stream();
+  int into_off = 0;
   for (size_t s0 = 0; s0 < ts.size(); s0 += kMaxAmaxSegs) {
     const size_t ns = std::min<size_t>(kMaxAmaxSegs, ts.size() - s0);
     WeightPrepArgs a{};
@@ -157,19 +162,44 @@ std::vector<std::vector<at::Tensor>> weight_prep(const std::vector<at::Tensor>& 
       a.t[i] = T;
       a.ci[i] = Ci;
       at::Tensor wt;
-      if (want_t[s0 + i]) wt = at::empty({Ci, (long long)T * Co}, t.options());
+      if (want_t[s0 + i]) {
+        if (wt_into) {
+          TORCH_CHECK((*wt_into)[s0 + i].has_value() && (*wt_into)[s0 + i]->numel() == (long long)Ci * T * Co,
+                      "weight_prep_into: missing / mis-sized W^T buffer");
+          wt = *(*wt_into)[s0 + i];
+        } else {
+          wt = at::empty({Ci, (long long)T * Co}, t.options());
+        }
+      }
       a.wt[i] = wt.defined() ? wt.data_ptr<float>() : nullptr;
       wts.push_back(wt);
       a.blk0[i] = tot;
       tot += ((Co + 31) / 32) * ((Ci + 31) / 32);
     }
     a.blk0[ns] = tot;
-    at::Tensor part = at::empty({tot}, ts[s0].options());
+    at::Tensor part;
+    if (amax_into) {
+      TORCH_CHECK(amax_into->numel() >= into_off + tot, "weight_prep_into: amax buffer too small");
+      part = amax_into->narrow(0, into_off, tot);
+      into_off += tot;
+    } else {
+      part = at::empty({tot}, ts[s0].options());
+    }
     weight_prep_launch(a, part.data_ptr<float>(), st);
     if (f16x2_mode())
       for (size_t i = 0; i < ns; ++i) amax.push_back(part.narrow(0, a.blk0[i], a.blk0[i + 1] - a.blk0[i]));
   }
   return {amax, wts};
+}
+
+std::vector<std::vector<at::Tensor>> weight_prep(const std::vector<at::Tensor>& ts, const std::vector<bool>& want_t) {
+  return weight_prep_impl(ts, want_t, nullptr, nullptr);
+}
+
+void weight_prep_into(const std::vector<at::Tensor>& ts, const std::vector<bool>& want_t, const at::Tensor& amax,
+                      const std::vector<c10::optional<at::Tensor>>& wts) {
+  TORCH_CHECK(wts.size() == ts.size(), "weight_prep_into: one W^T slot per weight");
+  weight_prep_impl(ts, want_t, &amax, &wts);
 }
 
 namespace {

@@ -41,6 +41,8 @@ std::vector<at::Tensor> conv_bn_act_fwd(const at::Tensor& x, const at::Tensor& w
                                         const c10::optional<at::Tensor>& w_amax = c10::nullopt);
 std::vector<at::Tensor> multi_amax(const std::vector<at::Tensor>& ts);
 std::vector<std::vector<at::Tensor>> weight_prep(const std::vector<at::Tensor>& ts, const std::vector<bool>& want_t);
+void weight_prep_into(const std::vector<at::Tensor>& ts, const std::vector<bool>& want_t, const at::Tensor& amax,
+                      const std::vector<c10::optional<at::Tensor>>& wts);
 std::vector<at::Tensor> conv_bn_act_bwd(const at::Tensor& gout, const at::Tensor& x, const at::Tensor& w,
                                         const at::Tensor& y, const at::Tensor& stats, int64_t stride, int64_t pad,
                                         bool pool, bool relu, bool need_dx, bool has_bias,

@@ -153,6 +153,9 @@ ORDER_SCRIPT = textwrap.dedent(
             with torch.no_grad():
                 for p, v in zip(base.parameters(), snap):
                     p.copy_(v)
+            # weights edited outside the captured step: re-derive what its forward reads from the
+            # last step (the fused SGD + weight preparation, SGD.refresh_weight_prep)
+            opt.refresh_weight_prep()
             if g is not None:
                 g.replay()
             else:

@@ -3,7 +3,8 @@ one grid) against the two separate launches (CDP_BWD_PAIR=0, read on every call)
 
 * At the VGG-11 layer shapes of the bench (256 images) and of the reference's 8-rank strong-scaling
   point (32 images, /root/reference/src/Part 2a/main.py:22), the pair is really taken (the
-  runtime's launch counter moves), and dX / dW equal the unpaired launches' and torch fp64's.
+  runtime's launch counter moves), and dX / dW equal the unpaired launches' (and, for the
+  unpooled layers, torch fp64's).
 * An NCHW-contiguous input that needs a gradient: the weight-gradient GEMM held back for the pair
   reads a channels_last copy of x and |max| partials made inside the backward call; both must stay
   alive until the paired launch is enqueued (else dX, allocated in between, may reuse their memory).
@@ -87,6 +88,12 @@ def test_paired_gradients_match_separate_launches_and_fp64(monkeypatch, B, layer
     # same tiles, same split-K partition, same reduction order: the pair changes only which
     # workgroup runs which tile
     assert _rel(dx_p, dx_s) <= 1e-6 and _rel(dw_p, dw_s) <= 1e-6, (_rel(dx_p, dx_s), _rel(dw_p, dw_s))
+    if pool:
+        # max-pool backward routes each window's gradient to its argmax: a window whose two largest
+        # values lie within fp32 rounding of each other can pick a different element than fp64
+        # (~1 such window per 2M at 256 images: rel-L2 ~1e-3 for every engine, torch fp32 included
+        # when it happens; scripts/diag/pair_accuracy.py), so fp64 is compared on the unpooled layers
+        return
     dx_r, dw_r = _fp64(x, conv, bn, pool, gy)
     e_dx, e_dw = _rel(dx_p, dx_r.cuda()), _rel(dw_p, dw_r.cuda())
     print(f"B={B} layer {layer}: paired vs fp64 rel-L2 dX {e_dx:.2e} dW {e_dw:.2e}")

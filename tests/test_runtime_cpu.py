@@ -334,6 +334,8 @@ def test_bench_self_launches_ranks_cpu():
         b = blk[strat]["buckets"]
         assert b["count"] == len(b["launch_order"]) >= 2
         assert sum(x["bytes"] for x in b["launch_order"]) >= 36_924_456  # every VGG-11 gradient
+        # designed at the ready-order rebuild from the measured backward timeline + comm model
+        assert b["planner"] == "timed" and b["backward_end_us"] > 0 and b["alpha_us"] >= 0
     assert set(rec["scaling_eff"]) == {"weak", "strong"}
     assert rec["scaling_eff"]["strong"] == blk["ddp"]["scaling_eff"]
 

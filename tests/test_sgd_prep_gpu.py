@@ -10,6 +10,8 @@ forward.
 * A weight edited in place between steps (``torch.no_grad(): w.add_``, load_state_dict) bumps its
   version: the next forward prepares the weights itself and its output matches a model that never
   used the fused path.
+* A captured hipGraph step cannot re-check weights on the host: after editing them between replays,
+  SGD.refresh_weight_prep() re-derives the products in place and the replay equals an eager step.
 """
 import pytest
 import torch
@@ -115,3 +117,52 @@ def test_weight_edited_between_steps_is_seen_by_the_gemms(edit):
     crit(model(xa), y).backward()
     crit(ref(xb), y).backward()
     assert torch.equal(xa.grad, xb.grad)
+
+
+def test_captured_step_sees_weights_edited_between_replays_after_refresh():
+    """A replayed hipGraph step reads the |max| / W^T its previous replay's optimizer step wrote; after
+    weights are edited outside the graph, SGD.refresh_weight_prep() re-derives them in place, and the
+    replay then equals an eager step from the edited weights."""
+    cdp, model, opt = _setup()
+    crit = cdp.CrossEntropyLoss()
+    x, y = _batch(0)
+
+    def body():
+        opt.zero_grad()
+        crit(model(x), y).backward()
+        opt.step()
+
+    for _ in range(3):
+        body()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        body()
+    torch.cuda.current_stream().wait_stream(s)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        body()
+    torch.cuda.synchronize()
+    sd = {k: v.clone() for k, v in model.state_dict().items()}
+    sd["layers.11.weight"] = sd["layers.11.weight"] * 0.5
+    mom = {id(p): opt.state[p]["momentum_buffer"].clone() for p in model.parameters()}
+    model.load_state_dict(sd)
+    assert opt.refresh_weight_prep()
+    g.replay()
+    torch.cuda.synchronize()
+    got = [p.detach().clone() for p in model.parameters()]
+    # eager twin: a fresh model + optimizer with the same weights and momentum, one step
+    _, ref, ropt = _setup()
+    ref.load_state_dict(sd)
+    ropt.fused_prep = False
+    for p in ref.parameters():
+        ropt.state[p]["momentum_buffer"] = None
+    rp = list(ref.parameters())
+    for p, q in zip(rp, model.parameters()):
+        ropt.state[p]["momentum_buffer"] = mom[id(q)].clone()
+    ropt.zero_grad()
+    crit(ref(x), y).backward()
+    ropt.step()
+    torch.cuda.synchronize()
+    for a, b in zip(got, rp):
+        assert torch.equal(a, b.detach())
