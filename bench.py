@@ -154,6 +154,11 @@ class _Run:
             if world > 1 and strategy == "bucketed_overlap":
                 self.sync = cdp.parallel.BucketedOverlap(model, bucket_cap_mb=args.bucket_cap_mb)
             self.opt = cdp.SGD(model.parameters(), lr=0.1, momentum=0.9, weight_decay=1e-4)
+            # A/B hook: the optimizer step without the next forward's weight preparation (a separate
+            # weight_prep launch per forward, as before round 4)
+            self.opt.fused_prep = os.environ.get("CDP_BENCH_NO_FUSED_PREP") != "1"
+            # one batch per step: the SGD kernel advances the loader's step counter
+            self.loader.advance_with(self.opt)
             self.crit = cdp.CrossEntropyLoss()
         else:
             os.environ["CDP_FORCE_REFERENCE"] = "1"

@@ -162,6 +162,7 @@ class DeviceLoader:
         self.dev = dataset.images.device
         self._counter = torch.zeros(1, dtype=torch.int64, device=self.dev)
         self._epoch = 0
+        self._external_advance = False
 
     def _order(self) -> torch.Tensor:
         if self.sampler is not None:
@@ -176,6 +177,16 @@ class DeviceLoader:
     def __len__(self):
         n = len(self.sampler) if self.sampler is not None else len(self.ds)
         return n // self.batch_size if self.drop_last else math.ceil(n / self.batch_size)
+
+    def advance_with(self, optimizer) -> bool:
+        """Let ``optimizer`` advance this loader's step counter inside its step kernel (cdp.SGD
+        ``advance_each_step``) instead of a one-thread launch per batch. One batch per optimizer
+        step only; GPU datasets only (returns False otherwise)."""
+        if self.dev.type != "cuda" or not hasattr(optimizer, "advance_each_step"):
+            return False
+        optimizer.advance_each_step(self._counter)
+        self._external_advance = True
+        return True
 
     @property
     def dataset(self):
@@ -199,7 +210,8 @@ class DeviceLoader:
             target = torch.empty(bsz, dtype=torch.int64, device=self.dev)
             data = C.augment(self.ds.images, idx, offset, bsz, self.ds.mean, self.ds.std, pad, flip, self._counter,
                              self.seed, out, nbatches, self.ds.labels, target)
-            C.counter_inc(self._counter)
+            if not self._external_advance:
+                C.counter_inc(self._counter)
             return data, target
         if nbatches > 0:
             offset += (int(self._counter.item()) % nbatches) * bsz

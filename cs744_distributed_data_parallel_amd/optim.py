@@ -53,6 +53,8 @@ class SGD(Optimizer):
         self._lr_tensor = None
         self._steps = 0
         self.fused_prep = True  # emit the next step's weight preparation from the step (one arena pass)
+        self._step_counter = None  # a device step counter this step advances (DeviceLoader.advance_with)
+        self._counter_pending = None
         all_params = [p for g in self.param_groups for p in g["params"]]
         if flat and all_params and all_params[0].is_cuda:
             self._arena = arena_for(all_params)
@@ -104,6 +106,7 @@ class SGD(Optimizer):
         if closure is not None:
             with torch.enable_grad():
                 loss = closure()
+        self._counter_pending = self._step_counter
         for gi, group in enumerate(self.param_groups):
             params = [p for p in group["params"] if p.grad is not None]
             if not params:
@@ -114,8 +117,21 @@ class SGD(Optimizer):
                 self._step_native(gi, group, params)
             else:
                 self._step_reference(group, params)
+        if self._counter_pending is not None:  # no fused launch took it (per-tensor / reference paths)
+            c = self._counter_pending
+            if c.is_cuda and not _native.force_reference():
+                _native.lib().counter_inc(c)
+            else:
+                c += 1
+            self._counter_pending = None
         self._steps += 1
         return loss
+
+    def advance_each_step(self, counter: torch.Tensor):
+        """Advance ``counter`` (a device int64 step counter, e.g. a DeviceLoader's) by one in every
+        ``step()``, inside the SGD kernel itself: one dispatch less per training step. Only for
+        loops that fetch exactly one batch per optimizer step."""
+        self._step_counter = counter
 
     def _first_flags(self, params):
         firsts = [self.state[p].get("momentum_buffer") is None for p in params]
@@ -190,11 +206,12 @@ class SGD(Optimizer):
         """One launch over the arena range: plain SGD, or SGD that also writes the next forward's
         weight |max| partials and W^T (FlatArena.prep_plan_for) when a model registered them."""
         plan = arena.prep_plan_for(s, e) if self.fused_prep else None
+        ctr, self._counter_pending = self._counter_pending, None
         if plan is None:
-            C.sgd_step(arena.data[s:e], arena.grad[s:e], mom, lr_t, lr, m, damp, wd, 1.0, nest, first, maxim)
+            C.sgd_step(arena.data[s:e], arena.grad[s:e], mom, lr_t, lr, m, damp, wd, 1.0, nest, first, maxim, ctr)
             return
         C.sgd_step_prep(arena.data[s:e], arena.grad[s:e], mom, lr_t, lr, m, damp, wd, 1.0, nest, first, maxim,
-                        plan["desc"], plan["meta"], plan["amax"])
+                        plan["desc"], plan["meta"], plan["amax"], ctr)
         arena.prep_mark_valid()
 
     def _step_reference(self, group, params):

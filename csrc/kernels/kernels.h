@@ -137,7 +137,7 @@ constexpr int kSgdPrepChunk4 = 1024;  // float4 per rest chunk (one workgroup)
 void sgd_prep_launch(float* p, const float* g, float* buf, const SgdPrepSeg* segs, int nseg, int nblk_w,
                      const SgdPrepChunk* chunks, int nchunk, float* amax_part, const float* lr_ptr, float lr,
                      float momentum, float dampening, float wd, float grad_scale, bool nesterov, bool first,
-                     bool maximize, hipStream_t st);
+                     bool maximize, hipStream_t st, long long* counter = nullptr);
 void slab_sum_launch(const float* slab, int S, long long n, float* dst, bool accumulate, hipStream_t st);
 void slab_sum_strided_launch(const float* slab, int S, long long n_src, int src_cols, int dst_cols, float* dst,
                              bool accumulate, hipStream_t st);
@@ -224,9 +224,10 @@ void xent_fwd_launch(const float* logits, const long long* tgt, int B, int C, fl
                      float* sum_out, hipStream_t st);
 void xent_bwd_launch(const float* logits, const long long* tgt, const float* gscale, int B, int C, float* dlogits,
                      hipStream_t st);
+// counter (optional): a step counter the kernel advances by one (DeviceLoader.advance_with)
 void sgd_launch(float* p, const float* g, float* buf, long long n, const float* lr_ptr, float lr, float momentum,
                 float dampening, float wd, float grad_scale, bool nesterov, bool first, bool maximize,
-                hipStream_t st);
+                hipStream_t st, long long* counter = nullptr);
 // nbatches > 0: batch offset idx_off + (counter % nbatches) * B; labels_out[b] = labels[idx[...]] when given
 void augment_launch(const unsigned char* imgs, const long long* idx, long long idx_off, int B, int H, int W, int C,
                     const float* mean, const float* inv_std, int pad, bool flip, const long long* counter,

@@ -135,8 +135,11 @@ __device__ __forceinline__ void sgd_one(float& p, float g, float& b, float lr, f
 
 __global__ __launch_bounds__(256) void sgd_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ buf,
                                                  long long n, const float* __restrict__ lr_ptr, float lr_host, float m,
-                                                 float damp, float wd, float gs, int flags) {
+                                                 float damp, float wd, float gs, int flags, long long* counter) {
   const bool nesterov = flags & 1, first = flags & 2, maximize = flags & 4, has_mom = flags & 8;
+  // a data loader's step counter advanced by the step (one dispatch less per step; the counter is
+  // read by this step's augment kernel, which ran before)
+  if (counter && blockIdx.x == 0 && threadIdx.x == 0) counter[0] += 1;
   const float lr = lr_ptr ? lr_ptr[0] : lr_host;
   const long long n4 = n >> 2;
   const long long stride = (long long)gridDim.x * blockDim.x;
@@ -176,8 +179,9 @@ __global__ __launch_bounds__(256) void sgd_prep_kernel(float* __restrict__ p, co
                                                       int nseg, int nblk_w, const SgdPrepChunk* __restrict__ chunks,
                                                       float* __restrict__ part, const float* __restrict__ lr_ptr,
                                                       float lr_host, float m, float damp, float wd, float gs,
-                                                      int flags) {
+                                                      int flags, long long* counter) {
   constexpr int TG = 9;
+  if (counter && blockIdx.x == 0 && threadIdx.x == 0) counter[0] += 1;  // as sgd_kernel
   __shared__ float tile[TG][32][33];
   __shared__ float red[4];
   const bool nesterov = flags & 1, first = flags & 2, maximize = flags & 4, has_mom = flags & 8;
@@ -688,19 +692,19 @@ void xent_bwd_launch(const float* logits, const long long* tgt, const float* gsc
 }
 void sgd_launch(float* p, const float* g, float* buf, long long n, const float* lr_ptr, float lr, float momentum,
                 float dampening, float wd, float grad_scale, bool nesterov, bool first, bool maximize,
-                hipStream_t st) {
+                hipStream_t st, long long* counter) {
   const int flags = (nesterov ? 1 : 0) | (first ? 2 : 0) | (maximize ? 4 : 0) | (momentum != 0.f ? 8 : 0);
   hipLaunchKernelGGL(sgd_kernel, dim3(grid_for((n + 3) / 4)), dim3(256), 0, st, p, g, buf, n, lr_ptr, lr, momentum,
-                     dampening, wd, grad_scale, flags);
+                     dampening, wd, grad_scale, flags, counter);
 }
 void sgd_prep_launch(float* p, const float* g, float* buf, const SgdPrepSeg* segs, int nseg, int nblk_w,
                      const SgdPrepChunk* chunks, int nchunk, float* amax_part, const float* lr_ptr, float lr,
                      float momentum, float dampening, float wd, float grad_scale, bool nesterov, bool first,
-                     bool maximize, hipStream_t st) {
+                     bool maximize, hipStream_t st, long long* counter) {
   const int flags = (nesterov ? 1 : 0) | (first ? 2 : 0) | (maximize ? 4 : 0) | (momentum != 0.f ? 8 : 0);
   if (nblk_w + nchunk <= 0) return;
   hipLaunchKernelGGL(sgd_prep_kernel, dim3(nblk_w + nchunk), dim3(256), 0, st, p, g, buf, segs, nseg, nblk_w, chunks,
-                     amax_part, lr_ptr, lr, momentum, dampening, wd, grad_scale, flags);
+                     amax_part, lr_ptr, lr, momentum, dampening, wd, grad_scale, flags, counter);
 }
 void augment_launch(const unsigned char* imgs, const long long* idx, long long idx_off, int B, int H, int W, int C,
                     const float* mean, const float* inv_std, int pad, bool flip, const long long* counter,

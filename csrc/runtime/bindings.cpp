@@ -59,10 +59,16 @@ PYBIND11_MODULE(_C, m) {
         py::arg("has_bias"), py::arg("dw_out") = py::none(), py::arg("db_out") = py::none());
   m.def("xent_fwd", &xent_fwd, py::arg("logits"), py::arg("target"), py::arg("correct") = py::none());
   m.def("xent_bwd", &xent_bwd);
-  m.def("sgd_step", &sgd_step);
+  m.def("sgd_step", &sgd_step, py::arg("p"), py::arg("g"), py::arg("buf"), py::arg("lr_t"), py::arg("lr"),
+        py::arg("momentum"), py::arg("dampening"), py::arg("wd"), py::arg("grad_scale"), py::arg("nesterov"),
+        py::arg("first"), py::arg("maximize"), py::arg("counter") = py::none());
   m.def("sgd_prep_plan", &sgd_prep_plan, py::arg("flat"), py::arg("start"), py::arg("end"), py::arg("weights"),
         py::arg("want_t"), "plan of the fused SGD + weight-preparation step over an arena range");
-  m.def("sgd_step_prep", &sgd_step_prep, "SGD over an arena range that also emits the next step's weight |max| / W^T");
+  m.def("sgd_step_prep", &sgd_step_prep, py::arg("p"), py::arg("g"), py::arg("buf"), py::arg("lr_t"), py::arg("lr"),
+        py::arg("momentum"), py::arg("dampening"), py::arg("wd"), py::arg("grad_scale"), py::arg("nesterov"),
+        py::arg("first"), py::arg("maximize"), py::arg("desc"), py::arg("meta"), py::arg("amax"),
+        py::arg("counter") = py::none(),
+        "SGD over an arena range that also emits the next step's weight |max| / W^T");
   m.def("augment", &augment, py::arg("images"), py::arg("indices"), py::arg("idx_offset"), py::arg("batch"),
         py::arg("mean"), py::arg("std"), py::arg("pad"), py::arg("flip"), py::arg("counter"), py::arg("seed"),
         py::arg("out") = py::none(), py::arg("nbatches") = 0, py::arg("labels") = py::none(),

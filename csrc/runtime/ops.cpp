@@ -1360,9 +1360,15 @@ at::Tensor xent_bwd(const at::Tensor& gloss, const at::Tensor& logits_, const at
 }
 
 // ---------------------------------------------------------------- SGD over a flat arena
+long long* counter_ptr(const c10::optional<at::Tensor>& c) {
+  if (!(c.has_value() && c->defined())) return nullptr;
+  TORCH_CHECK(c->is_cuda() && c->scalar_type() == at::kLong && c->numel() >= 1, "step counter must be a device int64");
+  return reinterpret_cast<long long*>(c->data_ptr<int64_t>());
+}
+
 void sgd_step(at::Tensor p, const at::Tensor& g, c10::optional<at::Tensor> buf, const c10::optional<at::Tensor>& lr_t,
               double lr, double momentum, double dampening, double wd, double grad_scale, bool nesterov, bool first,
-              bool maximize) {
+              bool maximize, const c10::optional<at::Tensor>& counter) {
   check_f32_cuda(p, "param");
   TORCH_CHECK(p.is_contiguous() && g.is_contiguous() && p.numel() == g.numel(), "sgd: flat contiguous tensors required");
   float* bp = nullptr;
@@ -1371,7 +1377,8 @@ void sgd_step(at::Tensor p, const at::Tensor& g, c10::optional<at::Tensor> buf, 
     bp = buf->data_ptr<float>();
   }
   sgd_launch(p.data_ptr<float>(), g.data_ptr<float>(), bp, p.numel(), fptr(lr_t), (float)lr, (float)momentum,
-             (float)dampening, (float)wd, (float)grad_scale, nesterov, first, maximize, cur_stream());
+             (float)dampening, (float)wd, (float)grad_scale, nesterov, first, maximize, cur_stream(),
+             counter_ptr(counter));
 }
 
 // ---------------------------------------------------------------- SGD + next-step weight preparation
@@ -1436,7 +1443,8 @@ std::vector<at::Tensor> sgd_prep_plan(const at::Tensor& flat, int64_t s, int64_t
 
 void sgd_step_prep(at::Tensor p, const at::Tensor& g, c10::optional<at::Tensor> buf, const c10::optional<at::Tensor>& lr_t,
                    double lr, double momentum, double dampening, double wd, double grad_scale, bool nesterov, bool first,
-                   bool maximize, const at::Tensor& desc, const at::Tensor& meta, at::Tensor amax) {
+                   bool maximize, const at::Tensor& desc, const at::Tensor& meta, at::Tensor amax,
+                   const c10::optional<at::Tensor>& counter) {
   check_f32_cuda(p, "param");
   TORCH_CHECK(p.is_contiguous() && g.is_contiguous() && p.numel() == g.numel(), "sgd: flat contiguous tensors required");
   float* bp = nullptr;
@@ -1454,7 +1462,7 @@ void sgd_step_prep(at::Tensor p, const at::Tensor& g, c10::optional<at::Tensor> 
   sgd_prep_launch(p.data_ptr<float>(), g.data_ptr<float>(), bp, reinterpret_cast<const SgdPrepSeg*>(d), nseg, nblk,
                   reinterpret_cast<const SgdPrepChunk*>(d + nseg * sizeof(SgdPrepSeg)), nchunk,
                   amax.data_ptr<float>(), fptr(lr_t), (float)lr, (float)momentum, (float)dampening, (float)wd,
-                  (float)grad_scale, nesterov, first, maximize, cur_stream());
+                  (float)grad_scale, nesterov, first, maximize, cur_stream(), counter_ptr(counter));
 }
 
 // ---------------------------------------------------------------- data augmentation

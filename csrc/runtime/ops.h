@@ -70,10 +70,11 @@ std::vector<at::Tensor> sgd_prep_plan(const at::Tensor& flat, int64_t s, int64_t
                                       const std::vector<bool>& want_t);
 void sgd_step_prep(at::Tensor p, const at::Tensor& g, c10::optional<at::Tensor> buf, const c10::optional<at::Tensor>& lr_t,
                    double lr, double momentum, double dampening, double wd, double grad_scale, bool nesterov, bool first,
-                   bool maximize, const at::Tensor& desc, const at::Tensor& meta, at::Tensor amax);
+                   bool maximize, const at::Tensor& desc, const at::Tensor& meta, at::Tensor amax,
+                   const c10::optional<at::Tensor>& counter);
 void sgd_step(at::Tensor p, const at::Tensor& g, c10::optional<at::Tensor> buf, const c10::optional<at::Tensor>& lr_t,
               double lr, double momentum, double dampening, double wd, double grad_scale, bool nesterov, bool first,
-              bool maximize);
+              bool maximize, const c10::optional<at::Tensor>& counter);
 at::Tensor augment(const at::Tensor& images, const c10::optional<at::Tensor>& indices, int64_t idx_offset, int64_t batch,
                    std::vector<double> mean, std::vector<double> std_, int64_t pad, bool flip,
                    const c10::optional<at::Tensor>& counter, int64_t seed, c10::optional<at::Tensor> out,

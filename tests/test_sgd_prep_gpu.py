@@ -166,3 +166,55 @@ def test_captured_step_sees_weights_edited_between_replays_after_refresh():
     torch.cuda.synchronize()
     for a, b in zip(got, rp):
         assert torch.equal(a, b.detach())
+
+
+def test_loader_counter_advanced_by_the_optimizer_step():
+    """DeviceLoader.advance_with(opt): the SGD kernel advances the loader's step counter (no
+    counter_inc launch); the batch sequence and the trained parameters are those of the default
+    path, eager and in a replayed hipGraph."""
+    import cs744_distributed_data_parallel_amd as cdp
+    from cs744_distributed_data_parallel_amd.data import DeviceLoader, synthetic_cifar10
+
+    def run(external, graph):
+        torch.manual_seed(0)
+        model = cdp.VGG11().cuda()
+        opt = cdp.SGD(model.parameters(), lr=0.1, momentum=0.9, weight_decay=1e-4)
+        crit = cdp.CrossEntropyLoss()
+        loader = DeviceLoader(synthetic_cifar10(256, seed=0, device=torch.device("cuda")), 32, shuffle=True)
+        if external:
+            assert loader.advance_with(opt)
+        order = loader._order()
+        labels = []
+
+        def body():
+            x, y = loader.batch(order, 0, 32, nbatches=8)
+            labels.append(y)
+            opt.zero_grad()
+            crit(model(x), y).backward()
+            opt.step()
+
+        for _ in range(3):
+            body()
+        if graph:
+            s = torch.cuda.Stream()
+            s.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(s):
+                body()
+            torch.cuda.current_stream().wait_stream(s)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                body()
+            for _ in range(3):
+                g.replay()
+                labels.append(labels[-1].clone())
+        torch.cuda.synchronize()
+        return [p.detach().clone() for p in model.parameters()], int(loader._counter.item()), labels
+
+    for graph in (False, True):
+        p_ext, c_ext, l_ext = run(True, graph)
+        p_def, c_def, l_def = run(False, graph)
+        assert c_ext == c_def == (3 if not graph else 7)
+        for a, b in zip(l_ext, l_def):
+            assert torch.equal(a, b)
+        for a, b in zip(p_ext, p_def):
+            assert torch.equal(a, b)
