@@ -308,6 +308,8 @@ class GradReducer:
         return True
 
     def prepare_for_backward(self, outputs: Sequence[torch.Tensor]):
+        if self._timing is not None:
+            self._timing[4][0] = True
         self._impl.prepare_for_backward(list(outputs))
 
     def disarm(self):
@@ -334,16 +336,22 @@ class GradReducer:
         cuda = self.arena.device.type == "cuda"
         stamps = {}
         handles = []
+        armed = [False]  # set by prepare_for_backward: only synchronised backwards are timed
+
         for i, p in enumerate(self.arena.params):
             def hook(_p, i=i):
+                if not armed[0]:
+                    return
                 if cuda:
+                    if torch.cuda.is_current_stream_capturing():
+                        return  # a captured step records nothing (and keeps no event nodes)
                     ev = torch.cuda.Event(enable_timing=True)
                     ev.record()
                     stamps[i] = ev
                 else:
                     stamps[i] = time.perf_counter()
             handles.append(p.register_post_accumulate_grad_hook(hook))
-        self._timing = (stamps, handles, cuda, list(self.arena.params))
+        self._timing = (stamps, handles, cuda, list(self.arena.params), armed)
 
     def stop_ready_timing(self):
         if self._timing is not None:
@@ -355,7 +363,7 @@ class GradReducer:
         """{param object id: seconds after the first recorded gradient} from the last timed backward."""
         if self._timing is None:
             return None
-        stamps, _, cuda, params = self._timing
+        stamps, _, cuda, params, _ = self._timing
         if len(stamps) != len(params):
             return None
         if cuda:
