@@ -180,7 +180,9 @@ __global__ __launch_bounds__(256) void sgd_prep_kernel(float* __restrict__ p, co
                                                       float* __restrict__ part, const float* __restrict__ lr_ptr,
                                                       float lr_host, float m, float damp, float wd, float gs,
                                                       int flags, long long* counter) {
-  constexpr int TG = 9;
+  // taps per group: 3 x 3 float4 in flight per thread keeps the kernel near 64 VGPRs (8 waves per
+  // SIMD for this bandwidth-bound pass; a whole 3x3 filter per group held 256 VGPRs, 1 wave per SIMD)
+  constexpr int TG = 3;
   if (counter && blockIdx.x == 0 && threadIdx.x == 0) counter[0] += 1;  // as sgd_kernel
   __shared__ float tile[TG][32][33];
   __shared__ float red[4];
@@ -211,7 +213,6 @@ __global__ __launch_bounds__(256) void sgd_prep_kernel(float* __restrict__ p, co
   const int local = b - sg.blk0;
   const int nci = (Ci + 31) / 32;
   const int co0 = (local / nci) * 32, ci0 = (local % nci) * 32;
-  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 32 x 8
   const unsigned bytes = (unsigned)((long long)Co * T * Ci * 4);
   float* const pw = p + sg.off;
   float* const bw = buf ? buf + sg.off : nullptr;
@@ -219,48 +220,110 @@ __global__ __launch_bounds__(256) void sgd_prep_kernel(float* __restrict__ p, co
   const __amdgpu_buffer_rsrc_t gr = make_rsrc(g + sg.off, bytes);
   const __amdgpu_buffer_rsrc_t br = make_rsrc(has_mom && !first ? bw : pw, bytes);
   float mx = 0.f;
-  for (int t0 = 0; t0 < T; t0 += TG) {
-    float vp[TG][4], vg[TG][4], vb[TG][4];
-    unsigned off[TG][4];
+  if ((Ci & 3) == 0) {
+    // float4 along ci: thread (co row tid / 8, ci quad tid % 8) of the 32 x 32 tile, one (co, tap)
+    // row of 32 ci per 8 threads (128 B), every tap of the group; the transpose goes through LDS
+    // and leaves as float4 runs of 4 co of W^T [ci][tap][co]
+    const int rco = threadIdx.x >> 3, c4 = threadIdx.x & 7;
+    const int co = co0 + rco, ci = ci0 + 4 * c4;
+    const bool ok = co < Co && ci < Ci;
+    for (int t0 = 0; t0 < T; t0 += TG) {
+      float4 vp[TG], vg[TG], vb[TG];
+      unsigned off[TG];
 #pragma unroll
-    for (int q = 0; q < TG; ++q)
-#pragma unroll
-      for (int jj = 0; jj < 4; ++jj) {
-        const int co = co0 + ty + 8 * jj, ci = ci0 + tx, tap = t0 + q;
-        off[q][jj] = (co < Co && ci < Ci && tap < T) ? (unsigned)(((co * T + tap) * Ci + ci) * 4) : kOOB;
-        vp[q][jj] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(pr, (int)off[q][jj], 0, 0));
-        vg[q][jj] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(gr, (int)off[q][jj], 0, 0));
-        vb[q][jj] = has_mom && !first ? __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(br, (int)off[q][jj], 0, 0))
-                                      : 0.f;
+      for (int q = 0; q < TG; ++q) {
+        off[q] = (ok && t0 + q < T) ? (unsigned)(((co * T + t0 + q) * Ci + ci) * 4) : kOOB;
+        vp[q] = bload4(pr, off[q]);
+        vg[q] = bload4(gr, off[q]);
+        vb[q] = has_mom && !first ? bload4(br, off[q]) : f4zero();
       }
 #pragma unroll
-    for (int q = 0; q < TG; ++q)
-#pragma unroll
-      for (int jj = 0; jj < 4; ++jj) {
-        sgd_one(vp[q][jj], vg[q][jj], vb[q][jj], lr, m, damp, wd, gs, nesterov, first, maximize, has_mom);
-        if (off[q][jj] != kOOB) {
-          pw[off[q][jj] >> 2] = vp[q][jj];
-          if (has_mom) bw[off[q][jj] >> 2] = vb[q][jj];
-          mx = fmaxf(mx, fabsf(vp[q][jj]));
+      for (int q = 0; q < TG; ++q) {
+        sgd_one(vp[q].x, vg[q].x, vb[q].x, lr, m, damp, wd, gs, nesterov, first, maximize, has_mom);
+        sgd_one(vp[q].y, vg[q].y, vb[q].y, lr, m, damp, wd, gs, nesterov, first, maximize, has_mom);
+        sgd_one(vp[q].z, vg[q].z, vb[q].z, lr, m, damp, wd, gs, nesterov, first, maximize, has_mom);
+        sgd_one(vp[q].w, vg[q].w, vb[q].w, lr, m, damp, wd, gs, nesterov, first, maximize, has_mom);
+        if (off[q] != kOOB) {
+          st4(pw + (off[q] >> 2), vp[q]);
+          if (has_mom) st4(bw + (off[q] >> 2), vb[q]);
+          mx = fmaxf(mx, fmaxf(fmaxf(fabsf(vp[q].x), fabsf(vp[q].y)), fmaxf(fabsf(vp[q].z), fabsf(vp[q].w))));
         }
       }
-    if (wt) {
+      if (wt) {
+#pragma unroll
+        for (int q = 0; q < TG; ++q) {
+          tile[q][rco][4 * c4] = vp[q].x;
+          tile[q][rco][4 * c4 + 1] = vp[q].y;
+          tile[q][rco][4 * c4 + 2] = vp[q].z;
+          tile[q][rco][4 * c4 + 3] = vp[q].w;
+        }
+        __syncthreads();
+        // thread (ci row tid / 8, co quad tid % 8): W^T[ci][tap][co .. co + 3]
+        const int rci = threadIdx.x >> 3, q4 = threadIdx.x & 7;
+        const int ci_o = ci0 + rci, co_o = co0 + 4 * q4;
+#pragma unroll
+        for (int q = 0; q < TG; ++q) {
+          const int tap = t0 + q;
+          if (tap >= T) break;
+          if (ci_o < Ci && co_o + 3 < Co) {
+            st4(wt + ((long long)ci_o * T + tap) * Co + co_o,
+                make_float4(tile[q][4 * q4][rci], tile[q][4 * q4 + 1][rci], tile[q][4 * q4 + 2][rci],
+                            tile[q][4 * q4 + 3][rci]));
+          } else if (ci_o < Ci) {
+            for (int j = 0; j < 4 && co_o + j < Co; ++j)
+              wt[((long long)ci_o * T + tap) * Co + co_o + j] = tile[q][4 * q4 + j][rci];
+          }
+        }
+        __syncthreads();
+      }
+    }
+  } else {
+    // Ci not a multiple of 4 (an RGB stem's 3 input channels): one element per lane
+    const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 32 x 8
+    for (int t0 = 0; t0 < T; t0 += TG) {
+      float vp[TG][4], vg[TG][4], vb[TG][4];
+      unsigned off[TG][4];
 #pragma unroll
       for (int q = 0; q < TG; ++q)
 #pragma unroll
-        for (int jj = 0; jj < 4; ++jj) tile[q][ty + 8 * jj][tx] = vp[q][jj];
-      __syncthreads();
+        for (int jj = 0; jj < 4; ++jj) {
+          const int co = co0 + ty + 8 * jj, ci = ci0 + tx, tap = t0 + q;
+          off[q][jj] = (co < Co && ci < Ci && tap < T) ? (unsigned)(((co * T + tap) * Ci + ci) * 4) : kOOB;
+          vp[q][jj] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(pr, (int)off[q][jj], 0, 0));
+          vg[q][jj] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(gr, (int)off[q][jj], 0, 0));
+          vb[q][jj] = has_mom && !first
+                          ? __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(br, (int)off[q][jj], 0, 0))
+                          : 0.f;
+        }
 #pragma unroll
-      for (int q = 0; q < TG; ++q) {
-        const int tap = t0 + q;
-        if (tap >= T) break;
+      for (int q = 0; q < TG; ++q)
 #pragma unroll
         for (int jj = 0; jj < 4; ++jj) {
-          const int ci = ci0 + ty + 8 * jj, co = co0 + tx;
-          if (ci < Ci && co < Co) wt[((long long)ci * T + tap) * Co + co] = tile[q][tx][ty + 8 * jj];
+          sgd_one(vp[q][jj], vg[q][jj], vb[q][jj], lr, m, damp, wd, gs, nesterov, first, maximize, has_mom);
+          if (off[q][jj] != kOOB) {
+            pw[off[q][jj] >> 2] = vp[q][jj];
+            if (has_mom) bw[off[q][jj] >> 2] = vb[q][jj];
+            mx = fmaxf(mx, fabsf(vp[q][jj]));
+          }
         }
+      if (wt) {
+#pragma unroll
+        for (int q = 0; q < TG; ++q)
+#pragma unroll
+          for (int jj = 0; jj < 4; ++jj) tile[q][ty + 8 * jj][tx] = vp[q][jj];
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < TG; ++q) {
+          const int tap = t0 + q;
+          if (tap >= T) break;
+#pragma unroll
+          for (int jj = 0; jj < 4; ++jj) {
+            const int ci = ci0 + ty + 8 * jj, co = co0 + tx;
+            if (ci < Ci && co < Co) wt[((long long)ci * T + tap) * Co + co] = tile[q][tx][ty + 8 * jj];
+          }
+        }
+        __syncthreads();
       }
-      __syncthreads();
     }
   }
   mx = wave_max(mx);
