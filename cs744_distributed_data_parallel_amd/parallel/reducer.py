@@ -309,8 +309,22 @@ class GradReducer:
 
     def prepare_for_backward(self, outputs: Sequence[torch.Tensor]):
         if self._timing is not None:
-            self._timing[4][0] = True
+            armed = self._timing[4]
+            if (not armed[0] and self._timing[2] and _native.available()
+                    and not torch.cuda.is_current_stream_capturing()):
+                # the timed backward is eager: at small batches the host enqueues kernels slower than
+                # the GPU runs them, so the events would time the host. A few ms of idle GPU first
+                # lets the host enqueue the whole backward ahead; the events then time the GPU's
+                # back-to-back execution (what a replayed hipGraph step sees). Once per reducer.
+                C = _native.lib()
+                C.gpu_sleep(self.CALIBRATION_SLEEP_US)
+                n = len(self._timing[3])
+                C.gpu_timestamp(self._timing[5], n)  # two back-to-back stamps: the cost of one
+                C.gpu_timestamp(self._timing[5], n + 1)
+            armed[0] = True
         self._impl.prepare_for_backward(list(outputs))
+
+    CALIBRATION_SLEEP_US = 5000.0
 
     def disarm(self):
         self._impl.disarm()
@@ -333,10 +347,15 @@ class GradReducer:
         """Record when each gradient becomes ready (GPU events on the compute stream, host clock on
         the CPU) until the ready-order rebuild, which plans the buckets from it."""
         self.stop_ready_timing()
-        cuda = self.arena.device.type == "cuda"
-        stamps = {}
+        cuda = self.arena.device.type == "cuda" and _native.available()
+        n = len(self.arena.params)
+        stamps = {}  # param index -> host time (CPU) or timestamp slot (GPU)
         handles = []
         armed = [False]  # set by prepare_for_backward: only synchronised backwards are timed
+        # GPU: one device int64 slot per parameter (+ 2 reference stamps) written by a one-thread
+        # kernel reading the GPU wall clock; a timing event would end in a release barrier
+        # (tens of us each on this stack) and stretch the very timeline it measures
+        ts = torch.zeros(n + 2, dtype=torch.int64, device=self.arena.device) if cuda else None
 
         for i, p in enumerate(self.arena.params):
             def hook(_p, i=i):
@@ -344,14 +363,13 @@ class GradReducer:
                     return
                 if cuda:
                     if torch.cuda.is_current_stream_capturing():
-                        return  # a captured step records nothing (and keeps no event nodes)
-                    ev = torch.cuda.Event(enable_timing=True)
-                    ev.record()
-                    stamps[i] = ev
+                        return  # a captured step records nothing
+                    _native.lib().gpu_timestamp(ts, i)
+                    stamps[i] = i
                 else:
                     stamps[i] = time.perf_counter()
             handles.append(p.register_post_accumulate_grad_hook(hook))
-        self._timing = (stamps, handles, cuda, list(self.arena.params), armed)
+        self._timing = (stamps, handles, cuda, list(self.arena.params), armed, ts)
 
     def stop_ready_timing(self):
         if self._timing is not None:
@@ -363,13 +381,19 @@ class GradReducer:
         """{param object id: seconds after the first recorded gradient} from the last timed backward."""
         if self._timing is None:
             return None
-        stamps, _, cuda, params, _ = self._timing
-        if len(stamps) != len(params):
+        stamps, _, cuda, params, _, ts = self._timing
+        n = len(params)
+        if len(stamps) != n:
             return None
         if cuda:
             torch.cuda.synchronize(self.arena.device)
-            origin = next(iter(stamps.values()))  # any event works as the origin (min subtracted below)
-            t = {i: origin.elapsed_time(e) * 1e-3 for i, e in stamps.items()}
+            raw = ts.cpu().tolist()
+            hz = _native.lib().gpu_wall_clock_khz() * 1e3
+            # every stamp is one more dispatch on the stream: subtract the cost of the stamps that
+            # precede each one (the back-to-back reference pair written before backward)
+            per = max(0, raw[n + 1] - raw[n])
+            order = sorted(range(n), key=lambda i: raw[i])
+            t = {i: (raw[i] - k * per) / hz for k, i in enumerate(order)}
         else:
             t = dict(stamps)
         t0 = min(t.values())

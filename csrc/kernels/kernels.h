@@ -247,6 +247,8 @@ constexpr int kMaxStackSrcs = 128;
 void stack_mean_launch(const float* const* srcs, int k, long long n, float* dst, hipStream_t st);
 void scale_launch(float* x, long long n, float a, hipStream_t st);
 void delay_scale_launch(float* x, long long n, float a, double delay_us, hipStream_t st);
+// ts[idx] = the GPU wall clock (100 MHz) when the stream reaches this point
+void timestamp_launch(long long* ts, int idx, hipStream_t st);
 void colsum_launch(const float* x, int R, int C, float* out, bool accumulate, hipStream_t st);
 void small_linear_fwd_launch(const float* x, const float* w, const float* b, int B, int I, int O, float* y,
                              hipStream_t st);

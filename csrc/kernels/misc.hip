@@ -806,6 +806,14 @@ __global__ __launch_bounds__(256) void delay_scale_kernel(float* __restrict__ x,
     x[i] *= a;
 }
 
+// One thread writes the GPU's constant-rate wall clock (s_memrealtime, 100 MHz) into ts[idx]:
+// a stream-ordered timestamp far cheaper than a timing event (which ends in a release barrier).
+__global__ void timestamp_kernel(long long* ts, int idx) { ts[idx] = (long long)wall_clock64(); }
+
+void timestamp_launch(long long* ts, int idx, hipStream_t st) {
+  hipLaunchKernelGGL(timestamp_kernel, dim3(1), dim3(1), 0, st, ts, idx);
+}
+
 void delay_scale_launch(float* x, long long n, float a, double delay_us, hipStream_t st) {
   // s_sleep 127 ~ 127*64 cycles ~ 3.4 us at 2.4 GHz
   const int sleeps = (int)(delay_us / 3.4) + 1;

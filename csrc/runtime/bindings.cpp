@@ -78,6 +78,9 @@ PYBIND11_MODULE(_C, m) {
   m.def("counter_inc", &counter_inc);
   m.def("stack_mean", &stack_mean);
   m.def("scale_", &scale_);
+  m.def("gpu_sleep", &gpu_sleep, py::arg("us"), "idle one workgroup ~us on the current stream");
+  m.def("gpu_wall_clock_khz", &gpu_wall_clock_khz);
+  m.def("gpu_timestamp", &gpu_timestamp, py::arg("ts"), py::arg("idx"), "ts[idx] = GPU wall clock (100 MHz)");
   m.def("maxpool2d_fwd", &maxpool2d_fwd);
   m.def("maxpool2d_bwd", &maxpool2d_bwd);
   m.def("avgpool_fwd", &avgpool_fwd);

@@ -983,6 +983,11 @@ static bool bn_fin_enabled(bool bwd = false) {
   const char* e = std::getenv(bwd ? "CDP_BN_BWD_FIN" : "CDP_BN_FIN_ACT");
   return !(e && e[0] == '0');
 }
+// CDP_BN_*=1 (set explicitly): take the fused path wherever it applies, whatever the batch (tests)
+static bool bn_fin_forced(bool bwd = false) {
+  const char* e = std::getenv(bwd ? "CDP_BN_BWD_FIN" : "CDP_BN_FIN_ACT");
+  return e && e[0] == '1';
+}
 
 std::vector<at::Tensor> conv_bn_act_fwd(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tensor>& b,
                                         const c10::optional<at::Tensor>& gamma,
@@ -1128,9 +1133,14 @@ std::vector<at::Tensor> conv_bn_act_bwd(const at::Tensor& gout_, const at::Tenso
   const bool stem_path = stem_enabled() && !need_dx && training && pool && relu && !zout.defined() && fused_db &&
                          C == 64 && stem_ok(cin, (int)w.size(2), (int)w.size(3), stride, pad, C) &&
                          cin == (int)w.size(1) && (H % 2) == 0 && (W % 2) == 0;
-  // few statistics partials (the deep layers): finalize and apply in one launch (bn_bwd_fin_apply_kernel)
+  // few statistics partials (the deep layers): finalize and apply in one launch (bn_bwd_fin_apply_kernel),
+  // at <= 64 images per GPU. Same-box A/B, hipGraph step, fused vs chan_finalize + bn_bwd_apply
+  // (three interleaved pairs each, round 4): 32 images 0.5394 vs 0.5444 ms (fused 0.9 % faster),
+  // 64 images 0.7135 vs 0.7134 (tie), 128 images 0.9478 vs 0.9458, 256 images 1.3444 vs 1.3411
+  // (the two-launch path 0.2 % faster: its 1024-block apply outruns the fused kernel's
+  // <= 512 blocks that each repeat the partial merge)
   const bool fused_fin = bn_fin_enabled(true) && training && !stem_path && !zout.defined() && (!has_bias || fused_db) &&
-                         bn_bwd_fin_apply_ok(nparts, C, H, W, pool);
+                         bn_bwd_fin_apply_ok(nparts, C, H, W, pool) && (N <= 64 || bn_fin_forced(true));
   if (!fused_fin)
     chan_finalize_launch(part.data_ptr<float>(), nparts, C, sums.data_ptr<float>(), dbeta.data_ptr<float>(),
                          dgamma.data_ptr<float>(), false, st, ps, fused_db ? db.data_ptr<float>() : nullptr,
@@ -1536,6 +1546,25 @@ void stack_mean(const std::vector<at::Tensor>& srcs, at::Tensor dst) {
     ptrs[i] = srcs[i].data_ptr<float>();
   }
   stack_mean_launch(ptrs.data(), k, dst.numel(), dst.data_ptr<float>(), cur_stream());
+}
+
+// one workgroup idles ~us microseconds on the current stream (no memory traffic): lets the host
+// enqueue a whole phase ahead of the GPU, so events recorded in it time the GPU's own execution
+void gpu_sleep(double us) { delay_scale_launch(nullptr, 0, 1.f, us, cur_stream()); }
+
+// frequency of the clock gpu_timestamp reads (kHz)
+int64_t gpu_wall_clock_khz() {
+  int dev = 0, khz = 0;
+  hipGetDevice(&dev);
+  if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev) != hipSuccess || khz <= 0) khz = 100000;
+  return khz;
+}
+
+// ts[idx] = the GPU's wall clock when the current stream reaches this point
+void gpu_timestamp(at::Tensor ts, int64_t idx) {
+  TORCH_CHECK(ts.is_cuda() && ts.scalar_type() == at::kLong && idx >= 0 && idx < ts.numel(),
+              "gpu_timestamp: device int64 buffer and an index inside it");
+  timestamp_launch(reinterpret_cast<long long*>(ts.data_ptr<int64_t>()), (int)idx, cur_stream());
 }
 
 void scale_(at::Tensor x, double a) {

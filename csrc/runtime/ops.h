@@ -82,6 +82,9 @@ at::Tensor augment(const at::Tensor& images, const c10::optional<at::Tensor>& in
                    const c10::optional<at::Tensor>& labels_out = c10::nullopt);
 void counter_inc(at::Tensor c);
 void stack_mean(const std::vector<at::Tensor>& srcs, at::Tensor dst);
+void gpu_sleep(double us);
+void gpu_timestamp(at::Tensor ts, int64_t idx);
+int64_t gpu_wall_clock_khz();
 void scale_(at::Tensor x, double a);
 std::vector<at::Tensor> maxpool2d_fwd(const at::Tensor& x, int64_t k, int64_t s, int64_t p);
 at::Tensor maxpool2d_bwd(const at::Tensor& gy, const at::Tensor& arg, std::vector<int64_t> in_shape, int64_t k,
