@@ -141,6 +141,7 @@ PYBIND11_MODULE(_C, m) {
       .def("remove_hooks", &Reducer::remove_hooks)
       .def("ready_order", &Reducer::ready_order)
       .def("disarm", &Reducer::disarm)
+      .def("set_defer", &Reducer::set_defer)
       .def("set_trace", &Reducer::set_trace)
       .def("trace_log", &Reducer::trace_log)
       .def_property_readonly("iterations", &Reducer::iterations)

@@ -258,8 +258,14 @@ std::shared_ptr<RcclWork> RcclComm::all_reduce(at::Tensor t, const std::string& 
   check_tensor(t);
   std::lock_guard<std::mutex> g(mu_);
   hipStream_t cur = begin();
-  RCCL_CHECK(ncclAllReduce(t.data_ptr(), t.data_ptr(), t.numel(), to_nccl(t.scalar_type()), to_op(op), comm_, stream_));
-  if (postop_delay_us_ > 0.0 || postop_scale_ != 1.0) {
+  // one rank: an in-place all-reduce (and broadcast / reduce below) is the identity, so no RCCL
+  // kernel is issued (the stream ordering and the work object stay). At world size 1 RCCL's
+  // kernels were measured to hold back the compute stream's dispatches for ~50 us each
+  // (scripts/diag/ready_timing.py); the test post-op keeps the collective so its ordering tests run.
+  const bool postop = postop_delay_us_ > 0.0 || postop_scale_ != 1.0;
+  if (world_ > 1 || postop)
+    RCCL_CHECK(ncclAllReduce(t.data_ptr(), t.data_ptr(), t.numel(), to_nccl(t.scalar_type()), to_op(op), comm_, stream_));
+  if (postop) {
     TORCH_CHECK(t.scalar_type() == at::kFloat, "test post-op needs fp32 tensors");
     delay_scale_launch(t.data_ptr<float>(), t.numel(), (float)postop_scale_, postop_delay_us_, stream_);
   }
@@ -270,7 +276,8 @@ std::shared_ptr<RcclWork> RcclComm::broadcast(at::Tensor t, int root, bool async
   check_tensor(t);
   std::lock_guard<std::mutex> g(mu_);
   hipStream_t cur = begin();
-  RCCL_CHECK(ncclBroadcast(t.data_ptr(), t.data_ptr(), t.numel(), to_nccl(t.scalar_type()), root, comm_, stream_));
+  if (world_ > 1)
+    RCCL_CHECK(ncclBroadcast(t.data_ptr(), t.data_ptr(), t.numel(), to_nccl(t.scalar_type()), root, comm_, stream_));
   return end(cur, async, {t}, "broadcast");
 }
 
@@ -278,8 +285,9 @@ std::shared_ptr<RcclWork> RcclComm::reduce(at::Tensor t, int root, const std::st
   check_tensor(t);
   std::lock_guard<std::mutex> g(mu_);
   hipStream_t cur = begin();
-  RCCL_CHECK(ncclReduce(t.data_ptr(), t.data_ptr(), t.numel(), to_nccl(t.scalar_type()), to_op(op), root, comm_,
-                        stream_));
+  if (world_ > 1)
+    RCCL_CHECK(ncclReduce(t.data_ptr(), t.data_ptr(), t.numel(), to_nccl(t.scalar_type()), to_op(op), root, comm_,
+                          stream_));
   return end(cur, async, {t}, "reduce");
 }
 

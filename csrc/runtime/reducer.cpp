@@ -181,7 +181,7 @@ void Reducer::mark_ready_locked(size_t i, bool from_hook) {
     }
   }
   const int b = bucket_of_[i];
-  if (--pending_[b] == 0) {
+  if (--pending_[b] == 0 && !defer_) {
     while (next_launch_ < (int)pending_.size() && pending_[next_launch_] == 0) launch(next_launch_++);
   }
 }
@@ -208,6 +208,8 @@ void Reducer::finalize() {
   std::lock_guard<std::mutex> g(mu_);
   if (!armed_) return;
   if (trace_) log_event("f", -1);
+  if (defer_)
+    while (next_launch_ < (int)pending_.size() && pending_[next_launch_] == 0) launch(next_launch_++);
   if (next_launch_ < (int)pending_.size()) {
     if (find_unused_) {
       for (size_t i = 0; i < params_.size(); ++i) mark_ready_locked(i, false);

@@ -44,6 +44,12 @@ class Reducer {
     std::lock_guard<std::mutex> g(mu_);
     return trace_log_;
   }
+  // defer: hold every bucket's launch until the end-of-backward callback (the reducer's timed
+  // calibration backward, so its ready timeline is the compute's own, free of comm interference)
+  void set_defer(bool on) {
+    std::lock_guard<std::mutex> g(mu_);
+    defer_ = on;
+  }
   void disarm() {
     std::lock_guard<std::mutex> g(mu_);
     armed_ = false;
@@ -72,6 +78,7 @@ class Reducer {
   bool armed_ = false, callback_queued_ = false, record_order_ = true, have_order_ = false;
   int64_t iterations_ = 0, launched_total_ = 0;
   bool trace_ = false;
+  bool defer_ = false;
   bool roctx_ = false;  // CDP_ROCTX=1: roctx range per bucket launch (rocprofv3 --marker-trace)
   std::vector<std::tuple<std::string, int64_t, int64_t>> trace_log_;  // (kind, index, CLOCK_MONOTONIC ns)
   void log_event(const char* kind, int64_t idx);
