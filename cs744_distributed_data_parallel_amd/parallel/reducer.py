@@ -336,6 +336,8 @@ class GradReducer:
         self._impl.prepare_for_backward(list(outputs))
 
     CALIBRATION_SLEEP_US = 5000.0
+    MAX_STAMP_COST_US = 8.0  # two back-to-back stamps: 1.6-2.1 us on MI355X when dispatches are not held
+    stamp_cost_us = None
 
     def disarm(self):
         self._impl.disarm()
@@ -409,7 +411,14 @@ class GradReducer:
             # every stamp is one more dispatch on the stream: subtract the cost of the stamps that
             # precede each one (the back-to-back reference pair written before backward)
             # (capped at 4 us: two back-to-back one-thread kernels measured 1.8-2.1 us on MI355X)
-            per = min(max(0, raw[n + 1] - raw[n]), int(4e-6 * hz))
+            per_raw = max(0, raw[n + 1] - raw[n])
+            self.stamp_cost_us = per_raw / hz * 1e6
+            if self.stamp_cost_us > self.MAX_STAMP_COST_US:
+                # the compute stream did not run its dispatches back to back during the timed
+                # backward (each one waited tens of us): its timeline is not the step's, so no plan
+                # is designed from it (the caller keeps the fixed-cap plan)
+                return None
+            per = min(per_raw, int(4e-6 * hz))
             order = sorted(range(n), key=lambda i: raw[i])
             t = {i: (raw[i] - k * per) / hz for k, i in enumerate(order)}
         else:
@@ -459,6 +468,9 @@ class GradReducer:
         if timed:
             rt = self._ready_times()
             alpha, beta = self._measure_comm()  # collective on every rank (same calls everywhere)
+            if rt is None and self.comm.rank == 0:
+                info = {"fallback": "timeline not measured" if self.stamp_cost_us is None else
+                        f"timeline distorted (back-to-back dispatch {self.stamp_cost_us:.0f} us)"}
             if rt is not None and self.comm.rank == 0:
                 ps = self.arena.params
                 nbytes = [self.arena.numels[i] * self.arena.data.element_size() for i in order]
@@ -475,6 +487,8 @@ class GradReducer:
         order, sizes = vals[:n], [k for k in vals[n + 1:] if k > 0]
         self.stop_ready_timing()
         changed = not (order == list(range(n)) and self.arena_in_ready_order)
+        if timed and not (sizes and sum(sizes) == n) and info:
+            self.plan_info = dict({"planner": "cap"}, **info)  # rank 0's reason (other ranks: cap)
         if sizes and sum(sizes) == n:
             groups, pos = [], 0
             for k in sizes:

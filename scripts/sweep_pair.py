@@ -1,0 +1,163 @@
+"""Tile / split-K sweep of VGG-11's paired gradient launches (bwd_pair: a block's data- and
+weight-gradient GEMMs in one grid) and forward GEMMs, timed inside the whole block.
+
+scripts/sweep_gemm.py times each GEMM alone; in the training step the two gradient GEMMs of a block
+share one launch, so the best pair is not the pair of the best singles (the grid, the wave
+quantisation and the CU residency are shared). For each (batch, layer) this sweeps, by coordinate
+descent from the planner's plans, the data-gradient plan with the weight-gradient plan fixed and
+vice versa (two rounds), timing ``torch.autograd.grad`` of one conv_bn_act block (forward at the
+planner's plan, backward under the override) captured 10x in a hipGraph; then the forward plan alone.
+
+    python scripts/sweep_pair.py [--batches 256,32] [--layers 1,...,7] [--out gpurun_out/sweep_pair.json]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+VGG = [(3, 64, 32), (64, 128, 16), (128, 256, 8), (256, 256, 8), (256, 512, 4), (512, 512, 4), (512, 512, 2),
+       (512, 512, 2)]
+POOL_AFTER = {1, 3, 5, 7}
+TILES = [(256, 128), (128, 128), (128, 64), (64, 128), (64, 64)]
+D_SPLITS = [1, 2, 3, 4, 6, 8, 12, 16]
+W_SPLITS = [1, 2, 3, 4, 6, 8, 12, 16, 24, 32]
+
+
+def time_graph(fn, reps=10, rounds=5):
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        fn()
+    torch.cuda.current_stream().wait_stream(s)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        for _ in range(reps):
+            fn()
+    ts = []
+    for _ in range(rounds):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        g.replay()
+        b.record()
+        b.synchronize()
+        ts.append(a.elapsed_time(b) * 1e3 / reps)
+    g.reset()
+    del g
+    ts.sort()
+    return ts[len(ts) // 2]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batches", default="256,32")
+    ap.add_argument("--layers", default="1,2,3,4,5,6,7")
+    ap.add_argument("--out", default="gpurun_out/sweep_pair.json")
+    ap.add_argument("--no-fwd", action="store_true")
+    ap.add_argument("--engine", default="f16x2", help="f16x2 (paired launches) or x3 (separate launches)")
+    args = ap.parse_args()
+    import cs744_distributed_data_parallel_amd as cdp
+    from cs744_distributed_data_parallel_amd.ops import functional as CF
+
+    C = cdp._native.lib()
+    C.set_conv_gemm(args.engine)
+    results = []
+    for B in [int(b) for b in args.batches.split(",")]:
+        for li in [int(v) for v in args.layers.split(",")]:
+            Ci, Co, HW = VGG[li]
+            torch.manual_seed(li)
+            conv = torch.nn.Conv2d(Ci, Co, 3, padding=1).cuda()
+            conv.weight.data = conv.weight.data.contiguous(memory_format=torch.channels_last)
+            bn = torch.nn.BatchNorm2d(Co).cuda()
+            pool = li in POOL_AFTER
+            x = torch.relu(torch.randn(B, Ci, HW, HW, device="cuda")).contiguous(memory_format=torch.channels_last)
+            x.requires_grad_()
+            oh = HW // 2 if pool else HW
+            gy = torch.randn(B, Co, oh, oh, device="cuda").contiguous(memory_format=torch.channels_last)
+            M = B * HW * HW
+            dshape, wshape, fshape = (M, Ci, 9 * Co), (M, Co, 9 * Ci), (M, Co, 9 * Ci)
+            d_plan = list(C.plan_info("conv", *dshape))
+            w_plan = list(C.plan_info("wgrad", *wshape))
+            f_plan = list(C.plan_info("conv", *fshape))
+            cur = {"d": d_plan, "w": w_plan}
+
+            def block(d, w):
+                def fn():
+                    out = CF.conv_bn_act(x, conv, bn, relu=True, pool=pool)
+                    C.set_gemm_override("conv", *d)
+                    C.set_gemm_override("wgrad", *w)
+                    try:
+                        torch.autograd.grad(out, [x, conv.weight], gy)
+                    finally:
+                        C.set_gemm_override("conv", 0, 0, 0)
+                        C.set_gemm_override("wgrad", 0, 0, 0)
+                return fn
+
+            n0 = C.pair_launches()
+            t_plan = time_graph(block(d_plan, w_plan))
+            paired = C.pair_launches() > n0
+            best = t_plan
+            rows = []
+            kt_d = (dshape[2] + 31) // 32
+            kt_w = (M + 31) // 32
+            for rnd in range(2):
+                for which, splits, kt in (("d", D_SPLITS, kt_d), ("w", W_SPLITS, kt_w)):
+                    for bm, bn in TILES:
+                        if which == "w" and bm == 256 and (wshape[2] % 128 or args.engine != "f16x2"):
+                            continue
+                        for sp in splits:
+                            if sp > max(1, kt // 2):
+                                continue
+                            cand = dict(cur)
+                            cand[which] = [bm, bn, sp]
+                            try:
+                                t = time_graph(block(cand["d"], cand["w"]))
+                            except RuntimeError as e:  # a combination the kernels refuse
+                                print(f"  skip {cand}: {str(e).splitlines()[0]}", flush=True)
+                                continue
+                            rows.append((cand["d"], cand["w"], round(t, 2)))
+                            if t < best * 0.995:
+                                best, cur = t, cand
+            rec = {"engine": args.engine, "B": B, "layer": li, "plan": {"d": d_plan, "w": w_plan}, "paired": paired,
+                   "t_plan_us": round(t_plan, 2), "best": cur, "t_best_us": round(best, 2), "all": rows}
+            print(f"B={B:3d} L{li} bwd plan d{d_plan} w{w_plan} {t_plan:7.2f} us (pair {paired}) | best "
+                  f"d{cur['d']} w{cur['w']} {best:7.2f} us", flush=True)
+            if not args.no_fwd:
+                def fwd(f):
+                    def fn():
+                        C.set_gemm_override("conv", *f)
+                        try:
+                            with torch.no_grad():
+                                CF.conv_bn_act(x, conv, bn, relu=True, pool=pool)
+                        finally:
+                            C.set_gemm_override("conv", 0, 0, 0)
+                    return fn
+
+                tf_plan = time_graph(fwd(f_plan))
+                fb, tf_best = f_plan, tf_plan
+                kt_f = (fshape[2] + 31) // 32
+                for bm, bn in TILES:
+                    for sp in D_SPLITS:
+                        if sp > max(1, kt_f // 2):
+                            continue
+                        t = time_graph(fwd([bm, bn, sp]))
+                        if t < tf_best * 0.995:
+                            fb, tf_best = [bm, bn, sp], t
+                rec.update(f_plan=f_plan, tf_plan_us=round(tf_plan, 2), f_best=fb, tf_best_us=round(tf_best, 2))
+                print(f"B={B:3d} L{li} fwd plan {f_plan} {tf_plan:7.2f} us | best {fb} {tf_best:7.2f} us", flush=True)
+            results.append(rec)
+            with open(args.out, "w") as f:
+                json.dump(results, f)
+    tp = sum(r["t_plan_us"] + r.get("tf_plan_us", 0) for r in results)
+    tb = sum(r["t_best_us"] + r.get("tf_best_us", 0) for r in results)
+    print(f"total planner {tp:.1f} us, best {tb:.1f} us")
+
+
+if __name__ == "__main__":
+    main()
