@@ -11,7 +11,7 @@ Behaviour kept:
   * ``.module``, ``module.``-prefixed ``state_dict``, ``no_sync()``, ``find_unused_parameters``
     (unused parameters raise unless enabled), ``bucket_cap_mb``.
 MI355X specifics: gradients are arena views (zero-copy buckets), the averaging happens inside the
-RCCL collective (ncclAvg), the all-reduce runs on the communicator's own high-priority stream, and
+RCCL collective (ncclAvg), the all-reduce runs on the communicator's own stream, and
 bucket caps default to xGMI-friendly sizes (:mod:`.buckets`).
 """
 from __future__ import annotations

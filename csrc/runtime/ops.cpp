@@ -538,7 +538,37 @@ std::array<int, 3> model_plan(bool wgrad, long long P, long long Q, long long R)
   return best;
 }
 
-GemmPlan plan_gemm(long long M, int Nout, int Kdim) {
+// Plans measured inside the training block where they beat the fitted model's plan: the data- and
+// weight-gradient GEMMs timed together in their paired launch (one grid: its wave quantisation and
+// CU residency are shared, so the best pair is not the pair of the best single launches), the
+// forward with its split-K reduction and BN pass (scripts/sweep_pair.py, hipGraph-timed,
+// profiles/tuning/). kind: 0 forward, 1 data gradient, 2 weight gradient; mode: conv_gemm_mode().
+struct TunedPlan {
+  int kind, mode;
+  long long M;
+  int N, K, bm, bn, splits;
+};
+const std::vector<TunedPlan>& tuned_plans() {
+  static const std::vector<TunedPlan> t = {
+  };
+  return t;
+}
+bool tuned_off() {
+  static const bool off = [] {
+    const char* e = std::getenv("CDP_TUNED_PLANS");
+    return e && e[0] == '0';
+  }();
+  return off;
+}
+const TunedPlan* tuned_plan(int kind, long long M, int N, int K) {
+  if (tuned_off()) return nullptr;
+  const int mode = conv_gemm_mode();
+  for (const auto& t : tuned_plans())
+    if (t.kind == kind && t.mode == mode && t.M == M && t.N == N && t.K == K) return &t;
+  return nullptr;
+}
+
+GemmPlan plan_gemm(long long M, int Nout, int Kdim, int kind = 0) {
   GemmPlan g;
   g.ktiles = (Kdim + 31) / 32;
   g.bn = (Nout % 128 == 0) ? 128 : 64;
@@ -562,6 +592,11 @@ GemmPlan plan_gemm(long long M, int Nout, int Kdim) {
       g.bn = m[1];
       g.splits = m[2];
     }
+  }
+  if (const TunedPlan* t = tuned_plan(kind, M, Nout, Kdim)) {
+    g.bm = t->bm;
+    g.bn = t->bn;
+    g.splits = std::max(1, std::min(t->splits, g.ktiles));
   }
   const PlanOverride& o = conv_override();
   if (o.bm) g.bm = o.bm;
@@ -599,6 +634,11 @@ WgradPlan plan_wgrad(int Cout, int Kdim, long long M) {
       w.bn = m[1];
       w.splits = m[2];
     }
+  }
+  if (const TunedPlan* t = tuned_plan(2, M, Cout, Kdim)) {
+    w.bm = t->bm;
+    w.bn = t->bn;
+    w.splits = std::max(1, std::min(t->splits, mt));
   }
   const PlanOverride& o = wgrad_override();
   if (o.bm) w.bm = o.bm;
@@ -654,11 +694,11 @@ void set_gemm_override(const std::string& kind, int64_t bm, int64_t bn, int64_t 
 }
 
 std::vector<int64_t> plan_info(const std::string& kind, int64_t M, int64_t N, int64_t K) {
-  if (kind == "conv") {
-    const GemmPlan g = plan_gemm(M, (int)N, (int)K);
+  if (kind == "conv" || kind == "dgrad") {
+    const GemmPlan g = plan_gemm(M, (int)N, (int)K, kind == "dgrad" ? 1 : 0);
     return {g.bm, g.bn, g.splits};
   }
-  TORCH_CHECK(kind == "wgrad", "plan_info: kind must be 'conv' or 'wgrad'");
+  TORCH_CHECK(kind == "wgrad", "plan_info: kind must be 'conv', 'dgrad' or 'wgrad'");
   const WgradPlan w = plan_wgrad((int)N, (int)K, M);  // N = Cout, K = Kdim, M = reduction rows
   return {w.bm, w.bn, w.splits};
 }
@@ -766,7 +806,7 @@ bool conv2d_dgrad_subpixel(const at::Tensor& dy, const at::Tensor& w, at::Tensor
       } else {
         p.w = w.data_ptr<float>();  // never read: no K-tiles
       }
-      GemmPlan g = plan_gemm(Mc, C, std::max(Kc, 32));
+      GemmPlan g = plan_gemm(Mc, C, std::max(Kc, 32), 1);
       p.ktiles = (Kc + 31) / 32;
       if (Kc == 0) g.splits = 1;
       p.y = dx.data_ptr<float>();
@@ -815,7 +855,7 @@ at::Tensor dgrad_impl(const at::Tensor& dy_, const at::Tensor& w_, std::vector<i
   at::Tensor dx = has_add ? *addend : at::empty({N, C, H, W}, opts.memory_format(at::MemoryFormat::ChannelsLast));
   const long long M = (long long)N * H * W;
   const int Kdim = KH * KW * Co;
-  GemmPlan g = plan_gemm(M, C, Kdim);
+  GemmPlan g = plan_gemm(M, C, Kdim, 1);
   ConvGemmParams p{};
   p.x = dy.data_ptr<float>();
   p.w = wt.data_ptr<float>();

@@ -100,9 +100,14 @@ RcclComm::RcclComm(const std::string& uid, int rank, int world, int device, doub
   ncclUniqueId id;
   std::memcpy(&id, uid.data(), sizeof(id));
   HIP_CHECK(hipSetDevice(device));
+  // Normal priority. A high-priority stream was measured to throttle the compute stream while it
+  // holds work: VGG-11's 32-image backward ran 2.0-2.2 ms instead of 0.45 ms with one small
+  // kernel per bucket on a high-priority side stream (normal priority: 0.45 ms; one-thread stamp
+  // kernels back to back on the compute stream: ~57 us apart instead of ~2 us;
+  // scripts/diag/queue_prio.py, scripts/diag/ddp_slowdown.py)
   int lo = 0, hi = 0;
   HIP_CHECK(hipDeviceGetStreamPriorityRange(&lo, &hi));
-  HIP_CHECK(hipStreamCreateWithPriority(&stream_, hipStreamNonBlocking, hi));
+  HIP_CHECK(hipStreamCreateWithPriority(&stream_, hipStreamNonBlocking, lo));
   HIP_CHECK(hipEventCreateWithFlags(&start_ev_, hipEventDisableTiming));
   ncclComm_t c = nullptr;
   RCCL_CHECK(ncclCommInitRank(&c, world, id, rank));

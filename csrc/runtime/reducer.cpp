@@ -8,7 +8,7 @@
 //  * autograd post-hooks on the AccumulateGrad nodes (C++, no Python/GIL on the hot path) count
 //    readiness per bucket; a bucket is launched the moment it is complete, strictly in bucket order
 //    so every rank issues the same collective sequence;
-//  * launches go to the RCCL communicator's own high-priority stream (ordered after the compute
+//  * launches go to the RCCL communicator's own stream (ordered after the compute
 //    stream by an event), so the all-reduce of late-layer buckets overlaps the rest of backward;
 //    the end-of-backward callback makes the compute stream wait on the last bucket only (buckets
 //    complete in order on one stream);
