@@ -133,7 +133,10 @@ class _Run:
 
         self.torch, self.cdp = torch, cdp
         self.args, self.world, self.dev, self.local_batch = args, world, dev, local_batch
-        self.sync_grads = sync_grads and world > 1
+        # diagnostic hook: CDP_BENCH_DDP_W1=1 wraps the model in DDP at one rank too (with
+        # CDP_REDUCER_TEST_POSTOP the bucket all-reduces then run real RCCL kernels)
+        self.ddp_w1 = os.environ.get("CDP_BENCH_DDP_W1") == "1" and world == 1
+        self.sync_grads = sync_grads and (world > 1 or self.ddp_w1)
         cdp.utils.seed_everything(0)
         model_name = model_name or args.model
         self.imagenet = model_name.startswith("resnet")
@@ -149,7 +152,7 @@ class _Run:
         self.sync = None
         if args.backend == "native":
             model = cdp.get_model(model_name).to(dev)
-            if world > 1 and strategy == "ddp":
+            if (world > 1 or self.ddp_w1) and strategy == "ddp":
                 model = cdp.DistributedDataParallel(model, bucket_cap_mb=args.bucket_cap_mb)
             if world > 1 and strategy == "bucketed_overlap":
                 self.sync = cdp.parallel.BucketedOverlap(model, bucket_cap_mb=args.bucket_cap_mb)
@@ -457,7 +460,9 @@ def rank_main(args) -> int:
         dev = torch.device("cuda", local)
         if world > 1 and args.dist_backend == "gloo":
             dist.init_process_group("gloo", rank=rank, world_size=world)
-        elif world > 1:
+        elif world > 1 or os.environ.get("CDP_BENCH_DDP_W1") == "1":
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            os.environ.setdefault("MASTER_PORT", "29561")
             # collectives that stall longer than 5 minutes are aborted by the communicator's watchdog
             dist.init_process_group("rccl" if args.backend == "native" else "nccl", rank=rank, world_size=world,
                                     comm_timeout_s=300.0)

@@ -19,7 +19,7 @@ x = torch.randn(B, 3, 32, 32, device="cuda").contiguous(memory_format=torch.chan
 y = torch.randint(0, 10, (B,), device="cuda")
 
 
-def run(name, side=None, every=8, kernel_on_side=False, iters=3):
+def run(name, side=None, every=8, kernel_on_side=False, iters=3, reuse_event=False, poll=False, comm=None):
     torch.manual_seed(0)
     model = cdp.VGG11().cuda()
     opt = cdp.SGD(model.parameters(), lr=0.1, momentum=0.9, weight_decay=1e-4)
@@ -27,17 +27,34 @@ def run(name, side=None, every=8, kernel_on_side=False, iters=3):
     n = len(params)
     ts = torch.zeros(n + 4, dtype=torch.int64, device="cuda")
     buf = torch.zeros(1024, device="cuda")
-    state = {"k": 0, "last": None}
+    state = {"k": 0, "last": None, "work": None, "stop": False}
+    e_shared = torch.cuda.Event()
+    if poll:
+        import threading
+        import time
+
+        def poller():
+            while not state["stop"]:
+                time.sleep(0.02)
+                e = state["last"]
+                if e is not None:
+                    e.query()
+
+        th = threading.Thread(target=poller, daemon=True)
+        th.start()
 
     def hook(_p, i):
         C.gpu_timestamp(ts, i)
-        if side is None:
+        if side is None and comm is None:
             return
         state["k"] += 1
         if state["k"] % every:
             return
+        if comm is not None:
+            state["work"] = comm.all_reduce(buf, "avg", True)
+            return
         cur = torch.cuda.current_stream()
-        e1 = torch.cuda.Event()
+        e1 = e_shared if reuse_event else torch.cuda.Event()
         e1.record(cur)
         side.wait_event(e1)
         if kernel_on_side:
@@ -58,6 +75,9 @@ def run(name, side=None, every=8, kernel_on_side=False, iters=3):
         if state["last"] is not None:
             torch.cuda.current_stream().wait_event(state["last"])
             state["last"] = None
+        if state["work"] is not None:
+            state["work"].wait()
+            state["work"] = None
         opt.step()
         torch.cuda.synchronize()
         r = ts.cpu().tolist()
@@ -65,12 +85,31 @@ def run(name, side=None, every=8, kernel_on_side=False, iters=3):
         us = lambda a, b: (b - a) / hz * 1e6  # noqa: E731
         print(f"{name} iter {it}: back-to-back stamp {us(r[n], r[n + 1]):.1f} us, backward span "
               f"{us(st[0], st[-1]):.0f} us", flush=True)
+    state["stop"] = True
     for h in hooks:
         h.remove()
 
 
 lo, hi = torch.cuda.Stream.priority_range() if hasattr(torch.cuda.Stream, "priority_range") else (0, -1)
 print("priority range", lo, hi)
+WANT = set(sys.argv[1:])
+if WANT:
+    import os
+
+    from cs744_distributed_data_parallel_amd import distributed as dist
+
+    run("plain")
+    run("side stream, normal priority", torch.cuda.Stream(priority=0))
+    run("side stream, reused first event", torch.cuda.Stream(priority=0), reuse_event=True)
+    run("side stream, event polled by a thread", torch.cuda.Stream(priority=0), poll=True)
+    if "comm" in WANT:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29557")
+        dist.init_process_group("rccl", rank=0, world_size=1)
+        run("side stream after RCCL init", torch.cuda.Stream(priority=0))
+        run("native communicator all_reduce (one rank: events only)", comm=dist.native_communicator())
+        run("side stream after RCCL init, again", torch.cuda.Stream(priority=0))
+    sys.exit(0)
 run("plain")
 run("side stream, normal priority", torch.cuda.Stream(priority=0))
 run("side stream, high priority", torch.cuda.Stream(priority=-1))
