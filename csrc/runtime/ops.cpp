@@ -549,7 +549,29 @@ struct TunedPlan {
   int N, K, bm, bn, splits;
 };
 const std::vector<TunedPlan>& tuned_plans() {
+  // {kind, mode, M, N, K, bm, bn, splits}: VGG-11 blocks at the reference's strong-scaling batch
+  // (32 images per GPU) and the headline batch (256); block time planner -> tuned (us, medians of
+  // alternating re-timings, scripts/sweep_pair.py, profiles/tuning/vgg11_pair_sweep_r4.md)
   static const std::vector<TunedPlan> t = {
+      // 32 images, block 1 (64->128 @16): 76.9 -> 74.7
+      {1, 3, 8192, 64, 1152, 128, 64, 3},
+      {2, 3, 8192, 128, 576, 128, 64, 24},
+      // 32 images, block 3 (256->256 @8): backward 98.5 -> 93.2, forward 37.6 -> 36.0
+      {1, 3, 2048, 256, 2304, 64, 128, 4},
+      {2, 3, 2048, 256, 2304, 128, 128, 6},
+      {0, 3, 2048, 256, 2304, 64, 128, 8},
+      // 32 images, block 4 (256->512 @4): 77.7 -> 72.3
+      {1, 3, 512, 256, 4608, 64, 64, 6},
+      // 32 images, block 5 (512->512 @4): 98.3 -> 89.9
+      {1, 3, 512, 512, 4608, 128, 128, 6},
+      // 32 images, blocks 6-7 (512->512 @2): 64.9 -> 62.9
+      {1, 3, 128, 512, 4608, 64, 128, 12},
+      // 256 images, block 4 (256->512 @4): 173.4 -> 166.7
+      {1, 3, 4096, 256, 4608, 256, 128, 3},
+      {2, 3, 4096, 512, 2304, 256, 128, 4},
+      // 256 images, blocks 6-7 (512->512 @2): 122.2 -> 111.4, 120.8 -> 110.4
+      {1, 3, 1024, 512, 4608, 256, 128, 6},
+      {2, 3, 1024, 512, 4608, 256, 128, 2},
   };
   return t;
 }
