@@ -429,6 +429,14 @@ class GradReducer:
     def _measure_comm(self, sizes_mb=(0.25, 2.0, 8.0), reps=3):
         """Fit alpha + beta * S to all-reduces of this communicator (every rank runs the same ones)."""
         cuda = self.arena.device.type == "cuda"
+        # GPU: timed on the GPU wall clock between two stamps on the compute stream around the
+        # (synchronous) collective, after a short GPU sleep so the host is ahead -- the host's
+        # launch-and-synchronize round trip (~100 us) is not part of what overlaps the backward
+        stamped = cuda and _native.available()
+        if stamped:
+            C = _native.lib()
+            hz = C.gpu_wall_clock_khz() * 1e3
+            stamp = torch.zeros(2, dtype=torch.int64, device=self.arena.device)
         xs, ts = [], []
         for mb in sizes_mb:
             n = max(4, int(mb * 1024 * 1024) // 4)
@@ -437,12 +445,21 @@ class GradReducer:
             for r in range(reps + 1):
                 if cuda:
                     torch.cuda.synchronize(self.arena.device)
+                if stamped:
+                    C.gpu_sleep(300.0)
+                    C.gpu_timestamp(stamp, 0)
                 t0 = time.perf_counter()
                 self.comm.all_reduce(buf, "sum")
+                if stamped:
+                    C.gpu_timestamp(stamp, 1)
                 if cuda:
                     torch.cuda.synchronize(self.arena.device)
                 if r:
-                    samples.append(time.perf_counter() - t0)
+                    if stamped:
+                        a, b = stamp.tolist()
+                        samples.append(max(0, b - a) / hz)
+                    else:
+                        samples.append(time.perf_counter() - t0)
             samples.sort()
             xs.append(n * 4)
             ts.append(samples[len(samples) // 2])

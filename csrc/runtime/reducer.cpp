@@ -208,8 +208,17 @@ void Reducer::finalize() {
   std::lock_guard<std::mutex> g(mu_);
   if (!armed_) return;
   if (trace_) log_event("f", -1);
-  if (defer_)
+  if (defer_) {
+    // the timed calibration backward: the bucket launches wait for the GPU to finish it. A
+    // collective enqueued while the GPU still runs the backward (the host is ahead of it) was
+    // measured to stretch that backward ~6x on MI355X, even at one rank with no RCCL kernel
+    // (scripts/diag/queue_prio.py: 0.36 -> 1.9-2.3 ms at 32 images), and it is the
+    // compute-only timeline the bucket planner needs
+    if (!bucket_views_.empty() && bucket_views_[0].is_cuda())
+      TORCH_CHECK(hipStreamSynchronize(c10::hip::getCurrentHIPStream().stream()) == hipSuccess,
+                  "reducer: stream synchronize failed");
     while (next_launch_ < (int)pending_.size() && pending_[next_launch_] == 0) launch(next_launch_++);
+  }
   if (next_launch_ < (int)pending_.size()) {
     if (find_unused_) {
       for (size_t i = 0; i < params_.size(); ++i) mark_ready_locked(i, false);

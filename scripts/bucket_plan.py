@@ -1,5 +1,5 @@
 """Bucket plan of the reducer for one batch size (one GPU, DDP over the native RCCL communicator at
-W = 1): the measured gradient-ready timeline of an eager backward (GPU events per parameter hook,
+W = 1): the measured gradient-ready timeline of an eager backward (GPU stamps per parameter hook,
 what the reducer's timed planner records at its ready-order rebuild), and the plan
 buckets.plan_buckets_timed designs from it for several xGMI comm models -- the W = 1 fit (no data
 moves), and the W = 8 ring (2 (W-1)/W S bytes per GPU) at assumed bus bandwidths / latencies.
@@ -49,9 +49,11 @@ alpha1, beta1 = red._measure_comm()
 red.stop_ready_timing()
 
 print(f"# VGG-11 bucket plan at {B} images per GPU (round 4, `scripts/bucket_plan.py {B}`)\n")
-print("Gradient-ready timeline of one eager backward on one MI355X (GPU events recorded by the "
-      "reducer's per-parameter hooks; us after the first gradient). Eager launches add host gaps, so "
-      "the hipGraph step's backward is shorter; the shape of the timeline is what the planner uses.\n")
+print("Gradient-ready timeline of the reducer's timed calibration backward on one MI355X (GPU "
+      "wall-clock stamps written by the per-parameter hooks; us after the first gradient). A 5 ms GPU "
+      "sleep before it lets the host enqueue the whole backward ahead, so the GPU runs it back to back "
+      "as in the captured step; its bucket launches wait for its end (Reducer::finalize). The "
+      "communicator fit times each all-reduce between two GPU stamps on the compute stream.\n")
 print("| # | parameter | bytes | ready us |\n|---|---|---|---|")
 for i, k in enumerate(order):
     print(f"| {i} | `{names.get(k, '?')}` | {nb[i]} | {ready[i] * 1e6:.1f} |")
