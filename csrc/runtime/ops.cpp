@@ -993,6 +993,7 @@ at::Tensor conv2d_wgrad_keep(const at::Tensor& dy, const at::Tensor& x, std::vec
 
 // ---------------------------------------------------------------- RGB stem (stem.hip)
 bool stem_enabled() { return true; }
+static bool bn_fin_enabled(bool bwd);
 
 // Training-mode conv + BN + act [+ pool] of a Cin <= 4 stem; same outputs as conv_bn_act_fwd with
 // x saved unpadded (xsave = x) and no f16x2 maxima for x / W (the stem kernels need none).
@@ -1019,15 +1020,26 @@ std::vector<at::Tensor> stem_bn_act_fwd(const at::Tensor& x_, const at::Tensor& 
   long long* nbt = nullptr;
   if (num_batches_tracked.has_value() && num_batches_tracked->defined())
     nbt = reinterpret_cast<long long*>(num_batches_tracked->data_ptr<int64_t>());
-  bn_finalize_launch(part.data_ptr<float>(), nparts, 256, (int)M, Co, fptr(gamma), fptr(beta),
-                     fptr_mut(running_mean), fptr_mut(running_var), nbt, (float)momentum, (float)eps,
-                     stats.data_ptr<float>(), st);
+  // up to 128 images (<= 512 partials of 256 rows) finalize and apply in one launch, as the
+  // deeper blocks do (one dispatch fewer at the strong-scaling batches)
+  const bool fused = bn_fin_enabled(false) && bn_fin_act_ok(nparts, Co, false);
+  if (!fused)
+    bn_finalize_launch(part.data_ptr<float>(), nparts, 256, (int)M, Co, fptr(gamma), fptr(beta),
+                       fptr_mut(running_mean), fptr_mut(running_var), nbt, (float)momentum, (float)eps,
+                       stats.data_ptr<float>(), st);
   at::Tensor out = at::empty({N, Co, pool ? H / 2 : H, pool ? W / 2 : W},
                              opts.memory_format(at::MemoryFormat::ChannelsLast));
   at::Tensor out_amax;
-  if (f16x2_mode()) out_amax = at::empty({bn_act_grid(N, H, W, Co, pool)}, opts);
-  bn_act_fwd_launch(y.data_ptr<float>(), stats.data_ptr<float>(), nullptr, out.data_ptr<float>(), N, H, W, Co, pool,
-                    relu, st, out_amax.defined() ? out_amax.data_ptr<float>() : nullptr);
+  if (f16x2_mode())
+    out_amax = at::empty({fused ? bn_fin_act_grid(N, H, W, Co, pool, nparts) : bn_act_grid(N, H, W, Co, pool)}, opts);
+  float* amax_p = out_amax.defined() ? out_amax.data_ptr<float>() : nullptr;
+  if (fused)
+    bn_fin_act_launch(part.data_ptr<float>(), nparts, 256, Co, fptr(gamma), fptr(beta), fptr_mut(running_mean),
+                      fptr_mut(running_var), nbt, (float)momentum, (float)eps, stats.data_ptr<float>(),
+                      y.data_ptr<float>(), out.data_ptr<float>(), N, H, W, pool, relu, amax_p, st);
+  else
+    bn_act_fwd_launch(y.data_ptr<float>(), stats.data_ptr<float>(), nullptr, out.data_ptr<float>(), N, H, W, Co, pool,
+                      relu, st, amax_p);
   return {out, y, stats, x, out_amax, at::Tensor(), at::Tensor()};
 }
 
