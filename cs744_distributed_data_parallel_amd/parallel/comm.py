@@ -4,7 +4,7 @@ Two interchangeable implementations of one small interface:
 
 * :class:`RcclCommunicator` -- the native C++ RCCL communicator (``_C.RcclComm``): one per GPU,
   bootstrapped from the ``torch.distributed`` TCP store (the reference's env:// rendezvous,
-  ``/root/reference/src/Part 2a/main.py:148-152``), own (normal-priority) HIP stream, stream-ordered
+  ``/root/reference/src/Part 2a/main.py:148-152``), own comm stream (a PyTorch pool stream), stream-ordered
   (hipGraph-capturable) collectives, watchdog-based failure detection.
 * :class:`TorchCommunicator` -- any ``torch.distributed`` process group (gloo for the CPU
   test-suite and CPU runs; nccl=RCCL as an alternative GPU path).

@@ -100,14 +100,14 @@ RcclComm::RcclComm(const std::string& uid, int rank, int world, int device, doub
   ncclUniqueId id;
   std::memcpy(&id, uid.data(), sizeof(id));
   HIP_CHECK(hipSetDevice(device));
-  // Normal priority. A high-priority stream was measured to throttle the compute stream while it
-  // holds work: VGG-11's 32-image backward ran 2.0-2.2 ms instead of 0.45 ms with one small
-  // kernel per bucket on a high-priority side stream (normal priority: 0.45 ms; one-thread stamp
-  // kernels back to back on the compute stream: ~57 us apart instead of ~2 us;
-  // scripts/diag/queue_prio.py, scripts/diag/ddp_slowdown.py)
-  int lo = 0, hi = 0;
-  HIP_CHECK(hipDeviceGetStreamPriorityRange(&lo, &hi));
-  HIP_CHECK(hipStreamCreateWithPriority(&stream_, hipStreamNonBlocking, lo));
+  // The comm stream is one of PyTorch's low-priority pool streams, not a stream created here.
+  // Measured on MI355X (VGG-11 eager backward at 32 images, a collective per ~8 gradients at one
+  // rank, scripts/diag/queue_prio.py + comm_diag runs): with a stream of our own -- created with
+  // hipStreamCreateWithPriority before or after RCCL init, or as a full-CU-mask stream -- the
+  // backward took 1.3-4.0 ms instead of 0.36-0.42 ms (compute dispatches ~57 us apart); on a pool
+  // stream it took 0.40-0.42 ms, and a 300 us kernel per collective on the comm stream still fully
+  // overlapped it. A high-priority stream holding work throttled compute as well (0.45 -> 2-3 ms).
+  stream_ = c10::hip::getStreamFromPool(/*isHighPriority=*/false, (c10::DeviceIndex)device).stream();
   HIP_CHECK(hipEventCreateWithFlags(&start_ev_, hipEventDisableTiming));
   ncclComm_t c = nullptr;
   RCCL_CHECK(ncclCommInitRank(&c, world, id, rank));
@@ -139,8 +139,7 @@ RcclComm::~RcclComm() {
     for (auto e : free_events_) hipEventDestroy(e);
     free_events_.clear();
   }
-  if (start_ev_) hipEventDestroy(start_ev_);
-  if (stream_) hipStreamDestroy(stream_);
+  if (start_ev_) hipEventDestroy(start_ev_);  // stream_ belongs to PyTorch's pool
 }
 
 std::string RcclComm::error() const {
