@@ -549,9 +549,9 @@ struct TunedPlan {
   int N, K, bm, bn, splits;
 };
 const std::vector<TunedPlan>& tuned_plans() {
-  // {kind, mode, M, N, K, bm, bn, splits}: VGG-11 blocks at the reference's strong-scaling batch
-  // (32 images per GPU) and the headline batch (256); block time planner -> tuned (us, medians of
-  // alternating re-timings, scripts/sweep_pair.py, profiles/tuning/vgg11_pair_sweep_r4.md)
+  // {kind, mode, M, N, K, bm, bn, splits}: VGG-11 blocks at the reference's strong-scaling batches
+  // (32 / 64 / 128 images per GPU) and the headline batch (256); block time planner -> tuned (us,
+  // medians of alternating re-timings, scripts/sweep_pair.py, profiles/tuning/vgg11_pair_sweep_r4.md)
   static const std::vector<TunedPlan> t = {
       // 32 images, block 1 (64->128 @16): 76.9 -> 74.7
       {1, 3, 8192, 64, 1152, 128, 64, 3},
@@ -566,6 +566,35 @@ const std::vector<TunedPlan>& tuned_plans() {
       {1, 3, 512, 512, 4608, 128, 128, 6},
       // 32 images, blocks 6-7 (512->512 @2): 64.9 -> 62.9
       {1, 3, 128, 512, 4608, 64, 128, 12},
+      // 128 images, block 1 (64->128 @16): backward 143.9 -> 128.7, forward 49.4 -> 47.9
+      {1, 3, 32768, 64, 1152, 128, 64, 1},
+      {2, 3, 32768, 128, 576, 128, 64, 24},
+      {0, 3, 32768, 128, 576, 128, 64, 1},
+      // 128 images, block 2 (128->256 @8): 133.7 -> 125.2
+      {1, 3, 8192, 128, 2304, 256, 128, 3},
+      {2, 3, 8192, 256, 1152, 256, 128, 12},
+      // 128 images, block 4 (256->512 @4): 127.7 -> 117.0
+      {1, 3, 2048, 256, 4608, 256, 128, 6},
+      {2, 3, 2048, 512, 2304, 256, 128, 4},
+      // 128 images, blocks 6-7 forward (512->512 @2): 35.7 -> 34.7
+      {0, 3, 512, 512, 4608, 64, 128, 8},
+      // 64 images, block 1: backward 100.9 -> 92.1
+      {1, 3, 16384, 64, 1152, 64, 64, 1},
+      {2, 3, 16384, 128, 576, 128, 64, 24},
+      // 64 images, block 2: backward 101.7 -> 95.7, forward 40.5 -> 35.0
+      {1, 3, 4096, 128, 2304, 64, 128, 3},
+      {2, 3, 4096, 256, 1152, 128, 128, 12},
+      {0, 3, 4096, 256, 1152, 64, 64, 1},
+      // 64 images, block 3: backward 124.8 -> 115.2
+      {1, 3, 4096, 256, 2304, 256, 128, 3},
+      {2, 3, 4096, 256, 2304, 256, 128, 8},
+      // 64 images, block 4: backward 99.5 -> 92.7, forward 35.9 -> 34.5
+      {1, 3, 1024, 256, 4608, 64, 128, 6},
+      {2, 3, 1024, 512, 2304, 64, 64, 1},
+      {0, 3, 1024, 512, 2304, 64, 128, 4},
+      // 64 images, blocks 6-7: backward 78.0 -> 72.2, forward 30.3 -> 29.6
+      {1, 3, 256, 512, 4608, 64, 128, 6},
+      {0, 3, 256, 512, 4608, 64, 128, 16},
       // 256 images, block 4 (256->512 @4): 173.4 -> 166.7
       {1, 3, 4096, 256, 4608, 256, 128, 3},
       {2, 3, 4096, 512, 2304, 256, 128, 4},
