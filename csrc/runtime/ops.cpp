@@ -595,6 +595,23 @@ const std::vector<TunedPlan>& tuned_plans() {
       // 64 images, blocks 6-7: backward 78.0 -> 72.2, forward 30.3 -> 29.6
       {1, 3, 256, 512, 4608, 64, 128, 6},
       {0, 3, 256, 512, 4608, 64, 128, 16},
+      // ResNet-50, 64 images at 224x224 (scripts/sweep_resnet.py, per GEMM, >= 4 % faster):
+      // forward 256->512 1x1/2 @56 82.9 -> 76.6, 256->128 1x1 @56 94.1 -> 87.5, 128->512 1x1 @28
+      // 61.7 -> 57.2, 1024->256 1x1 @14 37.8 -> 35.8, 64->64 1x1 @56 28.1 -> 26.9
+      {0, 3, 50176, 512, 256, 128, 128, 1},
+      {0, 3, 200704, 128, 256, 128, 128, 1},
+      {0, 3, 50176, 512, 128, 64, 128, 1},
+      {0, 3, 12544, 256, 1024, 64, 128, 1},
+      {0, 3, 200704, 64, 64, 64, 64, 1},
+      // data gradients of 256->64 @56 70.4 -> 65.9, 256->128 @56 111.7 -> 105.4, 512->128 @28
+      // 54.8 -> 48.9, 512->256 @28 77.5 -> 69.5, 256->1024 @14 36.7 -> 34.2 (all 1x1)
+      {1, 3, 200704, 256, 64, 128, 128, 1},
+      {1, 3, 200704, 256, 128, 128, 128, 1},
+      {1, 3, 50176, 512, 128, 64, 128, 1},
+      {1, 3, 50176, 512, 256, 128, 128, 1},
+      {1, 3, 12544, 256, 1024, 64, 128, 1},
+      // weight gradient of 512->128 1x1 @28: 42.5 -> 39.3
+      {2, 3, 50176, 128, 512, 128, 128, 64},
       // 256 images, block 4 (256->512 @4): 173.4 -> 166.7
       {1, 3, 4096, 256, 4608, 256, 128, 3},
       {2, 3, 4096, 512, 2304, 256, 128, 4},
