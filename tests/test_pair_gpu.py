@@ -1,10 +1,11 @@
 """The paired gradient launch (csrc/kernels/bwd_pair.h: a block's data- and weight-gradient GEMMs in
 one grid) against the two separate launches (CDP_BWD_PAIR=0, read on every call) and against fp64.
 
-* At the VGG-11 layer shapes of the bench (256 images) and of the reference's 8-rank strong-scaling
-  point (32 images, /root/reference/src/Part 2a/main.py:22), the pair is really taken (the
-  runtime's launch counter moves), and dX / dW equal the unpaired launches' (and, for the
-  unpooled layers, torch fp64's).
+* At the VGG-11 layer shapes of the bench (256 images) and of the reference's strong-scaling
+  points (128 / 64 / 32 images at W = 2 / 4 / 8, /root/reference/src/Part 2a/main.py:22) -- each
+  under its plans, the tuned-plan table's included -- the pair is really taken (the runtime's
+  launch counter moves), and dX / dW equal the unpaired launches' (and, for the unpooled layers,
+  torch fp64's).
 * An NCHW-contiguous input that needs a gradient: the weight-gradient GEMM held back for the pair
   reads a channels_last copy of x and |max| partials made inside the backward call; both must stay
   alive until the paired launch is enqueued (else dX, allocated in between, may reuse their memory).
@@ -68,7 +69,7 @@ def _rel(a, b):
     return ((a.double() - b.double()).norm() / b.double().norm()).item()
 
 
-@pytest.mark.parametrize("B", [256, 32])
+@pytest.mark.parametrize("B", [256, 128, 64, 32])
 @pytest.mark.parametrize("layer", range(1, 8))
 def test_paired_gradients_match_separate_launches_and_fp64(monkeypatch, B, layer):
     lib = _lib()
@@ -127,3 +128,21 @@ def test_held_weight_gradient_keeps_its_nchw_input_alive(monkeypatch):
     assert _rel(dx_p, dx_s) <= 1e-6 and _rel(dw_p, dw_s) <= 1e-6, (_rel(dx_p, dx_s), _rel(dw_p, dw_s))
     dx_r, dw_r = _fp64(x, conv, bn, False, gy, relu=False)
     assert _rel(dw_p, dw_r.cuda()) <= 1e-5 and _rel(dx_p, dx_r.cuda()) <= 1e-5
+
+
+def test_tuned_plans_are_the_planners_choice():
+    """The tuned-plan table (csrc/runtime/ops.cpp, tuned_plans()) is what the planner returns for its
+    shapes, per GEMM kind: VGG-11 block 5 at 32 images (512->512 at 4x4: M = 512, K = 4608) takes
+    128x128 data-gradient tiles over 6 splits while its forward GEMM of the same M, N, K keeps the
+    fitted model's plan."""
+    lib = _lib()
+    orig = lib.get_conv_gemm()
+    try:
+        lib.set_conv_gemm("f16x2")
+        assert list(lib.plan_info("dgrad", 512, 512, 4608)) == [128, 128, 6]
+        assert list(lib.plan_info("conv", 512, 512, 4608)) != [128, 128, 6]
+        assert list(lib.plan_info("wgrad", 4096, 512, 2304)) == [256, 128, 4]
+        lib.set_conv_gemm("x3")  # the table is per engine: x3 keeps its planner's plans
+        assert list(lib.plan_info("dgrad", 512, 512, 4608)) == list(lib.plan_info("conv", 512, 512, 4608))
+    finally:
+        lib.set_conv_gemm(orig)
