@@ -100,3 +100,53 @@ def test_comm_model_fit_recovers_alpha_beta():
     sizes = [2 ** 18, 2 ** 21, 2 ** 23]
     a, b = fit_comm_model(sizes, [12e-6 + s * 4e-12 for s in sizes])
     assert abs(a - 12e-6) < 1e-9 and abs(b - 4e-12) < 1e-15
+
+
+class _FakeLib:
+    @staticmethod
+    def gpu_wall_clock_khz():
+        return 100_000.0  # 100 MHz: 100 ticks per us
+
+
+def _timed_reducer(monkeypatch, stamp_cost_us):
+    """A GradReducer over a small CPU model whose last timed backward is faked as a GPU record:
+    parameters ready 10 us apart in reverse order, and the two back-to-back reference stamps
+    stamp_cost_us apart."""
+    import torch
+
+    from cs744_distributed_data_parallel_amd.parallel import reducer as R
+    from cs744_distributed_data_parallel_amd.parallel.local import LocalGroup
+    from cs744_distributed_data_parallel_amd.utils.arena import arena_for
+
+    model = torch.nn.Sequential(torch.nn.Linear(8, 16), torch.nn.ReLU(), torch.nn.Linear(16, 4))
+    params = list(model.parameters())
+    red = R.GradReducer(arena_for(params), LocalGroup(1).communicator(0), timed_plan=True)
+    n = len(params)
+    ticks = [1000 + 1000 * (n - 1 - i) for i in range(n)] + [0, int(stamp_cost_us * 100)]
+    red.stop_ready_timing()
+    red._timing = ({i: i for i in range(n)}, [], True, params, [True], torch.tensor(ticks, dtype=torch.int64))
+    monkeypatch.setattr(R._native, "lib", lambda: _FakeLib)
+    monkeypatch.setattr(R.torch.cuda, "synchronize", lambda *a, **k: None)
+    monkeypatch.setattr(R.GradReducer, "_measure_comm", lambda self, *a, **k: (20e-6, 1e-12))
+    return red, params
+
+
+def test_calibration_stamps_give_the_ready_timeline(monkeypatch):
+    red, params = _timed_reducer(monkeypatch, 2.0)
+    rt = red._ready_times()
+    assert rt is not None and abs(red.stamp_cost_us - 2.0) < 1e-9
+    # ready 10 us apart, minus the 2 us each preceding stamp adds: 8 us apart
+    got = sorted(rt[id(p)] for p in params)
+    assert all(abs((b - a) - 8e-6) < 1e-12 for a, b in zip(got, got[1:]))
+    assert red.rebuild_in_ready_order(list(range(len(params)))[::-1])
+    assert red.plan_info["planner"] == "timed"
+
+
+def test_distorted_calibration_timeline_keeps_the_cap_plan(monkeypatch):
+    """Dispatches ~50 us apart during the timed backward (the stream was held back): no plan is
+    designed from that timeline; the reducer keeps the fixed-cap plan and says why."""
+    red, params = _timed_reducer(monkeypatch, 50.0)
+    assert red._ready_times() is None
+    red.rebuild_in_ready_order(list(range(len(params)))[::-1])
+    assert red.plan_info["planner"] == "cap"
+    assert "distorted" in red.plan_info["fallback"]
