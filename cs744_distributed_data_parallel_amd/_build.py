@@ -61,6 +61,8 @@ def write_ninja() -> str:
     hipcc = _hipcc()
     os.makedirs(BUILD_DIR, exist_ok=True)
     kflags = f"--offload-arch={ARCH} -O3 -fPIC -std=c++17 -ffp-contract=fast -Wno-unused-result"
+    if os.environ.get("CDP_KFLAGS_EXTRA"):  # extra kernel flags for A/B builds (e.g. -DCDP_INTERLEAVE_VPM=2)
+        kflags += " " + os.environ["CDP_KFLAGS_EXTRA"]
     rflags = " ".join(
         [
             f"--offload-arch={ARCH} -O2 -fPIC -std=c++17 -w",
