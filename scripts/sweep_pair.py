@@ -70,12 +70,14 @@ def main():
     ap.add_argument("--out", default="gpurun_out/sweep_pair.json")
     ap.add_argument("--no-fwd", action="store_true")
     ap.add_argument("--engine", default="f16x2", help="f16x2 (paired launches) or x3 (separate launches)")
+    ap.add_argument("--wsplits", default=None, help="weight-gradient split counts to try (comma list)")
     args = ap.parse_args()
     import cs744_distributed_data_parallel_amd as cdp
     from cs744_distributed_data_parallel_amd.ops import functional as CF
 
     C = cdp._native.lib()
     C.set_conv_gemm(args.engine)
+    w_splits = [int(v) for v in args.wsplits.split(",")] if args.wsplits else W_SPLITS
     results = []
     for B in [int(b) for b in args.batches.split(",")]:
         for li in [int(v) for v in args.layers.split(",")]:
@@ -116,7 +118,7 @@ def main():
             kt_d = (dshape[2] + 31) // 32
             kt_w = (M + 31) // 32
             for rnd in range(2):
-                for which, splits, kt in (("d", D_SPLITS, kt_d), ("w", W_SPLITS, kt_w)):
+                for which, splits, kt in (("d", D_SPLITS, kt_d), ("w", w_splits, kt_w)):
                     for bm, bn in TILES:
                         if which == "w" and bm == 256 and (wshape[2] % 128 or args.engine != "f16x2"):
                             continue
