@@ -556,6 +556,9 @@ const std::vector<TunedPlan>& tuned_plans() {
       // 32 images, block 1 (64->128 @16): 76.9 -> 74.7
       {1, 3, 8192, 64, 1152, 128, 64, 3},
       {2, 3, 8192, 128, 576, 128, 64, 24},
+      // 32 images, block 2 (128->256 @8): 77.3 -> 75.7 (scripts/verify_plans.py, 5 alternations)
+      {1, 3, 2048, 128, 2304, 64, 64, 4},
+      {2, 3, 2048, 256, 1152, 128, 64, 6},
       // 32 images, block 3 (256->256 @8): backward 98.5 -> 93.2, forward 37.6 -> 36.0
       {1, 3, 2048, 256, 2304, 64, 128, 4},
       {2, 3, 2048, 256, 2304, 128, 128, 6},
@@ -612,6 +615,9 @@ const std::vector<TunedPlan>& tuned_plans() {
       {1, 3, 12544, 256, 1024, 64, 128, 1},
       // weight gradient of 512->128 1x1 @28: 42.5 -> 39.3
       {2, 3, 50176, 128, 512, 128, 128, 64},
+      // 256 images, blocks 2 and 3: data gradient over 2 / 1 splits (190.6 -> 186.8, 266.6 -> 260.9)
+      {1, 3, 16384, 128, 2304, 256, 128, 2},
+      {1, 3, 16384, 256, 2304, 256, 128, 1},
       // 256 images, block 4 (256->512 @4): 173.4 -> 166.7
       {1, 3, 4096, 256, 4608, 256, 128, 3},
       {2, 3, 4096, 512, 2304, 256, 128, 4},
