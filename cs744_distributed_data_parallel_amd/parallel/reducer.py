@@ -432,7 +432,7 @@ class GradReducer:
         # GPU: timed on the GPU wall clock between two stamps on the compute stream around the
         # (synchronous) collective, after a short GPU sleep so the host is ahead -- the host's
         # launch-and-synchronize round trip (~100 us) is not part of what overlaps the backward
-        stamped = cuda and _native.available()
+        stamped = cuda and _native.available() and self._stream_ordered_comm()
         if stamped:
             C = _native.lib()
             hz = C.gpu_wall_clock_khz() * 1e3
@@ -465,6 +465,18 @@ class GradReducer:
             ts.append(samples[len(samples) // 2])
             del buf
         return fit_comm_model(xs, ts)
+
+    def _stream_ordered_comm(self) -> bool:
+        """Collectives enqueued on GPU streams (RCCL), which GPU stamps around them can time; gloo
+        runs them on the host."""
+        if isinstance(self.comm, RcclCommunicator):
+            return True
+        if isinstance(self.comm, TorchCommunicator):
+            try:
+                return tdist.get_backend(self.comm.group) == "nccl"
+            except Exception:  # pragma: no cover - no default group
+                return False
+        return False
 
     def rebuild_in_ready_order(self, order: Optional[Sequence[int]] = None) -> bool:
         """Relayout the arena in gradient-ready order (rank 0's order, broadcast) and re-bucket.
