@@ -242,3 +242,51 @@ def test_watchdog_aborts_a_stuck_collective():
     env["PYTHONPATH"] = repo + os.pathsep + env.get("PYTHONPATH", "")
     r = subprocess.run([sys.executable, "-c", WATCHDOG_SCRIPT], env=env, capture_output=True, text=True, timeout=200)
     assert "WATCHDOG_OK" in r.stdout, r.stdout[-3000:] + r.stderr[-5000:]
+
+
+OVERLAP_SCRIPT = textwrap.dedent(
+    r"""
+    import os, torch
+    # every collective is followed on the comm stream by a ~300 us kernel (RcclComm test post-op)
+    os.environ["CDP_REDUCER_TEST_POSTOP"] = "300:1"
+    import cs744_distributed_data_parallel_amd as cdp
+    from cs744_distributed_data_parallel_amd import distributed as dist
+    dist.init_process_group("rccl", rank=0, world_size=1)
+    comm = dist.native_communicator()
+    C = cdp._native.lib()
+    hz = C.gpu_wall_clock_khz() * 1e3
+    buf = torch.zeros(1024, device="cuda")  # one workgroup of post-op: no CU starvation, only the streams
+    ts = torch.zeros(8, dtype=torch.int64, device="cuda")
+    worst = []
+    for rep in range(3):
+        torch.cuda.synchronize()
+        C.gpu_sleep(2000.0)                 # the host enqueues everything below ahead of the GPU
+        C.gpu_timestamp(ts, 0)
+        w = comm.all_reduce(buf, "sum", True)
+        for i in range(1, 7):
+            C.gpu_timestamp(ts, i)          # compute-stream dispatches while the comm stream works
+        w.wait()
+        C.gpu_timestamp(ts, 7)              # ordered after the collective and its post-op
+        torch.cuda.synchronize()
+        r = ts.cpu().tolist()
+        gaps = [(r[i + 1] - r[i]) / hz * 1e6 for i in range(1, 6)]
+        worst.append(max(gaps))
+        assert (r[7] - r[0]) / hz * 1e6 >= 250.0, r
+    print("GAPS", worst)
+    # the comm stream runs beside the compute stream without holding its dispatches back (with a
+    # stream the communicator created itself, collectives enqueued during a backward held every
+    # compute dispatch ~57 us; scripts/diag/queue_prio.py)
+    assert min(worst) < 25.0, worst
+    dist.destroy_process_group()
+    print("OVERLAP_OK")
+    """
+)
+
+
+def test_comm_stream_work_does_not_hold_back_compute_dispatches():
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()), RANK="0", WORLD_SIZE="1",
+               LOCAL_RANK="0")
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env["PYTHONPATH"] = repo + os.pathsep + env.get("PYTHONPATH", "")
+    r = subprocess.run([sys.executable, "-c", OVERLAP_SCRIPT], env=env, capture_output=True, text=True, timeout=300)
+    assert "OVERLAP_OK" in r.stdout, r.stdout[-3000:] + r.stderr[-5000:]
