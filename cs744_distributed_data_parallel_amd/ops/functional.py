@@ -45,9 +45,11 @@ def _bn_momentum(bn) -> float:
     return -1.0 if bn.momentum is None else float(bn.momentum)
 
 
-# f16x2 conv engine: a tensor produced by one of our kernels carries its producer's partial |max|
-# values (the operand scale of the GEMMs that consume it), tagged with the tensor's version so an
-# in-place change after production invalidates them (the consumer then measures the tensor itself).
+# f16x2 conv engine: a tensor produced by one of our kernels carries its producer's "act max" --
+# the per-image and per-channel |max| of what it wrote (csrc/kernels/act_max.h), from which the
+# GEMMs that consume it derive one power-of-two scale per GEMM row -- tagged with the tensor's
+# version so an in-place change after production invalidates it (the consumer then measures the
+# tensor itself).
 def _get_amax(t):
     tag = getattr(t, "_cdp_amax", None)
     if tag is None or tag[1] != t._version:
@@ -61,12 +63,13 @@ def _set_amax(t, amax):
 
 
 def weight_amax(weights):
-    """f16x2 engine: the partial |max| values of a model's conv weights in ONE launch (a list, one
-    entry per weight), for :func:`conv_bn_act`'s ``w_amax``; None for the other engines. Computed
-    from the current weights at every forward, so it is valid whatever changed them."""
+    """f16x2 engine: a model's conv weights' maxima (per output channel and per input channel, the
+    operand scales of the forward and data-gradient GEMMs) in ONE launch -- a list, one entry per
+    weight, for :func:`conv_bn_act`'s ``w_amax``; None for the other engines. Computed from the
+    current weights, so it is valid whatever changed them."""
     if not weights or not use_native(weights[0]):
         return None
-    parts = _native.lib().multi_amax(list(weights))
+    parts, _ = _native.lib().weight_prep(list(weights), [False] * len(weights))
     return parts if parts else None
 
 
@@ -205,7 +208,7 @@ class _ConvBNAct(torch.autograd.Function):
         prev = (None, None, False, False, 2)
         if li is not None and li.consumers == 1 and nig[0] and not park_dx and addend is None:
             prev = (li.y, li.stats, li.pool, li.relu, li.ps)
-        dx, dw, db, dgamma, dbeta, dres, prev_part = C.conv_bn_act_bwd(
+        dx, dw, db, dgamma, dbeta, dres, prev_part, _ = C.conv_bn_act_bwd(
             gout, x, w, y, stats, stride, pad, pool, relu, nig[0], has_bias, zout, training,
             _slot(wp, nig[1]), _slot(bp, nig[2] and has_bias), _slot(gp, nig[3]), _slot(betap, nig[4]), addend,
             *ctx.amax, ctx.w_t, part_in, *prev, bp,

@@ -115,6 +115,10 @@ class DistributedDataParallel(nn.Module):
         if self.world_size == 1:
             return
         self.comm.broadcast(self.arena.data, 0)
+        # a raw arena write bumps no parameter's _version: drop the optimizer's prepared weight
+        # products (W^T, f16x2 maxima) so the next forward re-derives them from rank 0's weights
+        if hasattr(self.arena, "prep_valid"):
+            self.arena.prep_valid = None
         if self._buffers_arena is not None:
             for f in self._buffers_arena.flats():
                 self.comm.broadcast(f, 0)

@@ -12,6 +12,8 @@ all-reduce overlapped with autograd" (BASELINE.json).
 """
 from __future__ import annotations
 
+import os
+
 import threading
 import time
 from typing import List, Optional, Sequence, Tuple
@@ -158,21 +160,22 @@ class _PyReducer:
                 return
             if self.trace:
                 self.log.append(("f", -1, time.monotonic_ns()))
-            if self.defer:
-                while self.next_launch < len(self.pending) and self.pending[self.next_launch] == 0:
-                    self._launch(self.next_launch)
-                    self.next_launch += 1
-            if self.next_launch < len(self.pending):
-                if self.find_unused:
-                    for i in range(len(self.params)):
-                        self._mark(i, False)
-                else:
-                    missing = [i for i, r in enumerate(self.ready) if not r]
-                    self.armed = False
-                    raise RuntimeError(
-                        f"DistributedDataParallel: parameters with indices {missing} did not receive gradients "
-                        "in this iteration. Enable find_unused_parameters=True."
-                    )
+            # parameters whose hook never fired are marked ready FIRST, so the launch loop below
+            # counts every bucket -- also in the deferred (calibration) iteration (csrc reducer.cpp)
+            missing = [i for i, r in enumerate(self.ready) if not r]
+            if missing and not self.find_unused:
+                self.armed = False
+                raise RuntimeError(
+                    f"DistributedDataParallel: parameters with indices {missing} did not receive gradients "
+                    "in this iteration. Enable find_unused_parameters=True."
+                )
+            for i in missing:
+                self._mark(i, False)
+            while self.next_launch < len(self.pending) and self.pending[self.next_launch] == 0:
+                self._launch(self.next_launch)
+                self.next_launch += 1
+            if self.next_launch != len(self.pending):
+                raise RuntimeError(f"reducer: {len(self.pending) - self.next_launch} bucket(s) left unlaunched")
             for w in self.works:
                 if w is not None:
                     w.wait()
@@ -246,7 +249,8 @@ class GradReducer:
             self._impl.remove_hooks()
             self._impl = None
         self._stream = torch.cuda.current_stream(a.device) if a.device.type == "cuda" else None
-        use_native = _native.available() and (
+        # CDP_PY_REDUCER=1: the Python twin of the C++ reducer (tests run both on the same cases)
+        use_native = _native.available() and os.environ.get("CDP_PY_REDUCER", "0") != "1" and (
             isinstance(self.comm, RcclCommunicator) or isinstance(self.comm, TorchCommunicator)
         )
         if use_native:

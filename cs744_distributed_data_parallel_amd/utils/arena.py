@@ -24,6 +24,18 @@ import torch
 ALIGN = 4  # elements (16 B for fp32)
 
 
+def weight_max_elems(co: int, ci: int) -> int:
+    """Floats of a conv weight's f16x2 maxima (csrc/kernels/kernels.h ``weight_max_elems``): the per-co
+    partials of every 32-wide ci block, then the per-ci partials of every 32-wide co block."""
+    return ((ci + 31) // 32) * co + ((co + 31) // 32) * ci
+
+
+def act_max_elems(n: int, c: int, copies: int = 8) -> int:
+    """int32 slots of an activation's f16x2 act max (csrc ``act_max_elems``): one per image, then
+    ``copies`` (kActCopies) x one per channel."""
+    return n + copies * c
+
+
 def _dense(t: torch.Tensor) -> bool:
     return t.is_contiguous() or (t.dim() == 4 and t.is_contiguous(memory_format=torch.channels_last))
 
@@ -205,9 +217,11 @@ class FlatArena:
 
         r = _native.lib().sgd_prep_plan(self.data, start, end, [w.data for w in weights], list(want))
         desc, meta, amax, wts = r[0], r[1], r[2], list(r[3:])
-        nblk = [((w.shape[0] + 31) // 32) * ((w.shape[1] + 31) // 32) for w in weights]
+        # each weight's maxima: per-co partials [ceil(Ci/32), Co] then per-ci [ceil(Co/32), Ci]
+        # (csrc weight_max_elems), back to back in plan order
+        sizes = [weight_max_elems(w.shape[0], w.shape[1]) for w in weights]
         views, b0 = [], 0
-        for n in nblk:
+        for n in sizes:
             views.append(amax.narrow(0, b0, n))
             b0 += n
         plan = {"desc": desc, "meta": meta, "amax": amax, "amax_views": views,

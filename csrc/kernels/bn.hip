@@ -16,6 +16,7 @@
 #include <algorithm>
 #include <cstdlib>
 
+#include "act_max.h"
 #include "common.h"
 #include "kernels.h"
 #include "x3_common.h"
@@ -176,18 +177,21 @@ __global__ __launch_bounds__(256) void bn_fin_act_kernel(const float* __restrict
                                                          float* running_var, long long* nbt, float momentum,
                                                          float eps, float* __restrict__ stats,
                                                          const float* __restrict__ y, float* __restrict__ out, int N,
-                                                         int H, int W, int pool, int relu, int chunks,
-                                                         float* __restrict__ amax_part) {
+                                                         int H, int W, int pool, int relu, int chunks, FastDiv fd_HWo,
+                                                         ActMaxOut am) {
   constexpr int TQ = 256 / CG;  // merge threads per channel
   constexpr int CQ = CG / 4;    // phase 2: channel quads x RL row lanes
   constexpr int RL = 256 / CQ;
   __shared__ double red[TQ][CG];
   __shared__ float s_sc[CG], s_sh[CG];
+  __shared__ ActMaxBlock<CG> sam;  // per-image / per-channel |max| of the block's output
   const int ngroups = C / CG;
   const int cg = blockIdx.x % ngroups, chunk = blockIdx.x / ngroups;
   const int tid = threadIdx.x;
   const int ch = tid % CG, q = tid / CG;
   const int c = cg * CG + ch;
+  const bool want = am.img != nullptr;
+  if (want) sam.init(tid, 256);  // (the merge's barriers below order it before every add)
   // phase-2 geometry, and this thread's first kFinRPT rows of y loaded before the merge: the y
   // round trip overlaps the partials' instead of following it
   const int cq = tid % CQ, rl = tid / CQ;
@@ -196,6 +200,7 @@ __global__ __launch_bounds__(256) void bn_fin_act_kernel(const float* __restrict
   const long long rows = (long long)N * Ho * Wo;
   const long long per = (rows + chunks - 1) / chunks;
   const long long r0 = (long long)chunk * per, r1 = min(rows, r0 + per);
+  const int img0 = fdiv((int)min(r0, rows - 1), fd_HWo);
   float4 pv[kFinRPT][4];
   fin_prefetch(y, pv, r0 + rl, r1, pool, H, W, Ho, Wo, C, n0, RL);
   // phase 1: thread (ch, q) merges partials b = q + TQ k -- one batch of buffer loads
@@ -271,7 +276,8 @@ __global__ __launch_bounds__(256) void bn_fin_act_kernel(const float* __restrict
   // phase 2: this chunk's output rows, 16 channel quads x 16 row lanes
   const float4 sc = make_float4(s_sc[4 * cq], s_sc[4 * cq + 1], s_sc[4 * cq + 2], s_sc[4 * cq + 3]);
   const float4 sh = make_float4(s_sh[4 * cq], s_sh[4 * cq + 1], s_sh[4 * cq + 2], s_sh[4 * cq + 3]);
-  float am = 0.f;
+  ImgRun run;
+  float4 cm = f4zero();
   auto emit = [&](long long r, const float4 (&v)[4]) {
     float4 z = affine_act(v[0], sc, sh, relu);
     if (pool) {
@@ -283,7 +289,10 @@ __global__ __launch_bounds__(256) void bn_fin_act_kernel(const float* __restrict
       z.w = fmaxf(fmaxf(z.w, z1.w), fmaxf(z2.w, z3.w));
     }
     st4(out + r * C + n0, z);
-    am = fmaxf(am, fmaxf(fmaxf(fabsf(z.x), fabsf(z.y)), fmaxf(fabsf(z.z), fabsf(z.w))));
+    if (want) {
+      run.add(fdiv((int)r, fd_HWo), absmax4(z), sam, img0, am);
+      cm = absmax4(cm, z);
+    }
   };
 #pragma unroll
   for (int i = 0; i < kFinRPT; ++i)
@@ -293,68 +302,87 @@ __global__ __launch_bounds__(256) void bn_fin_act_kernel(const float* __restrict
     fin_load_row(y, v, r, pool, H, W, Ho, Wo, C, n0);
     emit(r, v);
   }
-  if (amax_part) {
-    __shared__ float ared[4];
-    am = wave_max(am);
-    if ((tid & 63) == 0) ared[tid >> 6] = am;
+  if (want) {
+    run.flush(sam, img0, am);
+    sam.add_ch4(4 * cq, cm);
     __syncthreads();
-    if (tid == 0) amax_part[blockIdx.x] = fmaxf(fmaxf(ared[0], ared[1]), fmaxf(ared[2], ared[3]));
+    sam.publish(am, img0, N, cg * CG, CG, C, blockIdx.x % kActCopies, tid, 256);
   }
 }
 
 // ------------------------------------------------------------------ forward apply
-// out = [pool2](relu(y*scale+shift)) (+ residual before relu when res != null)
+// out = [pool2](relu(y*scale+shift)) (+ residual before relu when res != null). Block b writes the
+// contiguous float4 range [b * per, (b + 1) * per) of out (per a multiple of 256 and of C / 4 when
+// qmode != 0, so a thread's channel quad is fixed: qmode 1 = one quad (C / 4 divides 256), 2 = two
+// alternating quads (C / 4 == 512), 0 = any C, per-element LDS channel maxima), and folds the
+// per-image / per-channel |max| of what it writes into am (act_max.h).
 __global__ __launch_bounds__(256) void bn_act_fwd_kernel(const float* __restrict__ y, const float* __restrict__ stats,
                                                          const float* __restrict__ res, float* __restrict__ out,
-                                                         int N, int H, int W, int C, int pool, int relu,
-                                                         float* __restrict__ amax_part) {
+                                                         int N, int H, int W, int C, int pool, int relu, int per,
+                                                         int qmode, FastDiv fd_C4, FastDiv fd_HWo, ActMaxOut am) {
+  __shared__ ActMaxBlock<kMaxActC> sam;
   const int C4 = C >> 2;
   const int Ho = pool ? H / 2 : H, Wo = pool ? W / 2 : W;
-  const long long total = (long long)N * Ho * Wo * C4;
+  const int total = N * Ho * Wo * C4;
   const float* scale = stats + 2 * C;
   const float* shift = stats + 3 * C;
-  float am = 0.f;
-  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
-       i += (long long)gridDim.x * blockDim.x) {
-    const int c4 = (int)(i % C4);
-    const long long pix = i / C4;
+  const int tid = threadIdx.x;
+  const int i0 = blockIdx.x * per, i1 = min(total, i0 + per);
+  const bool want = am.img != nullptr;
+  const int img0 = fdiv(fdiv(min(i0, total - 1), fd_C4), fd_HWo);
+  if (want) {
+    sam.init(tid, 256);
+    __syncthreads();
+  }
+  ImgRun run;
+  float4 cm[2] = {f4zero(), f4zero()};
+  int k = 0;
+  for (int i = i0 + tid; i < i1; i += 256, ++k) {
+    const int pix = fdiv(i, fd_C4);
+    const int c4 = i - pix * C4;
     const float4 sc = ld4(scale + 4 * c4), sh = ld4(shift + 4 * c4);
+    float4 z;
     if (!pool) {
-      float4 z = affine_act(ld4(y + pix * C + 4 * c4), sc, sh, false);
+      z = affine_act(ld4(y + (long long)pix * C + 4 * c4), sc, sh, false);
       if (res) {
-        const float4 r = ld4(res + pix * C + 4 * c4);
+        const float4 r = ld4(res + (long long)pix * C + 4 * c4);
         z.x += r.x; z.y += r.y; z.z += r.z; z.w += r.w;
       }
       if (relu) {
         z.x = fmaxf(z.x, 0.f); z.y = fmaxf(z.y, 0.f); z.z = fmaxf(z.z, 0.f); z.w = fmaxf(z.w, 0.f);
       }
-      st4(out + pix * C + 4 * c4, z);
-      am = fmaxf(am, fmaxf(fmaxf(fabsf(z.x), fabsf(z.y)), fmaxf(fabsf(z.z), fabsf(z.w))));
     } else {
-      const int wo = (int)(pix % Wo);
-      const long long t = pix / Wo;
-      const int ho = (int)(t % Ho);
-      const int n = (int)(t / Ho);
+      const int wo = pix % Wo;
+      const int t = pix / Wo;
+      const int ho = t % Ho;
+      const int n = t / Ho;
       const float* base = y + (((long long)n * H + 2 * ho) * W + 2 * wo) * C + 4 * c4;
       const float4 z0 = affine_act(ld4(base), sc, sh, relu);
       const float4 z1 = affine_act(ld4(base + C), sc, sh, relu);
       const float4 z2 = affine_act(ld4(base + (long long)W * C), sc, sh, relu);
       const float4 z3 = affine_act(ld4(base + (long long)W * C + C), sc, sh, relu);
-      float4 m;
-      m.x = fmaxf(fmaxf(z0.x, z1.x), fmaxf(z2.x, z3.x));
-      m.y = fmaxf(fmaxf(z0.y, z1.y), fmaxf(z2.y, z3.y));
-      m.z = fmaxf(fmaxf(z0.z, z1.z), fmaxf(z2.z, z3.z));
-      m.w = fmaxf(fmaxf(z0.w, z1.w), fmaxf(z2.w, z3.w));
-      st4(out + pix * C + 4 * c4, m);
-      am = fmaxf(am, fmaxf(fmaxf(fabsf(m.x), fabsf(m.y)), fmaxf(fabsf(m.z), fabsf(m.w))));
+      z.x = fmaxf(fmaxf(z0.x, z1.x), fmaxf(z2.x, z3.x));
+      z.y = fmaxf(fmaxf(z0.y, z1.y), fmaxf(z2.y, z3.y));
+      z.z = fmaxf(fmaxf(z0.z, z1.z), fmaxf(z2.z, z3.z));
+      z.w = fmaxf(fmaxf(z0.w, z1.w), fmaxf(z2.w, z3.w));
+    }
+    st4(out + (long long)pix * C + 4 * c4, z);
+    if (want) {
+      run.add(fdiv(pix, fd_HWo), absmax4(z), sam, img0, am);
+      if (qmode == 1 || (qmode == 2 && !(k & 1))) cm[0] = absmax4(cm[0], z);
+      else if (qmode == 2) cm[1] = absmax4(cm[1], z);
+      else sam.add_ch4(4 * c4, make_float4(fabsf(z.x), fabsf(z.y), fabsf(z.z), fabsf(z.w)));
     }
   }
-  if (amax_part) {  // |max| of this block's output: operand scale of the consumer's f16x2 GEMMs
-    __shared__ float red[4];
-    am = wave_max(am);
-    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = am;
+  if (want) {  // per-image / per-channel |max| of this block's output (the consumer GEMMs' scales)
+    run.flush(sam, img0, am);
+    if (qmode == 1 && i0 + tid < i1) sam.add_ch4(4 * (tid % C4), cm[0]);
+    if (qmode == 2) {
+      if (i0 + tid < i1) sam.add_ch4(4 * tid, cm[0]);
+      if (i0 + tid + 256 < i1) sam.add_ch4(4 * (tid + 256), cm[1]);
+    }
     __syncthreads();
-    if (threadIdx.x == 0) amax_part[blockIdx.x] = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+    sam.publish(am, img0, N, 0, C, C, blockIdx.x % kActCopies, tid, 256);
   }
 }
 
@@ -546,15 +574,24 @@ __global__ __launch_bounds__(256) void chan_finalize_kernel(const float* __restr
 
 // dy = scale*(dz - sum(dz)/M - xhat*sum(dz*xhat)/M), full resolution; partial sum(dy) per
 // (block, channel) for the conv bias gradient. Each thread handles one pooled window (pool) or
-// one pixel; for odd H/W under pooling the uncovered border gets dz = 0.
+// one pixel; for odd H/W under pooling the uncovered border gets dz = 0. Block b walks the
+// contiguous (pooled) pixel range [b * per, (b + 1) * per), per = ceil(npix / gridDim.x), and folds
+// the per-image / per-channel |max| of the dy it writes into am (act_max.h).
 __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const float* __restrict__ y, const float* __restrict__ gout,
                                                            const float* __restrict__ stats,
                                                            const float* __restrict__ sums, float* __restrict__ dy,
                                                            float* __restrict__ dbias_part, int N, int H, int W,
                                                            int C, int pool, int relu, const float* __restrict__ zout,
-                                                           float* __restrict__ dres, float* __restrict__ amax_part) {
+                                                           float* __restrict__ dres, FastDiv fd_IMG, FastDiv fd_HW,
+                                                           ActMaxOut am) {
   __shared__ float4 red[256];
-  float am = 0.f;  // |max| of the written dy (operand scale of the f16x2 GEMMs)
+  __shared__ ActMaxBlock<kMaxActC> sam;
+  const bool want = am.img != nullptr;
+  if (want) {
+    sam.init(threadIdx.x, 256);
+    __syncthreads();
+  }
+  ImgRun run;  // fd_IMG: (pooled) pixels per image; fd_HW: full-resolution pixels per image
   const int C4 = C >> 2;
   const int tid = threadIdx.x;
   const int cq_per_thread = (C4 + 255) / 256;
@@ -571,9 +608,13 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const float* __restri
   const float invM = 1.f / (float)Mtot;
   const int Ho = pool ? H / 2 : H, Wo = pool ? W / 2 : W;
   const long long npix = pool ? (long long)N * Ho * Wo : Mtot;
+  const long long pper = (npix + gridDim.x - 1) / gridDim.x;
+  const long long p0 = (long long)blockIdx.x * pper, p1 = min(npix, p0 + pper);
+  const int img0 = fdiv((int)min(p0, npix - 1), fd_IMG);
   for (int j = 0; j < cq_per_thread; ++j) {
     const int cq = cq0 + j * 256;
     float4 acc = f4zero();
+    float4 cm = f4zero();  // this channel quad's |max| of dy
     if (active && cq < C4) {
       const float4 sc = ld4(scale + 4 * cq), sh = ld4(shift + 4 * cq);
       const float4 mu = ld4(mean + 4 * cq), is = ld4(invstd + 4 * cq);
@@ -581,6 +622,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const float* __restri
       float4 k1, k2;  // dy = sc*(dz - k1 - xhat*k2)
       k1.x = s1.x * invM; k1.y = s1.y * invM; k1.z = s1.z * invM; k1.w = s1.w * invM;
       k2.x = s2.x * invM; k2.y = s2.y * invM; k2.z = s2.z * invM; k2.w = s2.w * invM;
+      int img = 0;  // image of the pixel being emitted
       auto emit = [&](long long off, float4 yv, float4 dz) {
         float4 o;
 #pragma unroll
@@ -594,9 +636,13 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const float* __restri
         }
         st4(dy + off, o);
         acc.x += o.x; acc.y += o.y; acc.z += o.z; acc.w += o.w;
-        am = fmaxf(am, fmaxf(fmaxf(fabsf(o.x), fabsf(o.y)), fmaxf(fabsf(o.z), fabsf(o.w))));
+        if (want) {
+          run.add(img, absmax4(o), sam, img0, am);
+          cm = absmax4(cm, o);
+        }
       };
-      for (long long px = (long long)blockIdx.x * ppb + pl; px < npix; px += (long long)gridDim.x * ppb) {
+      for (long long px = p0 + pl; px < p1; px += ppb) {
+        img = fdiv((int)px, fd_IMG);
         const float4 g = ld4(gout + px * C + 4 * cq);
         if (!pool) {
           const float4 yv = ld4(y + px * C + 4 * cq);
@@ -641,9 +687,11 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const float* __restri
           const int w = (int)(px % W);
           const int h = (int)((px / W) % H);
           if (h < 2 * Ho && w < 2 * Wo) continue;
+          img = fdiv((int)px, fd_HW);
           emit(px * C + 4 * cq, ld4(y + px * C + 4 * cq), f4zero());
         }
       }
+      if (want) sam.add_ch4(4 * cq, cm);
     }
     red[tid] = acc;
     __syncthreads();
@@ -659,12 +707,10 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const float* __restri
     }
     __syncthreads();
   }
-  if (amax_part) {
-    am = wave_max(am);
-    float* r = reinterpret_cast<float*>(red);
-    if ((threadIdx.x & 63) == 0) r[threadIdx.x >> 6] = am;
+  if (want) {
+    run.flush(sam, img0, am);
     __syncthreads();
-    if (threadIdx.x == 0) amax_part[blockIdx.x] = fmaxf(fmaxf(r[0], r[1]), fmaxf(r[2], r[3]));
+    sam.publish(am, img0, N, 0, C, C, blockIdx.x % kActCopies, tid, 256);
   }
 }
 
@@ -677,16 +723,19 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const float* __restri
 __global__ __launch_bounds__(256) void bn_bwd_fin_apply_kernel(
     const float* __restrict__ part, int nparts, int PS, const float* __restrict__ y,
     const float* __restrict__ gout, const float* __restrict__ stats, float* __restrict__ dy, float* gbeta,
-    float* ggamma, float* gdb, int N, int H, int W, int C, int pool, int relu, int chunks,
-    float* __restrict__ amax_part) {
+    float* ggamma, float* gdb, int N, int H, int W, int C, int pool, int relu, int chunks, FastDiv fd_HWo,
+    ActMaxOut am) {
   __shared__ double red[3][4][64];
   __shared__ float s_k1[64], s_k2[64];
+  __shared__ ActMaxBlock<64> sam;  // per-image / per-channel |max| of the block's dy
   const int ngroups = C >> 6;
   const int cg = blockIdx.x % ngroups, chunk = blockIdx.x / ngroups;
   const int tid = threadIdx.x;
   const int ch = tid & 63, q = tid >> 6;
   const int c = cg * 64 + ch;
   const long long Mtot = (long long)N * H * W;
+  const bool want = am.img != nullptr;
+  if (want) sam.init(tid, 256);  // (the merge's barriers below order it before every add)
   // phase-2 geometry, and this thread's first kFinRPT rows of y and of gout loaded before the
   // merge (their round trip overlaps the partials')
   const int cq = tid & 15, rl = tid >> 4;
@@ -695,6 +744,7 @@ __global__ __launch_bounds__(256) void bn_bwd_fin_apply_kernel(
   const long long rows = (long long)N * Ho * Wo;
   const long long per = (rows + chunks - 1) / chunks;
   const long long r0 = (long long)chunk * per, r1 = min(rows, r0 + per);
+  const int img0 = fdiv((int)min(r0, rows - 1), fd_HWo);
   float4 pv[kFinRPT][4], pg[kFinRPT];
   fin_prefetch(y, pv, r0 + rl, r1, pool, H, W, Ho, Wo, C, n0);
 #pragma unroll
@@ -755,7 +805,9 @@ __global__ __launch_bounds__(256) void bn_bwd_fin_apply_kernel(
   const float4 mu = ld4(stats + n0), is = ld4(stats + C + n0);
   const float4 k1 = make_float4(s_k1[4 * cq], s_k1[4 * cq + 1], s_k1[4 * cq + 2], s_k1[4 * cq + 3]);
   const float4 k2 = make_float4(s_k2[4 * cq], s_k2[4 * cq + 1], s_k2[4 * cq + 2], s_k2[4 * cq + 3]);
-  float am = 0.f;
+  ImgRun run;
+  float4 cm = f4zero();
+  int img = 0;  // image of the row being emitted
   auto emit = [&](long long off, float4 yv, float4 dz) {
     float4 o;
 #pragma unroll
@@ -768,9 +820,13 @@ __global__ __launch_bounds__(256) void bn_bwd_fin_apply_kernel(
       if (e == 3) o.w = v;
     }
     st4(dy + off, o);
-    am = fmaxf(am, fmaxf(fmaxf(fabsf(o.x), fabsf(o.y)), fmaxf(fabsf(o.z), fabsf(o.w))));
+    if (want) {
+      run.add(img, absmax4(o), sam, img0, am);
+      cm = absmax4(cm, o);
+    }
   };
   auto row = [&](long long r, const float4 (&v)[4], float4 g) {
+    img = fdiv((int)r, fd_HWo);
     if (!pool) {
       const float4 yv = v[0];
       const float4 z = affine_act(yv, sc, sh, relu);
@@ -810,12 +866,11 @@ __global__ __launch_bounds__(256) void bn_bwd_fin_apply_kernel(
     fin_load_row(y, v, r, pool, H, W, Ho, Wo, C, n0);
     row(r, v, ld4(gout + r * C + n0));
   }
-  if (amax_part) {
-    __shared__ float ared[4];
-    am = wave_max(am);
-    if ((tid & 63) == 0) ared[tid >> 6] = am;
+  if (want) {
+    run.flush(sam, img0, am);
+    sam.add_ch4(4 * cq, cm);
     __syncthreads();
-    if (tid == 0) amax_part[blockIdx.x] = fmaxf(fmaxf(ared[0], ared[1]), fmaxf(ared[2], ared[3]));
+    sam.publish(am, img0, N, cg * 64, 64, C, blockIdx.x % kActCopies, tid, 256);
   }
 }
 
@@ -941,16 +996,19 @@ int bn_fin_act_grid(int N, int H, int W, int C, bool pool, int nparts) {
   return (int)(chunks * ngroups);
 }
 
+static int out_pixels_per_image(int H, int W, bool pool) { return pool ? (H / 2) * (W / 2) : H * W; }
+
 void bn_fin_act_launch(const float* part, int nparts, int rpp, int C, const float* gamma, const float* beta,
                        float* running_mean, float* running_var, long long* nbt, float momentum, float eps,
                        float* stats, const float* y, float* out, int N, int H, int W, bool pool, bool relu,
-                       float* amax_part, hipStream_t st) {
+                       ActMaxOut am, hipStream_t st) {
   const int grid = bn_fin_act_grid(N, H, W, C, pool, nparts);
   const int M = N * H * W;
   const int cg = fin_cg(nparts);
   hipLaunchKernelGGL(cg == 64 ? bn_fin_act_kernel<64> : bn_fin_act_kernel<16>, dim3(grid), dim3(256), 0, st, part,
                      nparts, rpp, M, C, gamma, beta, running_mean, running_var, nbt, momentum, eps, stats, y, out, N,
-                     H, W, pool ? 1 : 0, relu ? 1 : 0, grid / (C / cg), amax_part);
+                     H, W, pool ? 1 : 0, relu ? 1 : 0, grid / (C / cg),
+                     make_fastdiv(out_pixels_per_image(H, W, pool)), am);
 }
 
 bool bn_bwd_fin_apply_ok(int nparts, int C, int H, int W, bool pool) {
@@ -959,20 +1017,29 @@ bool bn_bwd_fin_apply_ok(int nparts, int C, int H, int W, bool pool) {
 
 void bn_bwd_fin_apply_launch(const float* part, int nparts, int ps, const float* y, const float* gout,
                              const float* stats, float* dy, float* gbeta, float* ggamma, float* gdb, int N, int H,
-                             int W, int C, bool pool, bool relu, float* amax_part, hipStream_t st) {
+                             int W, int C, bool pool, bool relu, ActMaxOut am, hipStream_t st) {
   const int grid = bn_fin_act_grid(N, H, W, C, pool);
   hipLaunchKernelGGL(bn_bwd_fin_apply_kernel, dim3(grid), dim3(256), 0, st, part, nparts, ps, y, gout, stats, dy,
-                     gbeta, ggamma, gdb, N, H, W, C, pool ? 1 : 0, relu ? 1 : 0, grid / (C / 64), amax_part);
+                     gbeta, ggamma, gdb, N, H, W, C, pool ? 1 : 0, relu ? 1 : 0, grid / (C / 64),
+                     make_fastdiv(out_pixels_per_image(H, W, pool)), am);
 }
 
 int bn_act_grid(int N, int H, int W, int C, bool pool) {
-  return act_grid((long long)N * (pool ? (H / 2) * (W / 2) : H * W) * (C / 4));
+  return act_grid((long long)N * out_pixels_per_image(H, W, pool) * (C / 4));
 }
 
 void bn_act_fwd_launch(const float* y, const float* stats, const float* res, float* out, int N, int H, int W, int C,
-                       bool pool, bool relu, hipStream_t st, float* amax_part) {
-  hipLaunchKernelGGL(bn_act_fwd_kernel, dim3(bn_act_grid(N, H, W, C, pool)), dim3(256), 0, st, y, stats, res, out, N,
-                     H, W, C, pool ? 1 : 0, relu ? 1 : 0, amax_part);
+                       bool pool, bool relu, hipStream_t st, ActMaxOut am) {
+  const int C4 = C / 4;
+  const long long total = (long long)N * out_pixels_per_image(H, W, pool) * C4;
+  // contiguous per-block ranges, whole multiples of 256 float4 (and of C4: fixed channel quads)
+  const int qmode = (C4 <= 256 && (256 % C4) == 0) ? 1 : C4 == 512 ? 2 : 0;
+  const long long unit = qmode == 2 ? 512 : 256;
+  const long long blocks = bn_act_grid(N, H, W, C, pool);
+  const long long per = std::max(unit, ((total + blocks - 1) / blocks + unit - 1) / unit * unit);
+  hipLaunchKernelGGL(bn_act_fwd_kernel, dim3((unsigned)((total + per - 1) / per)), dim3(256), 0, st, y, stats, res,
+                     out, N, H, W, C, pool ? 1 : 0, relu ? 1 : 0, (int)per, qmode, make_fastdiv(C4),
+                     make_fastdiv(out_pixels_per_image(H, W, pool)), am);
 }
 
 void bn_bwd_reduce_launch(const float* y, const float* gout, const float* stats, float* part, int nblocks, int N,
@@ -998,9 +1065,10 @@ void chan_finalize_launch(const float* part, int nparts, int C, float* out, floa
 
 void bn_bwd_apply_launch(const float* y, const float* gout, const float* stats, const float* sums, float* dy,
                          float* dbias_part, int nblocks, int N, int H, int W, int C, bool pool, bool relu,
-                         const float* zout, float* dres, hipStream_t st, float* amax_part) {
+                         const float* zout, float* dres, hipStream_t st, ActMaxOut am) {
   hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(nblocks), dim3(256), 0, st, y, gout, stats, sums, dy, dbias_part, N,
-                     H, W, C, pool ? 1 : 0, relu ? 1 : 0, zout, dres, amax_part);
+                     H, W, C, pool ? 1 : 0, relu ? 1 : 0, zout, dres, make_fastdiv(out_pixels_per_image(H, W, pool)),
+                     make_fastdiv(H * W), am);
 }
 
 }  // namespace cdp

@@ -34,6 +34,17 @@ __device__ __forceinline__ float wave_max(float v) {
   return v;
 }
 
+// LDS barrier that does not wait for global loads still in flight: __syncthreads' fence would
+// drain them (vmcnt(0)). The release / acquire fences are workgroup-scope and LDS-only
+// ("local" address space), so they order the LDS stores before the barrier and the LDS loads after
+// it in the compiler's memory model (a bare s_barrier is not a memory operation to LLVM, so nothing
+// would stop an LDS access from being scheduled across it) while lowering to lgkmcnt(0) alone.
+__device__ __forceinline__ void lds_barrier() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
 // Bijective XCD-aware remap of a flat workgroup id (cdna_hip_programming.md §5,
 // "XCD swizzle must be bijective"). Blocks are dealt round-robin over the 8 XCDs,
 // so consecutive *remapped* ids land on the same XCD and share its L2.

@@ -107,12 +107,14 @@ __device__ __forceinline__ void conv_x3_body(const ConvGemmParams& p, __bf16* __
 
   // per A row: spatial anchor and element offset of (n, anchor, kq)
   int a_h[A_LD], a_w[A_LD], a_n[A_LD], a_off[A_LD];
+  unsigned a_io[A_LD];  // f16x2: byte offset of the row's image slot (p.a_img), kOOB past M
 #pragma unroll
   for (int i = 0; i < A_LD; ++i) {
     const int m = m0 + rrow + RS * i;
     const bool ok = m < p.M;
     const int mm = ok ? m : 0;
     const int n = fdiv(mm, p.fd_PQ);
+    a_io[i] = ok ? (unsigned)n * 4u : kOOB;
     const int rem = mm - mul24(n, PQ);
     const int pp = fdiv(rem, p.fd_Q);
     const int qq = rem - mul24(pp, p.Q);
@@ -135,14 +137,50 @@ __device__ __forceinline__ void conv_x3_body(const ConvGemmParams& p, __bf16* __
     b_off[i] = n < p.Nout ? (unsigned)(mul24(n, p.Kdim) + kq) << ES : kOOB;
   }
 
-  // f16x2: power-of-two operand scales from the producers' partial maxima (wave-uniform); the
-  // partial loads go out first and are waited for after the first tiles' loads are issued
-  float sa = 1.f, sb = 1.f;
-  float amx_a[NP == 2 ? kAmaxK : 1], amx_b[NP == 2 ? kAmaxK : 1];
+  // f16x2: one power-of-two scale per GEMM row of each operand (x3_common.h) -- A rows by their
+  // image (p.a_img), B rows from the weight's per-row partials (p.b_row; the four threads that load
+  // a B row split its partials and meet by two shuffles). The loads go out here and are waited for
+  // after the first tiles' loads are issued.
+  constexpr int BQ = 4;  // B-row partials per thread in the first batch (16 per row)
+  float sa_r[NP == 2 ? A_LD : 1], sb_r[NP == 2 ? B_LD : 1];
+  unsigned am_a[NP == 2 ? A_LD : 1];
+  float am_b[NP == 2 ? B_LD : 1][BQ];
+  const __amdgpu_buffer_rsrc_t brow = make_rsrc(p.b_row, (unsigned)p.b_np * (unsigned)p.b_stride * 4u);
   if constexpr (NP == 2) {
-    amax_issue(p.amax_a, p.amax_na, amx_a);
-    amax_issue(p.amax_b, p.amax_nb, amx_b);
+    const __amdgpu_buffer_rsrc_t ir = make_rsrc(p.a_img, (unsigned)p.N * 4u);
+#pragma unroll
+    for (int i = 0; i < A_LD; ++i) am_a[i] = __builtin_amdgcn_raw_buffer_load_b32(ir, (int)a_io[i], 0, 0);
+#pragma unroll
+    for (int i = 0; i < B_LD; ++i) {
+      const int n = n0 + rrow + RS * i;
+#pragma unroll
+      for (int j = 0; j < BQ; ++j) {
+        const int q = (tid & 3) + 4 * j;
+        const unsigned o = (n < p.Nout && q < p.b_np) ? (unsigned)(q * p.b_stride + n) * 4u : kOOB;
+        am_b[i][j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(brow, (int)o, 0, 0));
+      }
+    }
   }
+  auto finish_scales = [&]() {
+    if constexpr (NP == 2) {
+#pragma unroll
+      for (int i = 0; i < A_LD; ++i) sa_r[i] = pow2_scale(__uint_as_float(am_a[i]));
+#pragma unroll
+      for (int i = 0; i < B_LD; ++i) {
+        const int n = n0 + rrow + RS * i;
+        float m = 0.f;
+#pragma unroll
+        for (int j = 0; j < BQ; ++j) m = fmaxf(m, am_b[i][j]);
+        for (int q = (tid & 3) + 4 * BQ; q < p.b_np; q += 4) {  // wide weights (Ci or Co > 512)
+          const unsigned o = n < p.Nout ? (unsigned)(q * p.b_stride + n) * 4u : kOOB;
+          m = fmaxf(m, __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(brow, (int)o, 0, 0)));
+        }
+        m = fmaxf(m, __shfl_xor(m, 1, kWave));
+        m = fmaxf(m, __shfl_xor(m, 2, kWave));
+        sb_r[i] = pow2_scale(m);
+      }
+    }
+  };
 
   // byte offset of A row i at filter tap (kh, kw), channel offset c (relative to kq); OOB if padded
   auto a_voff = [&](int i, int kh, int kw, int c) -> unsigned {
@@ -249,7 +287,7 @@ __device__ __forceinline__ void conv_x3_body(const ConvGemmParams& p, __bf16* __
         *reinterpret_cast<u32x4*>(d) = pack8(va[i]);
       } else if constexpr (NP == 2) {
         u32x4 s0, s1;
-        split8h(va[i], sa, s0, s1);
+        split8h(va[i], sa_r[i], s0, s1);
         *reinterpret_cast<u32x4*>(d) = s0;
         *reinterpret_cast<u32x4*>(d + PA) = s1;
       } else {
@@ -267,7 +305,7 @@ __device__ __forceinline__ void conv_x3_body(const ConvGemmParams& p, __bf16* __
         *reinterpret_cast<u32x4*>(d) = pack8(vb[i]);
       } else if constexpr (NP == 2) {
         u32x4 s0, s1;
-        split8h(vb[i], sb, s0, s1);
+        split8h(vb[i], sb_r[i], s0, s1);
         *reinterpret_cast<u32x4*>(d) = s0;
         *reinterpret_cast<u32x4*>(d + PB) = s1;
       } else {
@@ -369,10 +407,7 @@ __device__ __forceinline__ void conv_x3_body(const ConvGemmParams& p, __bf16* __
   if (kt_begin < kt_end) {
     load_tile(kt_begin, va0, vb0, true);
     load_tile(kt_begin + 1, va1, vb1, kt_begin + 1 < kt_end);
-    if constexpr (NP == 2) {
-      sa = amax_finish(p.amax_a, p.amax_na, amx_a);
-      sb = amax_finish(p.amax_b, p.amax_nb, amx_b);
-    }
+    finish_scales();
     store_tile(va0, vb0, smem);
     __syncthreads();
     int kt = kt_begin;
@@ -389,17 +424,33 @@ __device__ __forceinline__ void conv_x3_body(const ConvGemmParams& p, __bf16* __
       __syncthreads();
     }
     if (kt < kt_end) compute(smem);  // odd tile count: the last tile sits in stage 0
-  } else if constexpr (NP == 2) {  // no K-tiles: the (zero) accumulators still get unscaled
-    sa = amax_finish(p.amax_a, p.amax_na, amx_a);
-    sb = amax_finish(p.amax_b, p.amax_nb, amx_b);
+  } else {  // no K-tiles: the (zero) accumulators still get unscaled
+    finish_scales();
   }
 
-  if constexpr (NP == 2) {  // undo the operand scales (exact: powers of two)
-    const float inv = 1.f / (sa * sb);
+  if constexpr (NP == 2) {
+    // undo the row scales (exact: powers of two). Each row's reciprocal goes through LDS (the
+    // stages are free now; past conv_tile_stats' WM x BN floats): the threads with kq == 0 hold the
+    // scales of their loader rows, a lane's accumulators span 16 x TM rows and TN columns.
+    float* s_ia = reinterpret_cast<float*>(smem) + WM * BN;
+    float* s_ib = s_ia + BM;
+    __syncthreads();
+    if ((tid & 3) == 0) {
 #pragma unroll
-    for (int a = 0; a < TM; ++a)
+      for (int i = 0; i < A_LD; ++i) s_ia[rrow + RS * i] = 1.f / sa_r[i];
 #pragma unroll
-      for (int b = 0; b < TN; ++b) acc[a][b] *= inv;
+      for (int i = 0; i < B_LD; ++i) s_ib[rrow + RS * i] = 1.f / sb_r[i];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int b = 0; b < TN; ++b) {
+      const float ib = s_ib[wn * (BN / 2) + b * 32 + l32];
+#pragma unroll
+      for (int a = 0; a < TM; ++a)
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          acc[a][b][r] = acc[a][b][r] * s_ia[wm * (BM / WM) + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh] * ib;
+    }
   }
   conv_epilogue<BM, BN>(p, acc, reinterpret_cast<float*>(smem), m0, n0, tm_idx, split);
 }

@@ -63,11 +63,15 @@ struct ConvGemmParams {
   int pad_w;    // data gradient, sub-pixel class launches only: column pad (pad is the row pad)
   RowRemap rr;  // sub-pixel class launches: scatter output rows into dX
   const float* addend;  // optional: y += addend (same layout as y; may alias y)
-  // f16x2 engine: partial |max| values of the gathered operand (x / dY) and of the B^T rows,
-  // from their producers; the kernel derives the power-of-two operand scales from them
-  const float* amax_a;
-  const float* amax_b;
-  int amax_na, amax_nb;
+  // f16x2 engine: the operand scales are powers of two per GEMM ROW of each operand, so they
+  // factor out of every output exactly (x3_common.h):
+  //   A (gathered x / dY): one scale per image, from a_img[n] = max |A| over image n (float bits,
+  //     an activation's per-image slots, ActMaxOut); GEMM row m belongs to image m / (P*Q)
+  //   B (W rows co, or W^T rows ci): one scale per row, max over b_np partials
+  //     b_row[q * b_stride + n] (a weight's per-co / per-ci maxima, weight_prep)
+  const unsigned* a_img;
+  const float* b_row;
+  int b_np, b_stride;
 };
 
 struct WgradParams {
@@ -77,17 +81,40 @@ struct WgradParams {
   int N, H, W, C, P, Q, KH, KW, stride, pad;
   int Cout, Kdim, M, splits;
   FastDiv fd_PQ, fd_Q, fd_C, fd_KW;
-  const float* amax_dy;  // f16x2 engine: partial |max| values of dY and of x
-  const float* amax_x;
-  int amax_ndy, amax_nx;
+  // f16x2 engine: per-channel maxima (float bits, kActCopies copies each, ActMaxOut) of dY
+  // ([copies][Cout]: one scale per output row co) and of x ([copies][C]: one scale per column
+  // (tap, ci), by its channel ci)
+  const unsigned* dy_ch;
+  const unsigned* x_ch;
 };
+
+// ---- per-image / per-channel |max| of an activation (the f16x2 operand scales) ---------------
+// A producer kernel of an NHWC activation [N][HW][C] (BatchNorm apply, channel padding, the
+// standalone pass) reduces |value| per image and per channel on chip and publishes the maxima with
+// one atomicMax per (block, image) and per (block, channel) into zero-initialised slots: the
+// activation's "act max" tensor, int32 [N + kActCopies * C] = img[N] then ch[kActCopies][C] (float
+// bits; for non-negative floats the unsigned order is the float order). Block b adds its channel
+// maxima into copy b % kActCopies, so no more than 1/kActCopies of a grid's blocks meet on one
+// address; consumers take the max over the copies.
+constexpr int kActCopies = 8;
+struct ActMaxOut {
+  unsigned* img;  // [N] or nullptr (no maxima wanted)
+  unsigned* ch;   // [kActCopies][C]
+};
+inline long long act_max_elems(long long N, long long C) { return N + kActCopies * C; }
+// A conv weight [Co][T][Ci]'s maxima, float [nci * Co + nco * Ci] (nco = ceil(Co / 32), nci =
+// ceil(Ci / 32)): per-co partials [nci][Co] (max over a 32-wide ci block and all taps), then per-ci
+// partials [nco][Ci]; written by weight_prep_kernel / sgd_prep_kernel with plain stores.
+inline long long weight_max_elems(long long Co, long long Ci) {
+  return ((Ci + 31) / 32) * Co + ((Co + 31) / 32) * Ci;
+}
 
 // conv_igemm.hip (exact fp32-input MFMA)
 void conv_igemm_launch(const ConvGemmParams& p, int bm, int bn, bool dgrad, hipStream_t st);
 // conv_x3.hip (fp32-accurate 3-term bf16 split on the bf16 MFMA)
 // np = operand planes: 3 = split-bf16 (six products), 2 = f16x2 (power-of-two-scaled operands,
-// two fp16 terms, three products; needs p.amax_*), 1 = operands rounded to bf16, one product per
-// MAC (the non-parity fast mode)
+// two fp16 terms, three products; needs p.a_img / p.b_row), 1 = operands rounded to bf16, one
+// product per MAC (the non-parity fast mode)
 void conv_x3_launch(const ConvGemmParams& p, int bm, int bn, bool dgrad, hipStream_t st, int np = 3);
 void splitk_reduce_launch(const float* slab, int S, int M, int Nout, const float* bias, float* y, float* part,
                           hipStream_t st, const RowRemap* rr = nullptr, const float* addend = nullptr);
@@ -97,37 +124,33 @@ int splitk_rows_per_part();
 // x3: the split engines on the 16-bit MFMA (np as for conv_x3_launch); otherwise the exact
 // fp32-input MFMA
 void wgrad_launch(const WgradParams& p, int bm, int bn, bool x3, hipStream_t st, int np = 3);
-// partial |max| of x[0..n) into part[0..nparts) (nparts <= 1024), for operands without a fused
-// producer (the f16x2 engine's scales)
-void amax_launch(const float* x, long long n, float* part, int nparts, hipStream_t st);
-// Many tensors in one launch (a model's conv weights, once per forward): segment i's partials are
-// part[blk0[i] .. blk0[i+1]), one per block.
-constexpr int kMaxAmaxSegs = 64;
-struct MultiAmaxArgs {
-  const float* ptr[kMaxAmaxSegs];
-  long long n[kMaxAmaxSegs];
-  int blk0[kMaxAmaxSegs + 1];
-  int nseg;
-};
-void multi_amax_launch(const MultiAmaxArgs& a, float* part, hipStream_t st);
+// standalone act max of an NHWC activation [N][HW][C] (C % 4 == 0 or any C with the scalar path):
+// per-image and per-channel |max| into zeroed slots o (see ActMaxOut), for operands without a
+// fused producer
+void act_max_launch(const float* x, int N, long long HW, int C, ActMaxOut o, hipStream_t st);
 // Per-step weight preparation of a model's conv weights in one launch: for every segment (a
-// channels_last weight [Co][T][Ci]) the |max| partials (one per 32x32 (co, ci) block, f16x2
-// operand scale) and, when wt[s] != nullptr, the data-gradient operand W^T [Ci][T][Co].
+// channels_last weight [Co][T][Ci]) its maxima (weight_max_elems floats at part + pofs[s], the
+// f16x2 operand scales; one block per 32x32 (co, ci) tile) and, when wt[s] != nullptr, the
+// data-gradient operand W^T [Ci][T][Co].
+constexpr int kMaxAmaxSegs = 64;
 struct WeightPrepArgs {
   const float* w[kMaxAmaxSegs];
   float* wt[kMaxAmaxSegs];
   int co[kMaxAmaxSegs], t[kMaxAmaxSegs], ci[kMaxAmaxSegs];
   int blk0[kMaxAmaxSegs + 1];
+  long long pofs[kMaxAmaxSegs];
   int nseg;
 };
 void weight_prep_launch(const WeightPrepArgs& a, float* part, hipStream_t st);
 // SGD over an arena range fused with the next step's weight preparation (sgd_prep_kernel): one
 // descriptor per conv weight (element offset in the range, W^T destination or null, shape, first
-// |max|-partial block) and one per float4 chunk of the range outside every conv weight
+// block, offset of its maxima in the plan's buffer) and one per float4 chunk of the range outside
+// every conv weight
 struct SgdPrepSeg {
   long long off;
   float* wt;
   int co, t, ci, blk0;
+  long long pofs;
 };
 struct SgdPrepChunk {
   long long start;
@@ -135,7 +158,7 @@ struct SgdPrepChunk {
 };
 constexpr int kSgdPrepChunk4 = 1024;  // float4 per rest chunk (one workgroup)
 void sgd_prep_launch(float* p, const float* g, float* buf, const SgdPrepSeg* segs, int nseg, int nblk_w,
-                     const SgdPrepChunk* chunks, int nchunk, float* amax_part, const float* lr_ptr, float lr,
+                     const SgdPrepChunk* chunks, int nchunk, float* wmax, const float* lr_ptr, float lr,
                      float momentum, float dampening, float wd, float grad_scale, bool nesterov, bool first,
                      bool maximize, hipStream_t st, long long* counter = nullptr);
 void slab_sum_launch(const float* slab, int S, long long n, float* dst, bool accumulate, hipStream_t st);
@@ -190,25 +213,26 @@ void bn_finalize_launch(const float* part, int nparts, int rpp, int M, int C, co
                         float* stats, hipStream_t st);
 void bn_eval_stats_launch(int C, const float* gamma, const float* beta, const float* rm, const float* rv, float eps,
                           float* stats, hipStream_t st);
-// finalize + apply in one launch (training, no residual, nparts <= 128, C % 64 == 0); amax_part
-// (optional) gets bn_fin_act_grid entries
+// Every BN apply kernel below takes an ActMaxOut `am` (am.img == nullptr: none wanted): the
+// per-image / per-channel |max| of the tensor it writes (out / dy), for the consumer GEMMs' f16x2
+// operand scales.
+// finalize + apply in one launch (training, no residual, nparts <= 128, C % 64 == 0)
 bool bn_fin_act_ok(int nparts, int C, bool residual);
 int bn_fin_act_grid(int N, int H, int W, int C, bool pool, int nparts = 0);  // nparts 0: 64-channel blocks
 void bn_fin_act_launch(const float* part, int nparts, int rpp, int C, const float* gamma, const float* beta,
                        float* running_mean, float* running_var, long long* nbt, float momentum, float eps,
                        float* stats, const float* y, float* out, int N, int H, int W, bool pool, bool relu,
-                       float* amax_part, hipStream_t st);
+                       ActMaxOut am, hipStream_t st);
 // backward twin (training, no residual, nparts <= 128, C % 64 == 0, even map under pooling):
 // finalize the statistics partials (dbeta, dgamma, conv-bias gradient when gdb) and write dy in one
-// launch; amax_part (optional) gets bn_fin_act_grid entries
+// launch
 bool bn_bwd_fin_apply_ok(int nparts, int C, int H, int W, bool pool);
 void bn_bwd_fin_apply_launch(const float* part, int nparts, int ps, const float* y, const float* gout,
                              const float* stats, float* dy, float* gbeta, float* ggamma, float* gdb, int N, int H,
-                             int W, int C, bool pool, bool relu, float* amax_part, hipStream_t st);
-// amax_part (optional, bn_act_grid entries): per-block |max| of the written output
+                             int W, int C, bool pool, bool relu, ActMaxOut am, hipStream_t st);
 int bn_act_grid(int N, int H, int W, int C, bool pool);
 void bn_act_fwd_launch(const float* y, const float* stats, const float* res, float* out, int N, int H, int W, int C,
-                       bool pool, bool relu, hipStream_t st, float* amax_part = nullptr);
+                       bool pool, bool relu, hipStream_t st, ActMaxOut am = ActMaxOut{nullptr, nullptr});
 void bn_bwd_reduce_launch(const float* y, const float* gout, const float* stats, float* part, int nblocks, int N,
                           int H, int W, int C, bool pool, bool relu, const float* zout, hipStream_t st,
                           bool with_xsum = false);
@@ -217,7 +241,7 @@ void chan_finalize_launch(const float* part, int nparts, int C, float* out, floa
                           long long M = 0, int dbmode = 0);
 void bn_bwd_apply_launch(const float* y, const float* gout, const float* stats, const float* sums, float* dy,
                          float* dbias_part, int nblocks, int N, int H, int W, int C, bool pool, bool relu,
-                         const float* zout, float* dres, hipStream_t st, float* amax_part = nullptr);
+                         const float* zout, float* dres, hipStream_t st, ActMaxOut am = ActMaxOut{nullptr, nullptr});
 
 // misc.hip
 void xent_fwd_launch(const float* logits, const long long* tgt, int B, int C, float* loss, long long* correct,
@@ -238,9 +262,9 @@ void wtrans_launch(const float* w, float* wt, int Co, int T, int Ci, hipStream_t
 // sub-filter transpose: wt[ci][a][b][co] = w[co][kh0 + 2a][kw0 + 2b][ci] (a < nkh, b < nkw)
 void wtrans_sub_launch(const float* w, float* wt, int Co, int KH, int KW, int Ci, int kh0, int kw0, int nkh, int nkw,
                        hipStream_t st);
-// NHWC channel padding C (<= 4) -> 4 with zeros; amax_part (optional, pad_c4_grid entries): per-block |max|
-int pad_c4_grid(long long npix);
-void pad_c4_launch(const float* x, long long npix, int C, float* out, float* amax_part, hipStream_t st);
+// NHWC channel padding C (<= 4) -> 4 with zeros, N images of HW pixels; am (optional): the padded
+// tensor's act max (per image / per channel, see ActMaxOut)
+void pad_c4_launch(const float* x, int N, long long HW, int C, float* out, ActMaxOut am, hipStream_t st);
 // dst = mean of k <= kMaxStackSrcs tensors; srcs is a HOST array (the pointers travel in the kernel
 // arguments: no pointer-table upload, so nothing can race with a host buffer's lifetime)
 constexpr int kMaxStackSrcs = 128;

@@ -10,6 +10,7 @@
 //   torch.mean(torch.stack(inputs), 0)  /root/reference/src/Part 2a/main.py:122
 #include <algorithm>
 
+#include "act_max.h"
 #include "common.h"
 #include "kernels.h"
 #include "x3_common.h"
@@ -165,6 +166,27 @@ __global__ __launch_bounds__(256) void sgd_kernel(float* __restrict__ p, const f
   }
 }
 
+// ------------------------------------------------------------------ weight maxima
+// A 32x32 (co, ci) tile's contribution to its weight's maxima (weight_max_elems layout, kernels.h):
+// the per-co partial of its ci block and the per-ci partial of its co block. Threads fold their
+// values into s[0..32) (by co) and s[32..64) (by ci) with LDS atomics (zeroed by the caller before a
+// barrier); after a barrier the first 64 threads store the 64 partials.
+__device__ __forceinline__ void tile_max_add(unsigned* s, int co_local, int ci_local, float v) {
+  const unsigned b = __float_as_uint(fabsf(v));
+  if (b) {
+    lds_max_u32(&s[co_local], b);
+    lds_max_u32(&s[32 + ci_local], b);
+  }
+}
+__device__ __forceinline__ void tile_max_store(const unsigned* s, float* __restrict__ wmax, int Co, int Ci, int co0,
+                                               int ci0) {
+  const int t = threadIdx.x;
+  const int nci = (Ci + 31) / 32;
+  if (t < 32 && co0 + t < Co) wmax[(long long)(ci0 / 32) * Co + co0 + t] = __uint_as_float(s[t]);
+  else if (t >= 32 && t < 64 && ci0 + t - 32 < Ci)
+    wmax[(long long)nci * Co + (long long)(co0 / 32) * Ci + ci0 + t - 32] = __uint_as_float(s[t]);
+}
+
 // ------------------------------------------------------------------ SGD + next-step weight preparation
 // One pass over the parameter arena per step: the optimizer that writes W also emits what the next
 // forward / backward GEMMs need from it (weight_prep_kernel's products): the f16x2 |max| partial of
@@ -185,7 +207,7 @@ __global__ __launch_bounds__(256) void sgd_prep_kernel(float* __restrict__ p, co
   constexpr int TG = 3;
   if (counter && blockIdx.x == 0 && threadIdx.x == 0) counter[0] += 1;  // as sgd_kernel
   __shared__ float tile[TG][32][33];
-  __shared__ float red[4];
+  __shared__ unsigned smax[64];
   const bool nesterov = flags & 1, first = flags & 2, maximize = flags & 4, has_mom = flags & 8;
   const float lr = lr_ptr ? lr_ptr[0] : lr_host;
   const int b = blockIdx.x;
@@ -219,8 +241,10 @@ __global__ __launch_bounds__(256) void sgd_prep_kernel(float* __restrict__ p, co
   const __amdgpu_buffer_rsrc_t pr = make_rsrc(pw, bytes);
   const __amdgpu_buffer_rsrc_t gr = make_rsrc(g + sg.off, bytes);
   const __amdgpu_buffer_rsrc_t br = make_rsrc(has_mom && !first ? bw : pw, bytes);
-  float mx = 0.f;
+  if (threadIdx.x < 64) smax[threadIdx.x] = 0u;
+  __syncthreads();
   if ((Ci & 3) == 0) {
+    float4 mx4 = f4zero();  // |max| of the NEW (co, ci .. ci + 3) values over the taps
     // float4 along ci: thread (co row tid / 8, ci quad tid % 8) of the 32 x 32 tile, one (co, tap)
     // row of 32 ci per 8 threads (128 B), every tap of the group; the transpose goes through LDS
     // and leaves as float4 runs of 4 co of W^T [ci][tap][co]
@@ -246,7 +270,8 @@ __global__ __launch_bounds__(256) void sgd_prep_kernel(float* __restrict__ p, co
         if (off[q] != kOOB) {
           st4(pw + (off[q] >> 2), vp[q]);
           if (has_mom) st4(bw + (off[q] >> 2), vb[q]);
-          mx = fmaxf(mx, fmaxf(fmaxf(fabsf(vp[q].x), fabsf(vp[q].y)), fmaxf(fabsf(vp[q].z), fabsf(vp[q].w))));
+          mx4 = make_float4(fmaxf(mx4.x, fabsf(vp[q].x)), fmaxf(mx4.y, fabsf(vp[q].y)), fmaxf(mx4.z, fabsf(vp[q].z)),
+                            fmaxf(mx4.w, fabsf(vp[q].w)));
         }
       }
       if (wt) {
@@ -277,9 +302,15 @@ __global__ __launch_bounds__(256) void sgd_prep_kernel(float* __restrict__ p, co
         __syncthreads();
       }
     }
+    const float4 z = mx4;  // (this thread's co row rco, ci quad c4)
+    tile_max_add(smax, rco, 4 * c4, z.x);
+    tile_max_add(smax, rco, 4 * c4 + 1, z.y);
+    tile_max_add(smax, rco, 4 * c4 + 2, z.z);
+    tile_max_add(smax, rco, 4 * c4 + 3, z.w);
   } else {
     // Ci not a multiple of 4 (an RGB stem's 3 input channels): one element per lane
     const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 32 x 8
+    float mco[4] = {0.f, 0.f, 0.f, 0.f};
     for (int t0 = 0; t0 < T; t0 += TG) {
       float vp[TG][4], vg[TG][4], vb[TG][4];
       unsigned off[TG][4];
@@ -303,7 +334,7 @@ __global__ __launch_bounds__(256) void sgd_prep_kernel(float* __restrict__ p, co
           if (off[q][jj] != kOOB) {
             pw[off[q][jj] >> 2] = vp[q][jj];
             if (has_mom) bw[off[q][jj] >> 2] = vb[q][jj];
-            mx = fmaxf(mx, fabsf(vp[q][jj]));
+            mco[jj] = fmaxf(mco[jj], fabsf(vp[q][jj]));
           }
         }
       if (wt) {
@@ -325,11 +356,11 @@ __global__ __launch_bounds__(256) void sgd_prep_kernel(float* __restrict__ p, co
         __syncthreads();
       }
     }
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) tile_max_add(smax, ty + 8 * jj, tx, mco[jj]);
   }
-  mx = wave_max(mx);
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = mx;
   __syncthreads();
-  if (threadIdx.x == 0) part[b] = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+  tile_max_store(smax, part + sg.pofs, Co, Ci, co0, ci0);
 }
 
 // ------------------------------------------------------------------ augmentation
@@ -407,15 +438,16 @@ __global__ __launch_bounds__(256) void wtrans_kernel(const float* __restrict__ w
 
 // ------------------------------------------------------------------ weight preparation
 // One launch for all conv weights of a step (replaces a transpose launch per layer plus the
-// |max| pass): block (segment, co32, ci32) walks the T taps of its 32x32 (co, ci) block, keeps the
-// block's |max| (one partial per block) and, when asked, writes the tile transposed through LDS.
+// |max| pass): block (segment, co32, ci32) walks the T taps of its 32x32 (co, ci) block, writes its
+// per-co and per-ci |max| partials (the f16x2 operand scales of the weight's two GEMM roles) and,
+// when asked, the tile transposed through LDS.
 // Taps go in groups of TG: all of a group's loads are issued before any is used (branch-free: out
 // of range elements read 0 through the buffer range check), so a 3x3 filter costs one memory round
 // trip per block instead of nine.
 __global__ __launch_bounds__(256) void weight_prep_kernel(WeightPrepArgs a, float* __restrict__ part) {
   constexpr int TG = 9;
   __shared__ float tile[TG][32][33];
-  __shared__ float red[4];
+  __shared__ unsigned smax[64];
   const int b = blockIdx.x;
   int seg = 0;
   while (seg + 1 < a.nseg && a.blk0[seg + 1] <= b) ++seg;
@@ -427,7 +459,9 @@ __global__ __launch_bounds__(256) void weight_prep_kernel(WeightPrepArgs a, floa
   const int co0 = (local / nci) * 32, ci0 = (local % nci) * 32;
   const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 32 x 8
   const __amdgpu_buffer_rsrc_t wr = make_rsrc(w, (unsigned)((long long)Co * T * Ci * 4));
-  float m = 0.f;
+  if (threadIdx.x < 64) smax[threadIdx.x] = 0u;
+  __syncthreads();
+  float mco[4] = {0.f, 0.f, 0.f, 0.f};  // |max| of (co0 + ty + 8 jj, ci0 + tx) over the taps
   for (int t0 = 0; t0 < T; t0 += TG) {
     float v[TG][4];
 #pragma unroll
@@ -441,7 +475,7 @@ __global__ __launch_bounds__(256) void weight_prep_kernel(WeightPrepArgs a, floa
 #pragma unroll
     for (int g = 0; g < TG; ++g)
 #pragma unroll
-      for (int jj = 0; jj < 4; ++jj) m = fmaxf(m, fabsf(v[g][jj]));
+      for (int jj = 0; jj < 4; ++jj) mco[jj] = fmaxf(mco[jj], fabsf(v[g][jj]));
     if (wt) {
 #pragma unroll
       for (int g = 0; g < TG; ++g)
@@ -461,34 +495,47 @@ __global__ __launch_bounds__(256) void weight_prep_kernel(WeightPrepArgs a, floa
       __syncthreads();
     }
   }
-  m = wave_max(m);
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+#pragma unroll
+  for (int jj = 0; jj < 4; ++jj) tile_max_add(smax, ty + 8 * jj, tx, mco[jj]);
   __syncthreads();
-  if (threadIdx.x == 0) part[b] = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+  tile_max_store(smax, part + a.pofs[seg], Co, Ci, co0, ci0);
 }
 
 // ------------------------------------------------------------------ channel padding
 // out[p][0..C4) = (x[p][0..C), 0...) for NHWC pixels p: the RGB stem's 3 -> 4 channel padding in
-// one pass (one float4 store per pixel), plus the per-block |max| the f16x2 GEMM scales need.
-__global__ __launch_bounds__(256) void pad_c4_kernel(const float* __restrict__ x, long long npix, int C,
-                                                     float* __restrict__ out, float* __restrict__ amax_part) {
-  float am = 0.f;
-  for (long long p = (long long)blockIdx.x * 256 + threadIdx.x; p < npix; p += (long long)gridDim.x * 256) {
+// one pass (one float4 store per pixel) over a contiguous pixel range per block, plus the padded
+// tensor's per-image / per-channel |max| (act_max.h) the f16x2 GEMM scales need.
+__global__ __launch_bounds__(256) void pad_c4_kernel(const float* __restrict__ x, int N, long long HW, int C,
+                                                     float* __restrict__ out, FastDiv fd_HW, ActMaxOut am) {
+  __shared__ ActMaxBlock<4> sam;
+  const bool want = am.img != nullptr;
+  const long long npix = (long long)N * HW;
+  const long long per = (npix + gridDim.x - 1) / gridDim.x;
+  const long long p0 = (long long)blockIdx.x * per, p1 = min(npix, p0 + per);
+  const int img0 = (int)(min(p0, npix - 1) / HW);
+  if (want) {
+    sam.init(threadIdx.x, 256);
+    __syncthreads();
+  }
+  ImgRun run;
+  float4 cm = f4zero();
+  for (long long p = p0 + threadIdx.x; p < p1; p += 256) {
     const float* src = x + p * C;
     float v[4];
 #pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      v[c] = c < C ? src[c] : 0.f;
-      am = fmaxf(am, fabsf(v[c]));
+    for (int c = 0; c < 4; ++c) v[c] = c < C ? src[c] : 0.f;
+    const float4 z = make_float4(v[0], v[1], v[2], v[3]);
+    st4(out + p * 4, z);
+    if (want) {
+      run.add(fdiv((int)p, fd_HW), absmax4(z), sam, img0, am);
+      cm = absmax4(cm, z);
     }
-    st4(out + p * 4, make_float4(v[0], v[1], v[2], v[3]));
   }
-  if (amax_part) {
-    __shared__ float red[4];
-    am = wave_max(am);
-    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = am;
+  if (want) {
+    run.flush(sam, img0, am);
+    sam.add_ch4(0, cm);
     __syncthreads();
-    if (threadIdx.x == 0) amax_part[blockIdx.x] = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+    sam.publish(am, img0, N, 0, 4, 4, blockIdx.x % kActCopies, threadIdx.x, 256);
   }
 }
 
@@ -761,13 +808,13 @@ void sgd_launch(float* p, const float* g, float* buf, long long n, const float* 
                      dampening, wd, grad_scale, flags, counter);
 }
 void sgd_prep_launch(float* p, const float* g, float* buf, const SgdPrepSeg* segs, int nseg, int nblk_w,
-                     const SgdPrepChunk* chunks, int nchunk, float* amax_part, const float* lr_ptr, float lr,
+                     const SgdPrepChunk* chunks, int nchunk, float* wmax, const float* lr_ptr, float lr,
                      float momentum, float dampening, float wd, float grad_scale, bool nesterov, bool first,
                      bool maximize, hipStream_t st, long long* counter) {
   const int flags = (nesterov ? 1 : 0) | (first ? 2 : 0) | (maximize ? 4 : 0) | (momentum != 0.f ? 8 : 0);
   if (nblk_w + nchunk <= 0) return;
   hipLaunchKernelGGL(sgd_prep_kernel, dim3(nblk_w + nchunk), dim3(256), 0, st, p, g, buf, segs, nseg, nblk_w, chunks,
-                     amax_part, lr_ptr, lr, momentum, dampening, wd, grad_scale, flags, counter);
+                     wmax, lr_ptr, lr, momentum, dampening, wd, grad_scale, flags, counter);
 }
 void augment_launch(const unsigned char* imgs, const long long* idx, long long idx_off, int B, int H, int W, int C,
                     const float* mean, const float* inv_std, int pad, bool flip, const long long* counter,
@@ -788,9 +835,10 @@ void wtrans_launch(const float* w, float* wt, int Co, int T, int Ci, hipStream_t
   dim3 grid((Ci + 31) / 32, (Co + 31) / 32, T);
   hipLaunchKernelGGL(wtrans_kernel, grid, dim3(256), 0, st, w, wt, Co, T, Ci);
 }
-int pad_c4_grid(long long npix) { return (int)std::min<long long>(1024, std::max<long long>(1, (npix + 255) / 256)); }
-void pad_c4_launch(const float* x, long long npix, int C, float* out, float* amax_part, hipStream_t st) {
-  hipLaunchKernelGGL(pad_c4_kernel, dim3(pad_c4_grid(npix)), dim3(256), 0, st, x, npix, C, out, amax_part);
+void pad_c4_launch(const float* x, int N, long long HW, int C, float* out, ActMaxOut am, hipStream_t st) {
+  const long long npix = (long long)N * HW;
+  const int grid = (int)std::min<long long>(1024, std::max<long long>(1, (npix + 255) / 256));
+  hipLaunchKernelGGL(pad_c4_kernel, dim3(grid), dim3(256), 0, st, x, N, HW, C, out, make_fastdiv((int)HW), am);
 }
 void stack_mean_launch(const float* const* srcs, int k, long long n, float* dst, hipStream_t st) {
   StackSrcs a{};

@@ -103,17 +103,6 @@ __device__ __forceinline__ void stem_y_mfma(const float (&lo)[9][2], const float
         acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x2f32(hi[t][a], wl[32 * b + i][4 * t + 2 + h], acc[a][b], 0, 0, 0);
       }
 }
-// LDS barrier that does not wait for global loads still in flight: __syncthreads' fence would
-// drain them (vmcnt(0)). The release / acquire fences are workgroup-scope and LDS-only
-// ("local" address space), so they order the LDS stores before the barrier and the LDS loads after
-// it in the compiler's memory model (a bare s_barrier is not a memory operation to LLVM, so nothing
-// would stop an LDS access from being scheduled across it) while lowering to lgkmcnt(0) alone.
-__device__ __forceinline__ void lds_barrier() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
-  __builtin_amdgcn_s_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
-}
-
 // ---------------------------------------------------------------------------------- forward
 // y = conv(x) + b (when y != nullptr) and the per-256-row BatchNorm partials (mean, M2).
 __global__ __launch_bounds__(256, 2) void stem_fwd_kernel(const float* __restrict__ x, const float* __restrict__ w,

@@ -14,6 +14,9 @@
 #include <cstdlib>
 #include <type_traits>
 
+#include <algorithm>
+
+#include "act_max.h"
 #include "common.h"
 #include "kernels.h"
 #include "x3_common.h"
@@ -301,67 +304,75 @@ void wgrad_launch(const WgradParams& p, int bm, int bn, bool x3, hipStream_t st,
   else wgrad_launch_t<64, 64>(p, x3, st, np);
 }
 
-// ---------------------------------------------------------------- operand |max| partials
+// ---------------------------------------------------------------- standalone act max
 namespace {
-__global__ __launch_bounds__(256) void amax_kernel(const float* __restrict__ x, long long n, float* __restrict__ part) {
-  __shared__ float red[4];
-  float m = 0.f;
-  const long long stride = (long long)gridDim.x * 256;
-  long long i = (long long)blockIdx.x * 256 + threadIdx.x;
-  if ((reinterpret_cast<uintptr_t>(x) & 15) == 0) {
-    const long long n4 = n >> 2;
-    const float4* x4 = reinterpret_cast<const float4*>(x);
-    for (long long j = i; j < n4; j += stride) {
-      const float4 v = x4[j];
-      m = fmaxf(m, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
-    }
-    for (long long j = (n4 << 2) + i; j < n; j += stride) m = fmaxf(m, fabsf(x[j]));
-  } else {
-    for (long long j = i; j < n; j += stride) m = fmaxf(m, fabsf(x[j]));
-  }
-  m = wave_max(m);
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+// Per-image / per-channel |max| of an NHWC activation [N][HW][C] (act_max.h) for operands no fused
+// producer measured (user inputs, a classifier's input, tests). Block b reads the contiguous range
+// [b * per, (b + 1) * per) of float4s (VEC, C % 4 == 0; per a multiple of 256 and of C / 4 when
+// qmode != 0, as in bn_act_fwd_kernel) or of floats.
+template <bool VEC>
+__global__ __launch_bounds__(256) void act_max_kernel(const float* __restrict__ x, int N, int C, int total, int per,
+                                                      int qmode, FastDiv fd_U, FastDiv fd_HW, ActMaxOut am) {
+  __shared__ ActMaxBlock<kMaxActC> sam;
+  const int tid = threadIdx.x;
+  const int U = VEC ? C / 4 : C;  // units (float4 or float) per pixel
+  const int i0 = blockIdx.x * per, i1 = min(total, i0 + per);
+  const int img0 = fdiv(fdiv(min(i0, total - 1), fd_U), fd_HW);
+  const bool lds_ch = C <= kMaxActC;
+  sam.init(tid, 256);
   __syncthreads();
-  if (threadIdx.x == 0) part[blockIdx.x] = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
-}
-
-// block b of segment i (blk0[i] <= b < blk0[i+1]) reduces a strided share of tensor i
-__global__ __launch_bounds__(256) void multi_amax_kernel(MultiAmaxArgs a, float* __restrict__ part) {
-  __shared__ float red[4];
-  const int b = blockIdx.x;
-  int seg = 0;
-  while (seg + 1 < a.nseg && a.blk0[seg + 1] <= b) ++seg;
-  const int nb = a.blk0[seg + 1] - a.blk0[seg];
-  const float* x = a.ptr[seg];
-  const long long n = a.n[seg];
-  const long long stride = (long long)nb * 256;
-  float m = 0.f;
-  const long long i = (long long)(b - a.blk0[seg]) * 256 + threadIdx.x;
-  if ((reinterpret_cast<uintptr_t>(x) & 15) == 0) {
-    const long long n4 = n >> 2;
-    const float4* x4 = reinterpret_cast<const float4*>(x);
-    for (long long j = i; j < n4; j += stride) {
-      const float4 v = x4[j];
-      m = fmaxf(m, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+  ImgRun run;
+  float4 cm[2] = {f4zero(), f4zero()};
+  int k = 0;
+  for (int i = i0 + tid; i < i1; i += 256, ++k) {
+    const int pix = fdiv(i, fd_U);
+    const int u = i - pix * U;
+    const int img = fdiv(pix, fd_HW);
+    if constexpr (VEC) {
+      const float4 v = ld4(x + 4LL * i);
+      run.add(img, absmax4(v), sam, img0, am);
+      if (qmode == 1 || (qmode == 2 && !(k & 1))) cm[0] = absmax4(cm[0], v);
+      else if (qmode == 2) cm[1] = absmax4(cm[1], v);
+      else if (lds_ch) sam.add_ch4(4 * u, make_float4(fabsf(v.x), fabsf(v.y), fabsf(v.z), fabsf(v.w)));
+      else {
+        const float e[4] = {fabsf(v.x), fabsf(v.y), fabsf(v.z), fabsf(v.w)};
+        for (int j = 0; j < 4; ++j)
+          if (__float_as_uint(e[j])) glb_max_u32(&am.ch[4 * u + j], __float_as_uint(e[j]));
+      }
+    } else {
+      const float v = fabsf(x[i]);
+      run.add(img, v, sam, img0, am);
+      if (lds_ch) sam.add_ch(u, v);
+      else if (__float_as_uint(v)) glb_max_u32(&am.ch[u], __float_as_uint(v));
     }
-    for (long long j = (n4 << 2) + i; j < n; j += stride) m = fmaxf(m, fabsf(x[j]));
-  } else {
-    for (long long j = i; j < n; j += stride) m = fmaxf(m, fabsf(x[j]));
   }
-  m = wave_max(m);
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+  run.flush(sam, img0, am);
+  if (VEC && qmode == 1 && i0 + tid < i1) sam.add_ch4(4 * (tid % U), cm[0]);
+  if (VEC && qmode == 2) {
+    if (i0 + tid < i1) sam.add_ch4(4 * tid, cm[0]);
+    if (i0 + tid + 256 < i1) sam.add_ch4(4 * (tid + 256), cm[1]);
+  }
   __syncthreads();
-  if (threadIdx.x == 0) part[b] = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+  sam.publish(am, img0, N, 0, lds_ch ? C : 0, C, blockIdx.x % kActCopies, tid, 256);
 }
 }  // namespace
 
-void amax_launch(const float* x, long long n, float* part, int nparts, hipStream_t st) {
-  hipLaunchKernelGGL(amax_kernel, dim3(nparts), dim3(256), 0, st, x, n, part);
-}
-
-void multi_amax_launch(const MultiAmaxArgs& a, float* part, hipStream_t st) {
-  if (a.nseg <= 0) return;
-  hipLaunchKernelGGL(multi_amax_kernel, dim3(a.blk0[a.nseg]), dim3(256), 0, st, a, part);
+void act_max_launch(const float* x, int N, long long HW, int C, ActMaxOut o, hipStream_t st) {
+  const bool vec = (C % 4) == 0 && (reinterpret_cast<uintptr_t>(x) & 15) == 0;
+  const int U = vec ? C / 4 : C;
+  const long long total = (long long)N * HW * U;
+  if (total <= 0) return;
+  const int qmode = !vec ? 0 : (U <= 256 && (256 % U) == 0) ? 1 : U == 512 ? 2 : 0;
+  const long long unit = qmode == 2 ? 512 : 256;
+  const long long blocks = std::min<long long>(1024, std::max<long long>(1, (total + 255) / 256));
+  const long long per = std::max(unit, ((total + blocks - 1) / blocks + unit - 1) / unit * unit);
+  const dim3 grid((unsigned)((total + per - 1) / per));
+  if (vec)
+    hipLaunchKernelGGL(act_max_kernel<true>, grid, dim3(256), 0, st, x, N, C, (int)total, (int)per, qmode,
+                       make_fastdiv(U), make_fastdiv((int)HW), o);
+  else
+    hipLaunchKernelGGL(act_max_kernel<false>, grid, dim3(256), 0, st, x, N, C, (int)total, (int)per, 0,
+                       make_fastdiv(U), make_fastdiv((int)HW), o);
 }
 
 void slab_sum_launch(const float* slab, int S, long long n, float* dst, bool accumulate, hipStream_t st) {

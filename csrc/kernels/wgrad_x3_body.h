@@ -25,9 +25,9 @@ constexpr int WBK = 32;
 constexpr int XLD = WBK + 8;  // bf16 per LDS row
 
 // v[r] = row m+r of this thread's 4 columns; write, per column and plane, the RPT m-values
-// (packed bf16 pairs) into the [col][m] image at dst.
+// (packed bf16 pairs) into the [col][m] image at dst. sc[c]: column c's f16x2 scale (NP == 2).
 template <int RPT, int NP>
-__device__ __forceinline__ void split_store_cols(const float4 (&v)[RPT], __bf16* dst, int plane, float sc = 1.f) {
+__device__ __forceinline__ void split_store_cols(const float4 (&v)[RPT], __bf16* dst, int plane, const float (&sc)[4]) {
   // (component access by constant index only: a pointer walk over `v` makes the compiler
   // promote the register array to LDS scratch)
   auto comp = [](const float4& q, int c) { return c == 0 ? q.x : c == 1 ? q.y : c == 2 ? q.z : q.w; };
@@ -37,7 +37,7 @@ __device__ __forceinline__ void split_store_cols(const float4 (&v)[RPT], __bf16*
 #pragma unroll
     for (int r = 0; r < RPT / 2; ++r) {
       if constexpr (NP == 1) h0[r] = pack_bf16x2(f32x2{comp(v[2 * r], c), comp(v[2 * r + 1], c)});
-      else if constexpr (NP == 2) split_pair_h(comp(v[2 * r], c), comp(v[2 * r + 1], c), sc, h0[r], h1[r]);
+      else if constexpr (NP == 2) split_pair_h(comp(v[2 * r], c), comp(v[2 * r + 1], c), sc[c], h0[r], h1[r]);
       else split_pair(comp(v[2 * r], c), comp(v[2 * r + 1], c), h0[r], h1[r], h2[r]);
     }
     __bf16* d = dst + c * XLD;
@@ -127,16 +127,49 @@ __device__ __forceinline__ void wgrad_x3_body(const WgradParams& p, __bf16* __re
   for (int i = 0; i < RPT_A; ++i)
     a_off[i] = co < p.Cout ? (unsigned)(mul24(a_mq * RPT_A + i, p.Cout) + co) * 4u : kOOB;
   const __amdgpu_buffer_rsrc_t xr = make_rsrc(p.x, (unsigned)p.N * (unsigned)HWC * 4u);
-  float sa = 1.f, sb = 1.f;  // f16x2 operand scales (dY, x): partial loads first, waited for after
-  float amx_a[NP == 2 ? kAmaxK : 1], amx_b[NP == 2 ? kAmaxK : 1];  // the first tiles' loads are issued
+  // f16x2: one power-of-two scale per output row co (dY's channel co) and per output column
+  // (tap, ci) (x's channel ci), from the producers' per-channel maxima (x3_common.h). Thread t
+  // reduces the kActCopies copies of row t of the BM + BN rows and columns: loads issued here,
+  // waited for after the first tiles' loads; the scales meet in LDS (stage 1 of the pipelined
+  // kernel, or stage 0 behind a second barrier), and every thread keeps the 4 of its A columns
+  // (sa4) and of its B columns (sb4).
+  float sa4[4] = {1.f, 1.f, 1.f, 1.f}, sb4[4] = {1.f, 1.f, 1.f, 1.f};
+  unsigned chm[NP == 2 ? kActCopies : 1];
   if constexpr (NP == 2) {
-    amax_issue(p.amax_dy, p.amax_ndy, amx_a);
-    amax_issue(p.amax_x, p.amax_nx, amx_b);
+    static_assert(BM + BN <= NT, "one scale row per thread");
+    const int j = tid;
+    unsigned base = kOOB, stride = 0;
+    const unsigned* src = p.dy_ch;
+    unsigned nrow = (unsigned)p.Cout;
+    if (j < BM) {
+      if (co0 + j < p.Cout) base = (unsigned)(co0 + j) * 4u;
+      stride = (unsigned)p.Cout * 4u;
+    } else if (j < BM + BN) {
+      const int k = r0 + j - BM;
+      src = p.x_ch;
+      nrow = (unsigned)p.C;
+      if (k < p.Kdim) base = (unsigned)(k - fdiv(k, p.fd_C) * p.C) * 4u;
+      stride = (unsigned)p.C * 4u;
+    }
+    const __amdgpu_buffer_rsrc_t cr = make_rsrc(src, (unsigned)kActCopies * nrow * 4u);
+#pragma unroll
+    for (int q = 0; q < kActCopies; ++q)
+      chm[q] = __builtin_amdgcn_raw_buffer_load_b32(cr, (int)(base == kOOB ? kOOB : base + q * stride), 0, 0);
   }
   auto finish_scales = [&]() {
     if constexpr (NP == 2) {
-      sa = amax_finish(p.amax_dy, p.amax_ndy, amx_a);
-      sb = amax_finish(p.amax_x, p.amax_nx, amx_b);
+      float* scr = reinterpret_cast<float*>(smem + (PIPE ? STAGE : 0));
+      unsigned m = 0u;
+#pragma unroll
+      for (int q = 0; q < kActCopies; ++q) m = max(m, chm[q]);
+      if (tid < BM + BN) scr[tid] = pow2_scale(__uint_as_float(m));
+      lds_barrier();
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        sa4[c] = scr[a_cg * 4 + c];
+        sb4[c] = scr[BM + b_cg * 4 + c];
+      }
+      if constexpr (!PIPE) lds_barrier();  // stage 0 is the first tile's destination
     }
   };
 
@@ -201,8 +234,8 @@ __device__ __forceinline__ void wgrad_x3_body(const WgradParams& p, __bf16* __re
     }
   };
   auto store_tile = [&](const float4 (&ra)[RPT_A], const float4 (&rb)[RPT_B], __bf16* st) {
-    split_store_cols<RPT_A, NP>(ra, st + (a_cg * 4) * XLD + a_mq * RPT_A, PA, sa);
-    split_store_cols<RPT_B, NP>(rb, st + NP * PA + (b_cg * 4) * XLD + b_mq * RPT_B, PB, sb);
+    split_store_cols<RPT_A, NP>(ra, st + (a_cg * 4) * XLD + a_mq * RPT_A, PA, sa4);
+    split_store_cols<RPT_B, NP>(rb, st + NP * PA + (b_cg * 4) * XLD + b_mq * RPT_B, PB, sb4);
   };
 
   f32x16 acc[TM][TN];
@@ -315,14 +348,31 @@ __device__ __forceinline__ void wgrad_x3_body(const WgradParams& p, __bf16* __re
         __syncthreads();
       }
     }
+  } else {
+    finish_scales();
   }
 
-  if constexpr (NP == 2) {  // undo the operand scales (exact: powers of two)
-    const float inv = 1.f / (sa * sb);
+  if constexpr (NP == 2) {
+    // undo the row / column scales (exact: powers of two): the reciprocals meet in LDS (free now),
+    // written by the threads of the first m group of every A / B column group
+    float* s_ia = reinterpret_cast<float*>(smem);
+    float* s_ib = s_ia + BM;
+    __syncthreads();
 #pragma unroll
-    for (int a = 0; a < TM; ++a)
+    for (int c = 0; c < 4; ++c) {
+      if (a_mq == 0) s_ia[a_cg * 4 + c] = 1.f / sa4[c];
+      if (b_mq == 0) s_ib[b_cg * 4 + c] = 1.f / sb4[c];
+    }
+    __syncthreads();
 #pragma unroll
-      for (int b = 0; b < TN; ++b) acc[a][b] *= inv;
+    for (int b = 0; b < TN; ++b) {
+      const float ib = s_ib[wn * (BN / 2) + b * 32 + l32];
+#pragma unroll
+      for (int a = 0; a < TM; ++a)
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          acc[a][b][r] = acc[a][b][r] * s_ia[wm * (BM / WMW) + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh] * ib;
+    }
   }
   float* out = p.out + (long long)split * p.Cout * p.Kdim;
   const bool full = co0 + BM <= p.Cout && r0 + BN <= p.Kdim;

@@ -39,11 +39,19 @@ __device__ __forceinline__ void split_pair(float x, float y, unsigned& h0, unsig
 //
 // fp16 keeps 11 significant bits, so two terms carry 22 -- against 24 for fp32 and 3 x 8 for
 // the bf16 split -- and the product needs three MFMA terms (h0g0 + h0g1 + h1g0, dropped
-// h1g1 <= 2^-22 |ab|) instead of six. fp16's 5-bit exponent is what the per-tensor scale s = 2^e
-// is for: it maps the tensor's |max| to [2^14, 2^15), so nothing overflows and everything within
-// 2^18 of the max keeps all 22 bits (smaller values degrade gracefully to an absolute error of
-// 2^-40 max|x|, far below the fp32 accumulation error of the dot products they enter). s is
-// exact, so dividing the accumulator by s_a s_b in the epilogue is exact too.
+// h1g1 <= 2^-22 |ab|) instead of six. fp16's 5-bit exponent is what the scale s = 2^e is for: it
+// maps a group's |max| to [2^14, 2^15), so nothing overflows and everything within 2^17 of the
+// group max keeps all 22 bits (smaller values degrade to an absolute error of ~2^-39 of the group
+// max).
+//
+// The groups are GEMM rows, one scale per row of each operand (per image for the gathered
+// activation, per output / input channel for the weights, per channel for both weight-gradient
+// operands): an output y[m][n] = sum_k a[m][k] b[n][k] sees one scale s_m of A and one s_n of B,
+// so y = (sum_k (s_m a)(s_n b)) / (s_m s_n) -- the scales factor out of every dot product and the
+// epilogue's division is exact. The only values that lose bits are those more than 2^17 below the
+// max of their own row, i.e. dynamic range WITHIN one image (or one channel) along the reduction,
+// whose contribution to that output is then < 2^-39 max_k |a[m][k]| sum_k |b[n][k]|
+// (tests/test_accuracy_gpu.py documents that limit).
 typedef _Float16 f16x2_v __attribute__((ext_vector_type(2)));
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 
@@ -64,51 +72,14 @@ __device__ __forceinline__ void split_pair_h(float x, float y, float s, unsigned
   h1 = pack_f16x2(f32x2{__builtin_fmaf(x, s, -w.x), __builtin_fmaf(y, s, -w.y)});
 }
 
-// Power-of-two operand scale from a producer's partial |max| values part[0..n): maps the max to
-// [2^14, 2^15). Every lane of the calling wave gets the same value (no LDS, no barrier). A zero,
-// inf or NaN max gives 1 (zeros stay zeros; non-finite inputs propagate as in fp32).
-// The partials are read 32 independent buffer loads per lane at a time (2048 per round trip; past n
-// they read 0, neutral for |max|): a one-load-per-iteration loop waited a full memory latency per
-// 128 partials in every wave, ~16 round trips at the start of each GEMM fed by a 2048-block producer.
-// Split in two so a kernel can issue the first 2048 (amax_issue), then its first operand tiles, and
-// only then wait (amax_finish): the scale's round trip overlaps the tile loads.
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t amax_rsrc(const float* part, int n) {
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(part), (short)0, n * 4, 0x00020000);
-}
-constexpr int kAmaxK = 32;  // loads per lane per round trip
-__device__ __forceinline__ void amax_issue(const float* __restrict__ part, int n, float (&v)[kAmaxK]) {
-  const int lane = threadIdx.x & 63;
-  const __amdgpu_buffer_rsrc_t r = amax_rsrc(part, n);
-#pragma unroll
-  for (int k = 0; k < kAmaxK; ++k) v[k] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, (64 * k + lane) * 4, 0, 0));
-}
-__device__ __forceinline__ float amax_finish(const float* __restrict__ part, int n, const float (&v0)[kAmaxK]) {
-  const int lane = threadIdx.x & 63;
-  float m = 0.f;
-#pragma unroll
-  for (int k = 0; k < kAmaxK; ++k) m = fmaxf(m, v0[k]);
-  if (n > 64 * kAmaxK) {
-    const __amdgpu_buffer_rsrc_t r = amax_rsrc(part, n);
-    for (int base = 64 * kAmaxK; base < n; base += 64 * 16) {
-      float v[16];
-#pragma unroll
-      for (int k = 0; k < 16; ++k)
-        v[k] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, (base + 64 * k + lane) * 4, 0, 0));
-#pragma unroll
-      for (int k = 0; k < 16; ++k) m = fmaxf(m, v[k]);
-    }
-  }
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+// Power-of-two operand scale of a group whose |max| is m: maps m to [2^14, 2^15). A zero, inf or
+// NaN max gives 1 (zeros stay zeros; non-finite inputs propagate as in fp32). The exponent is
+// clamped to +-100 so both the scale and its reciprocal stay normal fp32 numbers.
+__device__ __forceinline__ float pow2_scale(float m) {
   if (!(m > 0.f) || !(m < 3.0e38f)) return 1.f;
   int e;
   (void)frexpf(m, &e);  // m < 2^e
   return ldexpf(1.f, max(-100, min(100, 15 - e)));
-}
-__device__ __forceinline__ float amax_scale(const float* __restrict__ part, int n) {
-  float v[kAmaxK];
-  amax_issue(part, n, v);
-  return amax_finish(part, n, v);
 }
 
 // Raw buffer resource over [base, base + bytes): loads past `bytes` return 0 (hardware range

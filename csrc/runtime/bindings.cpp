@@ -36,8 +36,11 @@ PYBIND11_MODULE(_C, m) {
         py::arg("beta"), py::arg("running_mean"), py::arg("running_var"), py::arg("num_batches_tracked"),
         py::arg("momentum"), py::arg("eps"), py::arg("training"), py::arg("stride"), py::arg("pad"), py::arg("pool"),
         py::arg("relu"), py::arg("residual"), py::arg("x_amax") = py::none(), py::arg("w_amax") = py::none());
-  m.def("multi_amax", &multi_amax, py::arg("tensors"),
-        "f16x2 engine: partial |max| values of many tensors in one launch (empty list for other engines)");
+  m.def("act_max", &act_max_of, py::arg("t"),
+        "f16x2 engine: an activation's per-image / per-channel |max| slots by the standalone pass (int32 [N + "
+        "copies * C], float bits; undefined tensor for other engines)");
+  m.def("act_max_memsets", &act_max_memsets, "slot-chunk memsets issued so far (tests)");
+  m.def("act_max_copies", &act_max_copies, "per-channel slot copies of an act max");
   m.def("conv_bn_act_bwd", &conv_bn_act_bwd, py::arg("gout"), py::arg("x"), py::arg("w"), py::arg("y"),
         py::arg("stats"), py::arg("stride"), py::arg("pad"), py::arg("pool"), py::arg("relu"), py::arg("need_dx"),
         py::arg("has_bias"), py::arg("zout") = py::none(), py::arg("training") = true, py::arg("dw_out") = py::none(),
@@ -46,7 +49,7 @@ PYBIND11_MODULE(_C, m) {
         py::arg("w_t") = py::none(), py::arg("part_in") = py::none(), py::arg("prev_y") = py::none(),
         py::arg("prev_stats") = py::none(), py::arg("prev_pool") = false, py::arg("prev_relu") = false,
         py::arg("prev_ps") = 2, py::arg("bias") = py::none(),
-        "fused block backward; returns (dx, dw, db, dgamma, dbeta, dres, prev_part). prev_* describe the BN whose "
+        "fused block backward; returns (dx, dw, db, dgamma, dbeta, dres, prev_part, dy_amax). prev_* describe the BN whose "
         "output is x: its statistics reduction is then fused into this block's data-gradient reduction and returned "
         "as prev_part (undefined when not fused), which that block's backward takes as part_in");
   m.def("weight_prep_into", &weight_prep_into, py::arg("weights"), py::arg("want_t"), py::arg("amax"), py::arg("wts"),
@@ -81,6 +84,27 @@ PYBIND11_MODULE(_C, m) {
   m.def("gpu_sleep", &gpu_sleep, py::arg("us"), "idle one workgroup ~us on the current stream");
   m.def("gpu_wall_clock_khz", &gpu_wall_clock_khz);
   m.def("gpu_timestamp", &gpu_timestamp, py::arg("ts"), py::arg("idx"), "ts[idx] = GPU wall clock (100 MHz)");
+  m.def("create_stream",
+        [](int priority, bool nonblocking, bool cu_mask) {
+          hipStream_t st = nullptr;
+          if (cu_mask) {
+            uint32_t mask[8];
+            for (auto& w : mask) w = 0xffffffffu;  // every CU: a stream on a queue of its own
+            TORCH_CHECK(hipExtStreamCreateWithCUMask(&st, 8, mask) == hipSuccess, "hipExtStreamCreateWithCUMask failed");
+          } else {
+            TORCH_CHECK(hipStreamCreateWithPriority(&st, nonblocking ? hipStreamNonBlocking : hipStreamDefault,
+                                                    priority) == hipSuccess,
+                        "hipStreamCreateWithPriority failed");
+          }
+          return reinterpret_cast<intptr_t>(st);
+        },
+        py::arg("priority") = 0, py::arg("nonblocking") = true, py::arg("cu_mask") = false,
+        "diagnostics: a raw HIP stream (never destroyed) for torch.cuda.ExternalStream");
+  m.def("stream_priority_range", [] {
+    int lo = 0, hi = 0;
+    hipDeviceGetStreamPriorityRange(&lo, &hi);
+    return std::vector<int>{lo, hi};
+  });
   m.def("maxpool2d_fwd", &maxpool2d_fwd);
   m.def("maxpool2d_bwd", &maxpool2d_bwd);
   m.def("avgpool_fwd", &avgpool_fwd);

@@ -88,68 +88,172 @@ bool f16x2_mode() { return conv_gemm_mode() == 3; }
 // 16-bit operand planes of the split kernels for the current engine
 int split_planes() { return conv_gemm_mode() == 2 ? 1 : conv_gemm_mode() == 3 ? 2 : 3; }
 
-// Partial |max| values of an f16x2 GEMM operand: the producer's (when the caller has them) or a
-// standalone pass. Undefined outside the f16x2 engine.
-at::Tensor amax_parts(const at::Tensor& t, const c10::optional<at::Tensor>& given, hipStream_t st) {
+// ---------------------------------------------------------------- act max slots
+// An activation's per-image / per-channel |max| slots (ActMaxOut, kernels.h) must start at zero:
+// its producer atomically maxes into them. They are views into chunks of device memory zeroed by
+// ONE memset per chunk, not per producer:
+//  * eager: a ring of chunks; the current chunk is bumped through, and a chunk is re-zeroed and
+//    reused only once no slot view of it is alive (its storage is then held by the ring alone);
+//  * inside a hipGraph capture: every capture takes fresh chunks (from the graph's memory pool,
+//    kept alive with it) whose memset is captured, so each replay re-zeroes them before its
+//    producers run.
+// Everything is ordered on the current stream, like the caching allocator's reuse.
+constexpr long long kSlotChunk = 1LL << 16;  // int32 slots per chunk (256 KB)
+struct SlotPool {
+  std::vector<at::Tensor> ring;
+  std::vector<long long> used;
+  int cur = -1;
+  unsigned long long cap_id = 0;
+  at::Tensor cap_cur;
+  long long cap_used = 0;
+  std::vector<at::Tensor> cap_keep;
+};
+
+std::atomic<long long>& slot_memsets() {
+  static std::atomic<long long> n{0};
+  return n;
+}
+
+at::Tensor alloc_slots(long long n, const at::Tensor& like, hipStream_t st) {
+  static std::mutex mu;
+  static std::unordered_map<int, SlotPool> pools;
+  std::lock_guard<std::mutex> lk(mu);
+  n = (n + 63) / 64 * 64;  // 256-B aligned views
+  SlotPool& P = pools[like.get_device()];
+  const at::TensorOptions opts = like.options().dtype(at::kInt);
+  auto fresh = [&](long long size) {
+    at::Tensor b = at::empty({size}, opts);
+    TORCH_CHECK(hipMemsetAsync(b.data_ptr(), 0, (size_t)size * 4, st) == hipSuccess, "act max slots: memset failed");
+    slot_memsets().fetch_add(1, std::memory_order_relaxed);
+    return b;
+  };
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  unsigned long long id = 0;
+  TORCH_CHECK(hipStreamGetCaptureInfo(st, &cs, &id) == hipSuccess, "act max slots: capture query failed");
+  if (cs == hipStreamCaptureStatusActive) {
+    if (id != P.cap_id || !P.cap_cur.defined() || P.cap_used + n > P.cap_cur.numel()) {
+      P.cap_cur = fresh(std::max(kSlotChunk, n));
+      P.cap_keep.push_back(P.cap_cur);
+      P.cap_used = 0;
+      P.cap_id = id;
+    }
+    at::Tensor v = P.cap_cur.narrow(0, P.cap_used, n);
+    P.cap_used += n;
+    return v;
+  }
+  TORCH_CHECK(cs == hipStreamCaptureStatusNone, "act max slots: stream capture invalidated");
+  if (P.cur < 0 || P.used[P.cur] + n > P.ring[P.cur].numel()) {
+    int pick = -1;
+    for (size_t i = 0; i < P.ring.size(); ++i)
+      if ((int)i != P.cur && P.ring[i].storage().use_count() == 1 && P.ring[i].numel() >= n) {
+        pick = (int)i;
+        break;
+      }
+    if (pick < 0) {
+      P.ring.push_back(fresh(std::max(kSlotChunk, n)));
+      P.used.push_back(0);
+      pick = (int)P.ring.size() - 1;
+    } else {
+      TORCH_CHECK(hipMemsetAsync(P.ring[pick].data_ptr(), 0, (size_t)P.ring[pick].numel() * 4, st) == hipSuccess,
+                  "act max slots: memset failed");
+      slot_memsets().fetch_add(1, std::memory_order_relaxed);
+      P.used[pick] = 0;
+    }
+    P.cur = pick;
+  }
+  at::Tensor v = P.ring[P.cur].narrow(0, P.used[P.cur], n);
+  P.used[P.cur] += n;
+  return v;
+}
+
+// (images, channels, pixels per image) of an activation operand: NHWC 4-D or [rows, features] 2-D
+struct ActShape {
+  long long N, C, HW;
+};
+ActShape act_shape(const at::Tensor& t) {
+  TORCH_CHECK(t.dim() == 4 || t.dim() == 2, "act max: 4-D NHWC or 2-D tensors only");
+  const long long N = t.size(0), C = t.size(1);
+  return {N, C, N * C > 0 ? t.numel() / (N * C) : 0};
+}
+ActMaxOut act_out(const at::Tensor& s, long long N) {
+  unsigned* b = reinterpret_cast<unsigned*>(s.data_ptr<int>());
+  return ActMaxOut{b, b + N};
+}
+// Fresh zeroed act max slots for an activation of `like`'s images / channels (f16x2 engine only).
+at::Tensor new_act_max(long long N, long long C, const at::Tensor& like, hipStream_t st) {
+  return alloc_slots(act_max_elems(N, C), like, st);
+}
+
+// The act max of an f16x2 GEMM activation operand t (NHWC channels_last 4-D or contiguous 2-D):
+// its producer's when the caller has it, else a standalone pass. Undefined outside the f16x2 engine.
+at::Tensor act_max(const at::Tensor& t, const c10::optional<at::Tensor>& given, hipStream_t st) {
   if (!f16x2_mode()) return at::Tensor();
-  if (given.has_value() && given->defined()) return *given;
-  const long long n = t.numel();
-  const int nparts = (int)std::max<long long>(1, std::min<long long>(1024, (n + 8191) / 8192));
-  at::Tensor part = at::empty({nparts}, t.options().dtype(at::kFloat));
-  amax_launch(t.data_ptr<float>(), n, part.data_ptr<float>(), nparts, st);
-  return part;
+  const ActShape s = act_shape(t);
+  if (given.has_value() && given->defined()) {
+    TORCH_CHECK(given->scalar_type() == at::kInt && given->numel() >= act_max_elems(s.N, s.C),
+                "act max of a [", s.N, ", ", s.C, ", ...] operand must be int32 with >= ", act_max_elems(s.N, s.C),
+                " slots (per image, then ", kActCopies, " x per channel)");
+    return *given;
+  }
+  // per-image / per-channel maxima do not depend on the memory layout: measure a dense NHWC view
+  const at::Tensor u = t.dim() == 2 ? t.contiguous() : nhwc(t);
+  at::Tensor slots = new_act_max(s.N, s.C, u, st);
+  act_max_launch(u.data_ptr<float>(), (int)s.N, s.HW, (int)s.C, act_out(slots, s.N), st);
+  return slots;
 }
 }  // namespace
 
-// Partial |max| values of many tensors in one launch per 64 (a model's conv weights, once per
-// forward): returns one view of partials per tensor, or an empty list outside the f16x2 engine.
-std::vector<at::Tensor> multi_amax(const std::vector<at::Tensor>& ts) {
-  std::vector<at::Tensor> out;
-  if (!f16x2_mode() || ts.empty()) return out;
-  hipStream_t st = cur_stream();
-  for (size_t s0 = 0; s0 < ts.size(); s0 += kMaxAmaxSegs) {
-    const size_t ns = std::min<size_t>(kMaxAmaxSegs, ts.size() - s0);
-    MultiAmaxArgs a{};
-    a.nseg = (int)ns;
-    std::vector<at::Tensor> keep;
-    int tot = 0;
-    for (size_t i = 0; i < ns; ++i) {
-      at::Tensor t = ts[s0 + i];
-      check_f32_cuda(t, "multi_amax input");
-      if (!t.is_contiguous() && !t.is_contiguous(at::MemoryFormat::ChannelsLast)) t = t.contiguous();
-      keep.push_back(t);
-      a.ptr[i] = t.data_ptr<float>();
-      a.n[i] = t.numel();
-      a.blk0[i] = tot;
-      tot += (int)std::max<long long>(1, std::min<long long>(128, (t.numel() + 32767) / 32768));
-    }
-    a.blk0[ns] = tot;
-    at::Tensor part = at::empty({tot}, ts[s0].options());
-    multi_amax_launch(a, part.data_ptr<float>(), st);
-    for (size_t i = 0; i < ns; ++i) out.push_back(part.narrow(0, a.blk0[i], a.blk0[i + 1] - a.blk0[i]));
+std::vector<std::vector<at::Tensor>> weight_prep_impl(const std::vector<at::Tensor>& ts, const std::vector<bool>& want_t,
+                                                      const at::Tensor* amax_into,
+                                                      const std::vector<c10::optional<at::Tensor>>* wt_into);
+
+namespace {
+// A conv weight's maxima (weight_max_elems floats; 2-D [O, I] weights as [O, I, 1, 1]): given or
+// measured here (weight_prep without the transpose). Undefined outside the f16x2 engine.
+at::Tensor weight_max(const at::Tensor& w, const c10::optional<at::Tensor>& given) {
+  if (!f16x2_mode()) return at::Tensor();
+  const long long Co = w.size(0), Ci = w.size(1);
+  if (given.has_value() && given->defined()) {
+    TORCH_CHECK(given->scalar_type() == at::kFloat && given->numel() == weight_max_elems(Co, Ci),
+                "weight max of a [", Co, ", ", Ci, ", ...] weight must be ", weight_max_elems(Co, Ci), " floats");
+    return *given;
   }
-  return out;
+  const at::Tensor w4 = w.dim() == 2 ? w.reshape({Co, Ci, 1, 1}) : w;
+  return weight_prep_impl({w4}, {false}, nullptr, nullptr)[0][0];
+}
+}  // namespace
+
+int64_t act_max_memsets() { return slot_memsets().load(std::memory_order_relaxed); }
+int64_t act_max_copies() { return kActCopies; }
+
+// The act max of a tensor by the standalone pass (tests; the f16x2 engine only, else undefined).
+at::Tensor act_max_of(const at::Tensor& t) {
+  check_f32_cuda(t, "act_max input");
+  const at::Tensor u = t.dim() == 4 ? nhwc(t) : t.contiguous();
+  return act_max(u, c10::nullopt, cur_stream());
 }
 
-// Per-step preparation of a model's conv weights in one launch per 64 weights: {amax partials per
-// weight (f16x2 engine; empty list otherwise), W^T [Ci][KH*KW*Co] per weight with want_t[i]
-// (undefined tensor otherwise)}. The transposes are the data-gradient B operand, so backward no
-// longer transposes every weight in its own launch.
-// With `into` (amax partials + W^T tensors from sgd_prep_plan), the products are written into
-// those buffers instead of fresh ones (refreshing a fused-step plan after the weights were edited).
+// Per-step preparation of a model's conv weights in one launch per 64 weights: {maxima per weight
+// (f16x2 engine: weight_max_elems floats each, the per-co / per-ci |max| partials; empty list
+// otherwise), W^T [Ci][KH*KW*Co] per weight with want_t[i] (undefined tensor otherwise)}. The
+// transposes are the data-gradient B operand, so backward no longer transposes every weight in its
+// own launch.
+// With `into` (maxima + W^T tensors from sgd_prep_plan), the products are written into those
+// buffers instead of fresh ones (refreshing a fused-step plan after the weights were edited).
 std::vector<std::vector<at::Tensor>> weight_prep_impl(const std::vector<at::Tensor>& ts, const std::vector<bool>& want_t,
                                                       const at::Tensor* amax_into,
                                                       const std::vector<c10::optional<at::Tensor>>* wt_into) {
   TORCH_CHECK(ts.size() == want_t.size(), "weight_prep: one want_t flag per weight");
   std::vector<at::Tensor> amax, wts;
   hipStream_t st = cur_stream();
-  int into_off = 0;
+  long long into_off = 0;
   for (size_t s0 = 0; s0 < ts.size(); s0 += kMaxAmaxSegs) {
     const size_t ns = std::min<size_t>(kMaxAmaxSegs, ts.size() - s0);
     WeightPrepArgs a{};
     a.nseg = (int)ns;
     std::vector<at::Tensor> keep;
     int tot = 0;
+    long long ptot = 0;
     for (size_t i = 0; i < ns; ++i) {
       const at::Tensor& t0 = ts[s0 + i];
       check_f32_cuda(t0, "weight_prep input");
@@ -174,20 +278,25 @@ std::vector<std::vector<at::Tensor>> weight_prep_impl(const std::vector<at::Tens
       a.wt[i] = wt.defined() ? wt.data_ptr<float>() : nullptr;
       wts.push_back(wt);
       a.blk0[i] = tot;
+      a.pofs[i] = ptot;
       tot += ((Co + 31) / 32) * ((Ci + 31) / 32);
+      ptot += weight_max_elems(Co, Ci);
     }
     a.blk0[ns] = tot;
     at::Tensor part;
     if (amax_into) {
-      TORCH_CHECK(amax_into->numel() >= into_off + tot, "weight_prep_into: amax buffer too small");
-      part = amax_into->narrow(0, into_off, tot);
-      into_off += tot;
+      TORCH_CHECK(amax_into->numel() >= into_off + ptot, "weight_prep_into: maxima buffer too small");
+      part = amax_into->narrow(0, into_off, ptot);
+      into_off += ptot;
     } else {
-      part = at::empty({tot}, ts[s0].options());
+      part = at::empty({ptot}, ts[s0].options());
     }
     weight_prep_launch(a, part.data_ptr<float>(), st);
     if (f16x2_mode())
-      for (size_t i = 0; i < ns; ++i) amax.push_back(part.narrow(0, a.blk0[i], a.blk0[i + 1] - a.blk0[i]));
+      for (size_t i = 0; i < ns; ++i) {
+        const long long end = i + 1 < ns ? a.pofs[i + 1] : ptot;
+        amax.push_back(part.narrow(0, a.pofs[i], end - a.pofs[i]));
+      }
   }
   return {amax, wts};
 }
@@ -204,19 +313,33 @@ void weight_prep_into(const std::vector<at::Tensor>& ts, const std::vector<bool>
 
 namespace {
 
-void set_amax(ConvGemmParams& p, const at::Tensor& a, const at::Tensor& b) {
-  if (!a.defined() || !b.defined()) return;
-  p.amax_a = a.data_ptr<float>();
-  p.amax_na = (int)a.numel();
-  p.amax_b = b.data_ptr<float>();
-  p.amax_nb = (int)b.numel();
+// f16x2 operand scales of a conv GEMM (kernels.h): A rows by the gathered operand's images (act
+// max `a` of p.N images x p.C channels), B rows from the weight's maxima `wm` of a [Co, Ci, ...]
+// weight -- its per-co partials for the forward (B = W), its per-ci partials for the data gradient
+// (B = W^T).
+void set_scales(ConvGemmParams& p, const at::Tensor& a, const at::Tensor& wm, bool dgrad, long long Co, long long Ci) {
+  if (!a.defined() || !wm.defined()) return;
+  TORCH_CHECK(a.numel() >= act_max_elems(p.N, p.C), "conv GEMM: act max smaller than its operand's");
+  TORCH_CHECK(wm.numel() == weight_max_elems(Co, Ci), "conv GEMM: weight maxima of a different shape");
+  p.a_img = reinterpret_cast<const unsigned*>(a.data_ptr<int>());
+  const long long nco = (Co + 31) / 32, nci = (Ci + 31) / 32;
+  if (!dgrad) {
+    p.b_row = wm.data_ptr<float>();
+    p.b_np = (int)nci;
+    p.b_stride = (int)Co;
+  } else {
+    p.b_row = wm.data_ptr<float>() + nci * Co;
+    p.b_np = (int)nco;
+    p.b_stride = (int)Ci;
+  }
 }
-void set_amax(WgradParams& p, const at::Tensor& dy, const at::Tensor& x) {
+// weight gradient: dY's per-channel maxima scale the output rows (co), x's the columns (tap, ci)
+void set_scales(WgradParams& p, const at::Tensor& dy, const at::Tensor& x) {
   if (!dy.defined() || !x.defined()) return;
-  p.amax_dy = dy.data_ptr<float>();
-  p.amax_ndy = (int)dy.numel();
-  p.amax_x = x.data_ptr<float>();
-  p.amax_nx = (int)x.numel();
+  TORCH_CHECK(dy.numel() >= act_max_elems(p.N, p.Cout) && x.numel() >= act_max_elems(p.N, p.C),
+              "weight gradient: act max smaller than its operand's");
+  p.dy_ch = reinterpret_cast<const unsigned*>(dy.data_ptr<int>()) + p.N;
+  p.x_ch = reinterpret_cast<const unsigned*>(x.data_ptr<int>()) + p.N;
 }
 
 // The x3 kernels address through 32-bit buffer offsets and 24-bit index multiplies; shapes past
@@ -236,7 +359,7 @@ bool x3_ok(const WgradParams& p) {
 
 void conv_launch(const ConvGemmParams& p, int bm, int bn, bool dgrad, hipStream_t st) {
   if (x3_family() && x3_ok(p, dgrad)) {
-    TORCH_CHECK(!f16x2_mode() || (p.amax_a && p.amax_b), "f16x2 conv GEMM launched without operand maxima");
+    TORCH_CHECK(!f16x2_mode() || (p.a_img && p.b_row), "f16x2 conv GEMM launched without operand maxima");
     conv_x3_launch(p, bm, bn, dgrad, st, split_planes());
   }
   else conv_igemm_launch(p, bm, bn, dgrad, st);
@@ -317,7 +440,7 @@ std::atomic<long long>& pair_counter() {
 
 void conv_launch_or_pair(const ConvGemmParams& p, const GemmPlan& g, bool dgrad, hipStream_t st,
                          PendingWgrad* pending) {
-  if (pending && pending->set && dgrad && f16x2_mode() && x3_ok(p, true) && p.amax_a && p.amax_b &&
+  if (pending && pending->set && dgrad && f16x2_mode() && x3_ok(p, true) && p.a_img && p.b_row &&
       bwd_pair_ok(p, g.bm, g.bn, pending->p, pending->bm, pending->bn, split_planes())) {
     bwd_pair_launch(p, g.bm, g.bn, pending->p, pending->bm, pending->bn, st);
     pair_counter().fetch_add(1, std::memory_order_relaxed);
@@ -732,18 +855,18 @@ void set_divs(P& p) {
 
 // Zero-pad the channel dim of a channels_last 4-D tensor up to a multiple of 4 (RGB stems:
 // 3 -> 4) so the float4 gather paths apply. C < 4 is one kernel that can also emit the padded
-// tensor's |max| partials (f16x2 operand scale) into *amax.
+// tensor's act max (f16x2 operand scales) into *amax.
 at::Tensor pad_channels4(const at::Tensor& t, at::Tensor* amax = nullptr) {
   const int64_t C = t.size(1), C4 = (C + 3) / 4 * 4;
   at::Tensor o = at::empty({t.size(0), C4, t.size(2), t.size(3)}, t.options().memory_format(at::MemoryFormat::ChannelsLast));
   if (C < 4 && t.is_contiguous(at::MemoryFormat::ChannelsLast)) {
-    const long long npix = t.size(0) * t.size(2) * t.size(3);
-    float* ap = nullptr;
+    hipStream_t st = cur_stream();
+    ActMaxOut am{nullptr, nullptr};
     if (amax) {
-      *amax = at::empty({pad_c4_grid(npix)}, t.options());
-      ap = amax->data_ptr<float>();
+      *amax = new_act_max(t.size(0), 4, t, st);
+      am = act_out(*amax, t.size(0));
     }
-    pad_c4_launch(t.data_ptr<float>(), npix, (int)C, o.data_ptr<float>(), ap, cur_stream());
+    pad_c4_launch(t.data_ptr<float>(), (int)t.size(0), t.size(2) * t.size(3), (int)C, o.data_ptr<float>(), am, st);
     return o;
   }
   o.zero_();
@@ -819,8 +942,8 @@ std::vector<at::Tensor> conv2d_fwd(const at::Tensor& x_, const at::Tensor& w_, c
   set_divs(p);
   at::Tensor part, rpp;
   hipStream_t st = cur_stream();
-  const at::Tensor xa = amax_parts(x, x_amax, st), wa = amax_parts(w, w_amax, st);
-  set_amax(p, xa, wa);
+  const at::Tensor xa = act_max(x, x_amax, st), wa = weight_max(w, w_amax);
+  set_scales(p, xa, wa, false, Co, C);
   p.y = y.data_ptr<float>();
   p.bias = fptr(bias);
   // BN partials: one per BM-row tile (splits == 1) or per reduction row block (split-K)
@@ -869,7 +992,8 @@ bool conv2d_dgrad_subpixel(const at::Tensor& dy, const at::Tensor& w, at::Tensor
       set_divs(p);
       p.rr = RowRemap{1, H, W, ph, pw, Hc, Wc, make_fastdiv(Hc * Wc), make_fastdiv(Wc)};
       p.x = dy.data_ptr<float>();
-      set_amax(p, dya, wa);  // a sub-filter's |max| is bounded by the whole filter's
+      // rows (n, i, j) keep dY's image n; a sub-filter's per-ci |max| is bounded by the whole filter's
+      set_scales(p, dya, wa, true, Co, C);
       if (!x3_ok(p, true)) return false;
       at::Tensor wt;
       if (Kc > 0) {
@@ -912,7 +1036,7 @@ at::Tensor dgrad_impl(const at::Tensor& dy_, const at::Tensor& w_, std::vector<i
                     addend->size(0) == N && addend->size(1) == C && addend->size(2) == H && addend->size(3) == W,
                 "dgrad addend must be a channels_last fp32 tensor of the input's shape");
   const float* addp = has_add ? addend->data_ptr<float>() : nullptr;
-  const at::Tensor dya = amax_parts(dy, dy_amax, st), wa = amax_parts(w, w_amax, st);  // |max| W^T = |max| W
+  const at::Tensor dya = act_max(dy, dy_amax, st), wa = weight_max(w, w_amax);  // W^T rows: W's per-ci maxima
   if (stride == 2 && x3_family()) {
     at::Tensor dx = has_add ? *addend : at::empty({N, C, H, W}, opts.memory_format(at::MemoryFormat::ChannelsLast));
     if (conv2d_dgrad_subpixel(dy, w, dx, (int)pad, st, addp, dya, wa)) return dx;
@@ -937,7 +1061,7 @@ at::Tensor dgrad_impl(const at::Tensor& dy_, const at::Tensor& w_, std::vector<i
   p.KH = KH; p.KW = KW; p.stride = (int)stride; p.pad = (int)pad; p.pad_w = (int)pad;
   p.Nout = C; p.M = (int)M; p.Kdim = Kdim; p.ktiles = g.ktiles; p.splits = g.splits;
   set_divs(p);
-  set_amax(p, dya, wa);
+  set_scales(p, dya, wa, true, Co, C);
   p.y = dx.data_ptr<float>();
   p.addend = addp;
   std::vector<at::Tensor> keep;
@@ -995,10 +1119,10 @@ at::Tensor wgrad_impl(const at::Tensor& dy_, const at::Tensor& x_, std::vector<i
   const WgradPlan wp = plan_wgrad(Co, Kdim, M);
   p.splits = wp.splits;
   set_divs(p);
-  const at::Tensor dya = amax_parts(dy, dy_amax, st), xa = amax_parts(x, x_amax, st);
-  set_amax(p, dya, xa);
+  const at::Tensor dya = act_max(dy, dy_amax, st), xa = act_max(x, x_amax, st);
+  set_scales(p, dya, xa);
   // the GEMM launch, held back in `pending` when it can run beside the block's data gradient
-  const bool hold = pending && f16x2_mode() && x3_ok(p) && (C % 4) == 0 && (Co % 4) == 0 && p.amax_dy && p.amax_x;
+  const bool hold = pending && f16x2_mode() && x3_ok(p) && (C % 4) == 0 && (Co % 4) == 0 && p.dy_ch && p.x_ch;
   auto launch = [&](std::function<void()> after) {
     if (hold) {
       pending->set = true;
@@ -1081,17 +1205,19 @@ std::vector<at::Tensor> stem_bn_act_fwd(const at::Tensor& x_, const at::Tensor& 
                        stats.data_ptr<float>(), st);
   at::Tensor out = at::empty({N, Co, pool ? H / 2 : H, pool ? W / 2 : W},
                              opts.memory_format(at::MemoryFormat::ChannelsLast));
-  at::Tensor out_amax;
-  if (f16x2_mode())
-    out_amax = at::empty({fused ? bn_fin_act_grid(N, H, W, Co, pool, nparts) : bn_act_grid(N, H, W, Co, pool)}, opts);
-  float* amax_p = out_amax.defined() ? out_amax.data_ptr<float>() : nullptr;
+  at::Tensor out_amax;  // the output's act max: the next conv's operand scales (f16x2)
+  ActMaxOut am{nullptr, nullptr};
+  if (f16x2_mode()) {
+    out_amax = new_act_max(N, Co, out, st);
+    am = act_out(out_amax, N);
+  }
   if (fused)
     bn_fin_act_launch(part.data_ptr<float>(), nparts, 256, Co, fptr(gamma), fptr(beta), fptr_mut(running_mean),
                       fptr_mut(running_var), nbt, (float)momentum, (float)eps, stats.data_ptr<float>(),
-                      y.data_ptr<float>(), out.data_ptr<float>(), N, H, W, pool, relu, amax_p, st);
+                      y.data_ptr<float>(), out.data_ptr<float>(), N, H, W, pool, relu, am, st);
   else
     bn_act_fwd_launch(y.data_ptr<float>(), stats.data_ptr<float>(), nullptr, out.data_ptr<float>(), N, H, W, Co, pool,
-                      relu, st, amax_p);
+                      relu, st, am);
   return {out, y, stats, x, out_amax, at::Tensor(), at::Tensor()};
 }
 
@@ -1134,15 +1260,16 @@ std::vector<at::Tensor> conv_bn_act_fwd(const at::Tensor& x, const at::Tensor& w
   // other stems: zero-pad 3 -> 4 channels so the float4 gather path runs (the padded input is what
   // backward needs, so it is returned for saving)
   const bool padc = (x.size(1) % 4) != 0;
-  const bool have_xa = x_amax.has_value() && x_amax->defined();
   at::Tensor pad_amax;  // the padding pass measures x on the way (f16x2)
-  const at::Tensor xin = padc ? pad_channels4(nhwc(x), f16x2_mode() && !have_xa ? &pad_amax : nullptr) : x;
+  const at::Tensor xin = padc ? pad_channels4(nhwc(x), f16x2_mode() ? &pad_amax : nullptr) : x;
   const at::Tensor win = padc ? pad_channels4(nhwc(w)) : w;
   // f16x2 operand maxima: x's from its producer when given; W's once per step, reused by backward
-  // (zero channel padding does not change either)
-  const at::Tensor xa = amax_parts(xin, pad_amax.defined() ? c10::optional<at::Tensor>(pad_amax) : x_amax,
-                                   cur_stream());
-  const at::Tensor wa = amax_parts(win, w_amax, cur_stream());
+  // (zero channel padding does not change a maximum; a given x act max of the unpadded tensor is
+  // not used for the padded one, whose channel count differs)
+  const at::Tensor xa = act_max(xin, pad_amax.defined() ? c10::optional<at::Tensor>(pad_amax)
+                                     : padc ? c10::optional<at::Tensor>() : x_amax,
+                                cur_stream());
+  const at::Tensor wa = weight_max(win, padc ? c10::optional<at::Tensor>() : w_amax);
   std::vector<at::Tensor> r = conv2d_fwd(xin, win, b, stride, pad, training, xa, wa);
   at::Tensor y = r[0];
   const int N = y.size(0), C = y.size(1), H = y.size(2), W = y.size(3);
@@ -1179,24 +1306,25 @@ std::vector<at::Tensor> conv_bn_act_fwd(const at::Tensor& x, const at::Tensor& w
   }
   at::Tensor out = at::empty({N, C, pool ? H / 2 : H, pool ? W / 2 : W},
                              opts.memory_format(at::MemoryFormat::ChannelsLast));
-  at::Tensor out_amax;  // the output's |max| partials: the next conv's operand scale (f16x2)
-  if (f16x2_mode())
-    out_amax = at::empty({fused_fin ? bn_fin_act_grid(N, H, W, C, pool, nparts) : bn_act_grid(N, H, W, C, pool)},
-                         opts);
+  at::Tensor out_amax;  // the output's act max: the next conv's operand scales (f16x2)
+  ActMaxOut am{nullptr, nullptr};
+  if (f16x2_mode()) {
+    out_amax = new_act_max(N, C, out, st);
+    am = act_out(out_amax, N);
+  }
   if (fused_fin)
     bn_fin_act_launch(r[1].data_ptr<float>(), nparts, rpp, C, fptr(gamma), fptr(beta), fptr_mut(running_mean),
                       fptr_mut(running_var), nbt, (float)momentum, (float)eps, stats.data_ptr<float>(),
-                      y.data_ptr<float>(), out.data_ptr<float>(), N, H, W, pool, relu,
-                      out_amax.defined() ? out_amax.data_ptr<float>() : nullptr, st);
+                      y.data_ptr<float>(), out.data_ptr<float>(), N, H, W, pool, relu, am, st);
   else
     bn_act_fwd_launch(y.data_ptr<float>(), stats.data_ptr<float>(), res.defined() ? res.data_ptr<float>() : nullptr,
-                      out.data_ptr<float>(), N, H, W, C, pool, relu, st,
-                      out_amax.defined() ? out_amax.data_ptr<float>() : nullptr);
+                      out.data_ptr<float>(), N, H, W, C, pool, relu, st, am);
   return {out, y, stats, xin, out_amax, xa, wa};
 }
 
 // ---------------------------------------------------------------- fused block backward
-// Returns {dx (undefined when !need_dx), dw, db, dgamma, dbeta, dresidual (when zout given)}.
+// Returns {dx (undefined when !need_dx), dw, db, dgamma, dbeta, dresidual (when zout given),
+// prev_part, dy's act max (f16x2)}.
 std::vector<at::Tensor> conv_bn_act_bwd(const at::Tensor& gout_, const at::Tensor& x, const at::Tensor& w,
                                         const at::Tensor& y, const at::Tensor& stats, int64_t stride, int64_t pad,
                                         bool pool, bool relu, bool need_dx, bool has_bias,
@@ -1283,7 +1411,7 @@ std::vector<at::Tensor> conv_bn_act_bwd(const at::Tensor& gout_, const at::Tenso
                         : at::empty({C, cin, w.size(2), w.size(3)}, opts.memory_format(at::MemoryFormat::ChannelsLast));
     TORCH_CHECK(dw.is_contiguous(at::MemoryFormat::ChannelsLast), "stem dW slot must be channels_last");
     slab_sum_strided_launch(slab.data_ptr<float>(), nb, (long long)C * 36, 4, cin, dw.data_ptr<float>(), false, st);
-    return {at::Tensor(), dw, db, dgamma, dbeta, at::Tensor(), at::Tensor()};
+    return {at::Tensor(), dw, db, dgamma, dbeta, at::Tensor(), at::Tensor(), at::Tensor()};
   }
   at::Tensor dy = at::empty({N, C, H, W}, opts.memory_format(at::MemoryFormat::ChannelsLast));
   at::Tensor dbpart;
@@ -1291,19 +1419,22 @@ std::vector<at::Tensor> conv_bn_act_bwd(const at::Tensor& gout_, const at::Tenso
   if (sep_db) dbpart = at::empty({nblk, C, 2}, opts);
   at::Tensor dres;
   if (zout.defined()) dres = at::empty({N, C, H, W}, opts.memory_format(at::MemoryFormat::ChannelsLast));
-  at::Tensor dy_amax;  // dy's |max| partials: operand scale of both gradient GEMMs (f16x2)
-  if (f16x2_mode()) dy_amax = at::empty({fused_fin ? bn_fin_act_grid(N, H, W, C, pool) : nblk}, opts);
+  at::Tensor dy_amax;  // dy's act max: operand scales of both gradient GEMMs (f16x2)
+  ActMaxOut am{nullptr, nullptr};
+  if (f16x2_mode()) {
+    dy_amax = new_act_max(N, C, dy, st);
+    am = act_out(dy_amax, N);
+  }
   if (fused_fin)
     bn_bwd_fin_apply_launch(part.data_ptr<float>(), nparts, ps, y.data_ptr<float>(), gout.data_ptr<float>(),
                             stats.data_ptr<float>(), dy.data_ptr<float>(), dbeta.data_ptr<float>(),
                             dgamma.data_ptr<float>(), has_bias ? db.data_ptr<float>() : nullptr, N, H, W, C, pool,
-                            relu, dy_amax.defined() ? dy_amax.data_ptr<float>() : nullptr, st);
+                            relu, am, st);
   else
     bn_bwd_apply_launch(y.data_ptr<float>(), gout.data_ptr<float>(), stats.data_ptr<float>(),
                         sums.data_ptr<float>(), dy.data_ptr<float>(), sep_db ? dbpart.data_ptr<float>() : nullptr,
                         nblk, N, H, W, C, pool, relu, zout.defined() ? zout.data_ptr<float>() : nullptr,
-                        dres.defined() ? dres.data_ptr<float>() : nullptr, st,
-                        dy_amax.defined() ? dy_amax.data_ptr<float>() : nullptr);
+                        dres.defined() ? dres.data_ptr<float>() : nullptr, st, am);
   const c10::optional<at::Tensor> dya = dy_amax.defined() ? c10::optional<at::Tensor>(dy_amax) : c10::nullopt;
   if (sep_db)
     chan_finalize_launch(dbpart.data_ptr<float>(), nblk, C, nullptr, db.data_ptr<float>(), nullptr, false, st);
@@ -1377,7 +1508,7 @@ std::vector<at::Tensor> conv_bn_act_bwd(const at::Tensor& gout_, const at::Tenso
     }
     bwd_reduce_launch(a, st);
   }
-  return {dx, dw, db, dgamma, dbeta, dres, prev_part};
+  return {dx, dw, db, dgamma, dbeta, dres, prev_part, dy_amax};
 }
 
 // ---------------------------------------------------------------- linear
@@ -1402,7 +1533,7 @@ at::Tensor linear_fwd(const at::Tensor& x_, const at::Tensor& w_, const c10::opt
   p.Nout = O; p.M = B; p.Kdim = I; p.ktiles = g.ktiles; p.splits = g.splits;
   set_divs(p);
   hipStream_t st = cur_stream();
-  set_amax(p, amax_parts(x, c10::nullopt, st), amax_parts(w, c10::nullopt, st));
+  set_scales(p, act_max(x, c10::nullopt, st), weight_max(w, c10::nullopt), false, O, I);
   if (g.splits == 1) {
     p.y = y.data_ptr<float>();
     p.bias = fptr(b);
@@ -1451,7 +1582,7 @@ std::vector<at::Tensor> linear_bwd(const at::Tensor& gy_, const at::Tensor& x_, 
   const WgradPlan wp = plan_wgrad(O, I, B);
   p.splits = wp.splits;
   set_divs(p);
-  set_amax(p, amax_parts(gy, c10::nullopt, st), amax_parts(x, c10::nullopt, st));
+  set_scales(p, act_max(gy, c10::nullopt, st), act_max(x, c10::nullopt, st));
   if (p.splits == 1) {
     p.out = dw.data_ptr<float>();
     wgrad_launch(p, wp.bm, wp.bn, x3_family() && x3_ok(p), st, split_planes());
@@ -1521,9 +1652,9 @@ void sgd_step(at::Tensor p, const at::Tensor& g, c10::optional<at::Tensor> buf, 
 // Plan of the fused optimizer step over the flat range [s, e) of `flat` (an arena's parameter
 // storage): one segment per conv weight (a channels_last view inside the range), the W^T
 // destinations where want_t, and float4 chunks for everything else in the range. Returns
-// {descriptor (device bytes), meta (cpu int64: nseg, nblk_w, nchunk), amax partials (device; one per
-// 32x32 (co, ci) block, weight i's at [blk0_i, blk0_{i+1}) as weight_prep lays them out),
-// W^T per weight (undefined where not wanted)}. Built once per arena layout, outside any capture.
+// {descriptor (device bytes), meta (cpu int64: nseg, nblk_w, nchunk), weight maxima (device;
+// weight_max_elems floats per weight, back to back, as weight_prep lays them out), W^T per weight
+// (undefined where not wanted)}. Built once per arena layout, outside any capture.
 std::vector<at::Tensor> sgd_prep_plan(const at::Tensor& flat, int64_t s, int64_t e, const std::vector<at::Tensor>& ws,
                                       const std::vector<bool>& want_t) {
   check_f32_cuda(flat, "arena");
@@ -1534,6 +1665,7 @@ std::vector<at::Tensor> sgd_prep_plan(const at::Tensor& flat, int64_t s, int64_t
   std::vector<std::pair<long long, long long>> covered;
   std::vector<at::Tensor> outs;
   int blk = 0;
+  long long ptot = 0;
   for (size_t i = 0; i < ws.size(); ++i) {
     const at::Tensor& w = ws[i];
     check_f32_cuda(w, "sgd_prep weight");
@@ -1546,8 +1678,9 @@ std::vector<at::Tensor> sgd_prep_plan(const at::Tensor& flat, int64_t s, int64_t
     at::Tensor wt;
     if (want_t[i]) wt = at::empty({Ci, (long long)T * Co}, flat.options());
     outs.push_back(wt);
-    segs.push_back(SgdPrepSeg{off, wt.defined() ? wt.data_ptr<float>() : nullptr, Co, T, Ci, blk});
+    segs.push_back(SgdPrepSeg{off, wt.defined() ? wt.data_ptr<float>() : nullptr, Co, T, Ci, blk, ptot});
     blk += ((Co + 31) / 32) * ((Ci + 31) / 32);
+    ptot += weight_max_elems(Co, Ci);
     covered.push_back({off, off + (w.numel() + 3) / 4 * 4});
   }
   std::sort(covered.begin(), covered.end());
@@ -1571,7 +1704,7 @@ std::vector<at::Tensor> sgd_prep_plan(const at::Tensor& flat, int64_t s, int64_t
   if (!chunks.empty()) std::memcpy(host.data_ptr<uint8_t>() + seg_bytes, chunks.data(), bytes - seg_bytes);
   at::Tensor desc = host.to(flat.device());
   at::Tensor meta = at::tensor({(int64_t)segs.size(), (int64_t)blk, (int64_t)chunks.size()}, at::kLong);
-  at::Tensor amax = at::empty({std::max(blk, 1)}, flat.options());
+  at::Tensor amax = at::empty({std::max(ptot, 1LL)}, flat.options());
   std::vector<at::Tensor> r = {desc, meta, amax};
   for (auto& t : outs) r.push_back(t);
   return r;
@@ -1591,9 +1724,8 @@ void sgd_step_prep(at::Tensor p, const at::Tensor& g, c10::optional<at::Tensor> 
   TORCH_CHECK(meta.device().is_cpu() && meta.numel() == 3 && desc.is_cuda(), "sgd_step_prep: plan from sgd_prep_plan");
   const int64_t* mt = meta.data_ptr<int64_t>();
   const int nseg = (int)mt[0], nblk = (int)mt[1], nchunk = (int)mt[2];
-  TORCH_CHECK(desc.numel() >= (int64_t)(nseg * sizeof(SgdPrepSeg) + nchunk * sizeof(SgdPrepChunk)) &&
-                  amax.numel() >= nblk,
-              "sgd_step_prep: descriptor / amax smaller than the plan");
+  TORCH_CHECK(desc.numel() >= (int64_t)(nseg * sizeof(SgdPrepSeg) + nchunk * sizeof(SgdPrepChunk)),
+              "sgd_step_prep: descriptor smaller than the plan");
   const uint8_t* d = desc.data_ptr<uint8_t>();
   sgd_prep_launch(p.data_ptr<float>(), g.data_ptr<float>(), bp, reinterpret_cast<const SgdPrepSeg*>(d), nseg, nblk,
                   reinterpret_cast<const SgdPrepChunk*>(d + nseg * sizeof(SgdPrepSeg)), nchunk,

@@ -39,7 +39,9 @@ std::vector<at::Tensor> conv_bn_act_fwd(const at::Tensor& x, const at::Tensor& w
                                         const c10::optional<at::Tensor>& residual,
                                         const c10::optional<at::Tensor>& x_amax = c10::nullopt,
                                         const c10::optional<at::Tensor>& w_amax = c10::nullopt);
-std::vector<at::Tensor> multi_amax(const std::vector<at::Tensor>& ts);
+at::Tensor act_max_of(const at::Tensor& t);
+int64_t act_max_memsets();
+int64_t act_max_copies();
 std::vector<std::vector<at::Tensor>> weight_prep(const std::vector<at::Tensor>& ts, const std::vector<bool>& want_t);
 void weight_prep_into(const std::vector<at::Tensor>& ts, const std::vector<bool>& want_t, const at::Tensor& amax,
                       const std::vector<c10::optional<at::Tensor>>& wts);

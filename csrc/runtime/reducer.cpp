@@ -208,6 +208,22 @@ void Reducer::finalize() {
   std::lock_guard<std::mutex> g(mu_);
   if (!armed_) return;
   if (trace_) log_event("f", -1);
+  // Parameters whose hook never fired (e.g. reached from an output that stays out of the loss)
+  // are marked ready FIRST, so the launch loop below counts every bucket -- also in the deferred
+  // (calibration) iteration, where marking launches nothing by itself.
+  std::string missing;
+  for (size_t i = 0; i < params_.size(); ++i)
+    if (!ready_flag_[i]) {
+      if (find_unused_) mark_ready_locked(i, false);
+      else missing += std::to_string(i) + " ";
+    }
+  if (!missing.empty()) {
+    armed_ = false;
+    TORCH_CHECK(false,
+                "DistributedDataParallel: parameters with indices [ ", missing,
+                "] did not receive gradients in this iteration. Enable find_unused_parameters=True or make sure "
+                "all forward outputs participate in the loss.");
+  }
   if (defer_) {
     // the timed calibration backward: the bucket launches wait for the GPU to finish it. A
     // collective enqueued while the GPU still runs the backward (the host is ahead of it) was
@@ -217,22 +233,10 @@ void Reducer::finalize() {
     if (!bucket_views_.empty() && bucket_views_[0].is_cuda())
       TORCH_CHECK(hipStreamSynchronize(c10::hip::getCurrentHIPStream().stream()) == hipSuccess,
                   "reducer: stream synchronize failed");
-    while (next_launch_ < (int)pending_.size() && pending_[next_launch_] == 0) launch(next_launch_++);
   }
-  if (next_launch_ < (int)pending_.size()) {
-    if (find_unused_) {
-      for (size_t i = 0; i < params_.size(); ++i) mark_ready_locked(i, false);
-    } else {
-      std::string missing;
-      for (size_t i = 0; i < params_.size(); ++i)
-        if (!ready_flag_[i]) missing += std::to_string(i) + " ";
-      armed_ = false;
-      TORCH_CHECK(false,
-                  "DistributedDataParallel: parameters with indices [ ", missing,
-                  "] did not receive gradients in this iteration. Enable find_unused_parameters=True or make sure "
-                  "all forward outputs participate in the loss.");
-    }
-  }
+  while (next_launch_ < (int)pending_.size() && pending_[next_launch_] == 0) launch(next_launch_++);
+  TORCH_CHECK(next_launch_ == (int)pending_.size(), "reducer: ", (int)pending_.size() - next_launch_,
+              " bucket(s) left unlaunched at the end of backward");
   if (rccl_) {
     // all buckets run in order on the communicator stream: waiting on the last one covers them all
     if (!works_.empty() && works_.back()) works_.back()->wait();

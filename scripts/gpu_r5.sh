@@ -1,0 +1,11 @@
+#!/bin/bash
+# Round-5 GPU check: the whole GPU suite (all failures listed), a 1-GPU bench, the HW-queue diagnostic.
+set -o pipefail
+mkdir -p gpurun_out
+timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 200 --timeout-method thread > gpurun_out/gputest.log 2>&1
+rc=$?
+tail -15 gpurun_out/gputest.log | grep -E "passed|failed|FAILED|ERROR"
+if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "pytest rc=$rc (not a plain test failure): stopping"; exit $rc; fi
+timeout -k 10 300 python bench.py --steps 20 --warmup 5 > gpurun_out/b1.log 2>&1 || { echo "bench failed"; tail -30 gpurun_out/b1.log; exit 1; }
+tail -1 gpurun_out/b1.log
+if [ "$1" = "cq" ]; then bash scripts/diag/comm_queue.sh; fi

@@ -77,7 +77,7 @@ def main():
             w = cl(torch.randn(Co, Ci, 3, 3, device="cuda") * (1.0 / (Ci * 9) ** 0.5))
             gy = cl(torch.randn(B, Co, HW, HW, device="cuda"))
             b = torch.zeros(Co, device="cuda")
-            xa, wa, ga = C.multi_amax([x, w, gy])
+            xa, ga, wa = C.act_max(x), C.act_max(gy), C.weight_prep([w], [False])[0][0]
             wt = C.weight_prep([w], [True])[1][0]
             M = B * HW * HW
             for op in args.ops.split(","):

@@ -69,7 +69,7 @@ def main():
         P, Q = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
         gy = cl(torch.randn(B, Co, P, Q, device="cuda"))
         b = torch.zeros(Co, device="cuda")
-        xa, wa, ga = C.multi_amax([x, w, gy])
+        xa, ga, wa = C.act_max(x), C.act_max(gy), C.weight_prep([w], [False])[0][0]
         wt = C.weight_prep([w], [True])[1][0]
         M = B * P * Q
         ops = [("fwd", "conv", (M, Co, k * k * Ci), CONV_TILES,

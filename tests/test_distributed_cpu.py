@@ -4,6 +4,8 @@ The strategy-equivalence test is the SURVEY.md §4 oracle: with identical seeds,
 (gather/scatter), Part 2b (blocking all-reduce), the hook-bucketed reducer, our DDP wrapper and
 torch's own DDP all produce the same parameters after k SGD steps.
 """
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -115,6 +117,37 @@ def _reducer_unused(rank, world, find_unused):
     return err, float(net.module.a.weight.grad.abs().sum()) if net.module.a.weight.grad is not None else None
 
 
+def _unused_output_head(rank, world, py_reducer=False):
+    """find_unused_parameters with an output that stays out of the loss (its parameters are reached
+    from the outputs, so only the end-of-backward callback can mark them), in the first -- timed,
+    launch-deferred -- iteration of the default bucket planner."""
+    import copy
+
+    import cs744_distributed_data_parallel_amd as cdp
+
+    class Net(torch.nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.a = torch.nn.Linear(4, 4)
+            self.b = torch.nn.Linear(4, 4)
+
+        def forward(self, x):
+            return self.a(x), self.b(x)
+
+    if py_reducer:
+        os.environ["CDP_PY_REDUCER"] = "1"
+    torch.manual_seed(0)
+    module = Net()
+    ref = copy.deepcopy(module)
+    net = cdp.DistributedDataParallel(module, find_unused_parameters=True)
+    x = torch.randn(3, 4, generator=torch.Generator().manual_seed(100 + rank))
+    out_a, _ = net(x)
+    out_a.pow(2).sum().backward()
+    ref(x)[0].pow(2).sum().backward()
+    return (net.module.a.weight.grad.clone().numpy(), ref.a.weight.grad.clone().numpy(), net.reducer.iterations,
+            net.reducer.native)
+
+
 def _no_sync(rank, world):
     import cs744_distributed_data_parallel_amd as cdp
 
@@ -210,6 +243,21 @@ def test_unused_parameters_error_and_find_unused():
     assert errs[0][0] is not None and "did not receive gradients" in errs[0][0]
     ok = run_ranks(_reducer_unused, 2, (True,))
     assert ok[0][0] is None and ok[0][1] > 0
+
+
+@pytest.mark.parametrize("py_reducer", [False, True])
+def test_find_unused_with_an_output_left_out_of_the_loss(py_reducer):
+    """Every bucket is all-reduced when an output's parameters get no gradient: the
+    synced gradient equals the mean of the ranks' local gradients on both ranks, with the C++
+    reducer and with its Python twin."""
+    import cs744_distributed_data_parallel_amd as cdp
+
+    (g0, l0, it0, nat), (g1, l1, it1, _) = run_ranks(_unused_output_head, 2, (py_reducer,))
+    assert nat == (cdp.native_available() and not py_reducer)
+    assert not np.allclose(l0, l1)
+    np.testing.assert_allclose(g0, g1, rtol=0, atol=1e-7)
+    np.testing.assert_allclose(g0, (l0 + l1) / 2, rtol=1e-6, atol=1e-7)
+    assert it0 == it1 == 1
 
 
 def test_no_sync_accumulates_locally():

@@ -481,8 +481,8 @@ def test_split_k_conv_is_deterministic_and_exact_order(N, Ci, H, W, Co, k, s, p)
 
 
 def test_weight_prep_transposes_and_maxima():
-    """One launch for all conv weights: W^T [Ci, KH*KW*Co] where asked, and the |max| partials
-    (f16x2) whose max is each weight's |max|; dgrad with the prepared W^T equals dgrad without."""
+    """One launch for all conv weights: W^T [Ci, KH*KW*Co] where asked, and (f16x2) the per-output-
+    and per-input-channel |max| partials; dgrad with the prepared W^T equals dgrad without."""
     torch.manual_seed(4)
     ws = [cl(torch.randn(co, ci, k, k, device="cuda")) for co, ci, k in
           [(64, 3, 3), (128, 64, 3), (512, 512, 3), (256, 64, 1), (10, 7, 3), (64, 3, 7), (40, 36, 5)]]
@@ -495,9 +495,18 @@ def test_weight_prep_transposes_and_maxima():
         ref = w.permute(1, 2, 3, 0).reshape(ci, kh * kw * co)  # [ci][kh][kw][co]
         assert torch.equal(wt, ref)
     if C().get_conv_gemm() == "f16x2":
+        # per weight: the per-co partials of every 32-wide ci block, then the per-ci partials of
+        # every 32-wide co block (csrc weight_max_elems), exact
         assert len(amax) == len(ws)
         for w, a in zip(ws, amax):
-            assert a.max().item() == w.abs().max().item()
+            co, ci = w.shape[:2]
+            nci, nco = (ci + 31) // 32, (co + 31) // 32
+            wa = w.abs()
+            ref_co = torch.stack([wa[:, 32 * j:32 * (j + 1)].amax(dim=(1, 2, 3)) for j in range(nci)])
+            ref_ci = torch.stack([wa[32 * j:32 * (j + 1)].amax(dim=(0, 2, 3)) for j in range(nco)])
+            assert a.numel() == nci * co + nco * ci
+            assert torch.equal(a[:nci * co].view(nci, co), ref_co)
+            assert torch.equal(a[nci * co:].view(nco, ci), ref_ci)
     x = torch.randn(2, 128, 8, 8, device="cuda")
     gy = torch.randn(2, 512, 8, 8, device="cuda")
     w = ws[2]
