@@ -338,6 +338,18 @@ def test_bench_self_launches_ranks_cpu():
         assert b["planner"] == "timed" and b["backward_end_us"] > 0 and b["alpha_us"] >= 0
     assert set(rec["scaling_eff"]) == {"weak", "strong"}
     assert rec["scaling_eff"]["strong"] == blk["ddp"]["scaling_eff"]
+    # BASELINE.json config #5 at N > 1: ResNet-50 under DDP with the timed bucket plan (reduced
+    # 32x32 images in CPU mode)
+    rn = rec["resnet50"]
+    for k in ("ms_per_step", "ms_per_step_no_sync", "exposed_comm_ms", "scaling_eff", "value", "buckets",
+              "replicas_identical", "local_batch", "global_batch"):
+        assert k in rn, k
+    assert rn["replicas_identical"] is True and rn["strategy"] == "ddp" and rn["global_batch"] == 2 * rn["local_batch"]
+    assert 0 < rn["scaling_eff"] <= 1.0 and rn["exposed_comm_ms"] >= 0
+    rb = rn["buckets"]
+    assert rb["params"] == 161 and rb["count"] == len(rb["launch_order"]) >= 1
+    assert sum(x["bytes"] for x in rb["launch_order"]) == 25_557_032 * 4  # every ResNet-50 gradient
+    assert rb["planner"] == "timed"
 
 
 def test_bench_launcher_at_eight_ranks_cpu():
