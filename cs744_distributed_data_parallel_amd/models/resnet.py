@@ -17,6 +17,7 @@ import torch
 import torch.nn as nn
 
 from ..ops import functional as CF
+from ..utils.arena import install_load_hooks
 
 
 class BasicBlock(nn.Module):
@@ -83,6 +84,7 @@ class Bottleneck(nn.Module):
 class ResNet(nn.Module):
     def __init__(self, block, layers, num_classes=1000, channels_last=True):
         super().__init__()
+        install_load_hooks(self)  # loaded weights refresh the optimizer's prepared products
         self.inplanes = 64
         self.conv1 = nn.Conv2d(3, 64, 7, 2, 3, bias=False)
         self.bn1 = nn.BatchNorm2d(64)

@@ -22,6 +22,7 @@ import torch
 import torch.nn as nn
 
 from ..ops import functional as CF
+from ..utils.arena import install_load_hooks
 
 cfg = {
     "VGG11": [64, "M", 128, "M", 256, 256, "M", 512, 512, "M", 512, 512, "M"],
@@ -51,6 +52,7 @@ class VGG(nn.Module):
 
     def __init__(self, name: str = "VGG11", num_classes: int = 10, channels_last: bool = True):
         super().__init__()
+        install_load_hooks(self)  # loaded weights refresh the optimizer's prepared products
         self.name = name
         self.layers = make_layers(cfg[name])
         flatten_features = 512

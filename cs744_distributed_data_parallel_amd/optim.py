@@ -70,6 +70,26 @@ class SGD(Optimizer):
             if st and st.get("momentum_buffer") is not None:
                 st["momentum_buffer"] = views[p._cdp_index]
 
+    def load_state_dict(self, state_dict):
+        super().load_state_dict(state_dict)
+        self._adopt_momentum()
+
+    def _adopt_momentum(self):
+        """Loaded momentum buffers are fresh tensors, while a replayed hipGraph step reads and writes
+        the arena's momentum storage: copy them into their arena views now (not at the next eager
+        step), so a replay after ``load_state_dict`` continues from the loaded state."""
+        a = self._arena
+        if a is None or a.momentum is None:
+            return
+        views = a.momentum_views()
+        with torch.no_grad():
+            for p in a.params:
+                st = self.state.get(p)
+                b = st.get("momentum_buffer") if st else None
+                if b is not None and b.data_ptr() != views[p._cdp_index].data_ptr():
+                    views[p._cdp_index].copy_(b)
+                    st["momentum_buffer"] = views[p._cdp_index]
+
     # ------------------------------------------------------------------ fused weight preparation
     def refresh_weight_prep(self) -> bool:
         """Re-derive the next forward's weight |max| / W^T from the current weights (in place).

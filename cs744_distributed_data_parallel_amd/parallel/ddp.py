@@ -23,7 +23,7 @@ from typing import Optional
 import torch
 import torch.nn as nn
 
-from ..utils.arena import BufferArena, arena_for
+from ..utils.arena import BufferArena, arena_for, install_load_hooks
 from .buckets import DEFAULT_BUCKET_CAP_MB, DEFAULT_FIRST_BUCKET_CAP_MB
 from .comm import Communicator
 from .reducer import GradReducer
@@ -61,6 +61,7 @@ class DistributedDataParallel(nn.Module):
     ):
         super().__init__()
         self.module = module
+        install_load_hooks(module)  # loaded weights refresh the optimizer's prepared products
         self.device_ids = device_ids
         self.broadcast_buffers = broadcast_buffers
         self.find_unused_parameters = find_unused_parameters

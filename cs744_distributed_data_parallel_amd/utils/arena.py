@@ -36,6 +36,28 @@ def act_max_elems(n: int, c: int, copies: int = 8) -> int:
     return n + copies * c
 
 
+def refresh_prep_after_load(module, incompatible_keys=None):
+    """``load_state_dict`` post-hook: the weights were written in place, which a replayed hipGraph step
+    cannot notice (it reads the W^T / f16x2 maxima its previous replay's fused optimizer step wrote).
+    Re-derive those products from the loaded weights now (FlatArena.prep_refresh), or drop them when
+    no fused plan exists yet, so the next replay -- or eager forward -- uses the loaded weights."""
+    seen = set()
+    for p in module.parameters():
+        a = getattr(p, "_cdp_arena", None)
+        if a is None or id(a) in seen:
+            continue
+        seen.add(id(a))
+        if not a.prep_refresh():
+            a.prep_valid = None
+
+
+def install_load_hooks(module) -> None:
+    """Register :func:`refresh_prep_after_load` on ``module`` once (models and the DDP wrapper)."""
+    if not getattr(module, "_cdp_load_hook", False):
+        module.register_load_state_dict_post_hook(refresh_prep_after_load)
+        module._cdp_load_hook = True
+
+
 def _dense(t: torch.Tensor) -> bool:
     return t.is_contiguous() or (t.dim() == 4 and t.is_contiguous(memory_format=torch.channels_last))
 

@@ -168,6 +168,57 @@ def test_captured_step_sees_weights_edited_between_replays_after_refresh():
         assert torch.equal(a, b.detach())
 
 
+@pytest.mark.parametrize("what", ["model", "model+optimizer"])
+def test_captured_step_after_load_state_dict_matches_eager(what):
+    """No manual refresh: ``model.load_state_dict`` (its post-hook re-derives the fused-step products
+    from the loaded weights) and ``opt.load_state_dict`` (the loaded momentum moves into the arena
+    the graph reads) between replays of a captured step, and the next replay equals an eager step
+    of a fresh model + optimizer loaded from the same state."""
+    cdp, model, opt = _setup()
+    crit = cdp.CrossEntropyLoss()
+    x, y = _batch(0)
+
+    def body():
+        opt.zero_grad()
+        crit(model(x), y).backward()
+        opt.step()
+
+    for _ in range(3):
+        body()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        body()
+    torch.cuda.current_stream().wait_stream(s)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        body()
+    torch.cuda.synchronize()
+    sd = {k: v.clone() for k, v in model.state_dict().items()}
+    for k in ("layers.8.weight", "layers.11.weight", "layers.25.weight"):
+        sd[k] = sd[k] * 0.5
+    osd = opt.state_dict()
+    if what == "model+optimizer":
+        for st in osd["state"].values():
+            st["momentum_buffer"] = st["momentum_buffer"] * 0.25
+    model.load_state_dict(sd)
+    if what == "model+optimizer":
+        opt.load_state_dict(osd)
+    g.replay()
+    torch.cuda.synchronize()
+    got = [p.detach().clone() for p in model.parameters()]
+    _, ref, ropt = _setup()
+    ref.load_state_dict(sd)
+    ropt.load_state_dict(osd)
+    ropt.fused_prep = False
+    ropt.zero_grad()
+    crit(ref(x), y).backward()
+    ropt.step()
+    torch.cuda.synchronize()
+    for a, b in zip(got, ref.parameters()):
+        assert torch.equal(a, b.detach())
+
+
 def test_loader_counter_advanced_by_the_optimizer_step():
     """DeviceLoader.advance_with(opt): the SGD kernel advances the loader's step counter (no
     counter_inc launch); the batch sequence and the trained parameters are those of the default
