@@ -181,12 +181,40 @@ class DeviceLoader:
     def advance_with(self, optimizer) -> bool:
         """Let ``optimizer`` advance this loader's step counter inside its step kernel (cdp.SGD
         ``advance_each_step``) instead of a one-thread launch per batch. One batch per optimizer
-        step only; GPU datasets only (returns False otherwise)."""
+        step only; GPU datasets only (returns False otherwise). ``advance_with(None)`` detaches it
+        again (e.g. before gradient accumulation or an evaluation pass over the same loader): the
+        loader then advances its counter at every batch itself. An eager batch() fetched twice
+        without an optimizer step in between warns once (both batches would share a seed)."""
+        prev = getattr(self, "_advancer", None)
+        if optimizer is None:
+            if prev is not None and getattr(prev, "_step_counter", None) is self._counter:
+                prev.advance_each_step(None)
+            self._advancer = None
+            self._external_advance = False
+            return True
         if self.dev.type != "cuda" or not hasattr(optimizer, "advance_each_step"):
             return False
+        if prev is not None and prev is not optimizer:
+            self.advance_with(None)
         optimizer.advance_each_step(self._counter)
+        self._advancer = optimizer
+        self._advance_seen = None
         self._external_advance = True
         return True
+
+    def _check_one_batch_per_step(self):
+        opt = getattr(self, "_advancer", None)
+        if opt is None or torch.cuda.is_current_stream_capturing():
+            return
+        steps = getattr(opt, "_steps", None)
+        if steps is not None and steps == self._advance_seen and not getattr(self, "_warned_reuse", False):
+            import warnings
+
+            warnings.warn("DeviceLoader: two batches without an optimizer step while the optimizer advances the "
+                          "loader's step counter (advance_with): they share an augmentation seed and batch offset; "
+                          "call advance_with(None) for gradient accumulation or evaluation", stacklevel=3)
+            self._warned_reuse = True
+        self._advance_seen = steps
 
     @property
     def dataset(self):
@@ -212,6 +240,8 @@ class DeviceLoader:
                              self.seed, out, nbatches, self.ds.labels, target)
             if not self._external_advance:
                 C.counter_inc(self._counter)
+            else:
+                self._check_one_batch_per_step()
             return data, target
         if nbatches > 0:
             offset += (int(self._counter.item()) % nbatches) * bsz

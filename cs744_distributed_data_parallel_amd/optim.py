@@ -150,7 +150,7 @@ class SGD(Optimizer):
     def advance_each_step(self, counter: torch.Tensor):
         """Advance ``counter`` (a device int64 step counter, e.g. a DeviceLoader's) by one in every
         ``step()``, inside the SGD kernel itself: one dispatch less per training step. Only for
-        loops that fetch exactly one batch per optimizer step."""
+        loops that fetch exactly one batch per optimizer step; ``None`` stops it."""
         self._step_counter = counter
 
     def _first_flags(self, params):

@@ -269,3 +269,24 @@ def test_loader_counter_advanced_by_the_optimizer_step():
             assert torch.equal(a, b)
         for a, b in zip(p_ext, p_def):
             assert torch.equal(a, b)
+
+
+def test_loader_advance_with_detaches_and_warns_on_reuse():
+    """advance_with(None) hands the step counter back to the loader: batches then
+    advance it themselves; a second eager batch without an optimizer step in between warns."""
+    import cs744_distributed_data_parallel_amd as cdp
+    from cs744_distributed_data_parallel_amd.data import DeviceLoader, synthetic_cifar10
+
+    model = cdp.VGG11().cuda()
+    opt = cdp.SGD(model.parameters(), lr=0.1, momentum=0.9)
+    loader = DeviceLoader(synthetic_cifar10(256, seed=0, device=torch.device("cuda")), 32, shuffle=True)
+    order = loader._order()
+    assert loader.advance_with(opt)
+    loader.batch(order, 0, 32, nbatches=8)
+    with pytest.warns(UserWarning, match="two batches without an optimizer step"):
+        loader.batch(order, 0, 32, nbatches=8)
+    c0 = int(loader._counter.item())
+    assert loader.advance_with(None) and opt._step_counter is None
+    loader.batch(order, 0, 32, nbatches=8)
+    loader.batch(order, 0, 32, nbatches=8)
+    assert int(loader._counter.item()) == c0 + 2
