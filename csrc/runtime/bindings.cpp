@@ -128,6 +128,7 @@ PYBIND11_MODULE(_C, m) {
       .def_property_readonly("size", &RcclComm::size)
       .def_property_readonly("device", &RcclComm::device)
       .def_property_readonly("stream_ptr", [](RcclComm& c) { return reinterpret_cast<intptr_t>(c.stream()); })
+      .def_property_readonly("stream_kind", &RcclComm::stream_kind)
       .def("count", &RcclComm::count)
       .def("healthy", &RcclComm::healthy)
       .def("error", &RcclComm::error)

@@ -1231,6 +1231,13 @@ std::vector<at::Tensor> stem_bn_act_fwd(const at::Tensor& x_, const at::Tensor& 
 // 1.399 vs 1.407 ms at 256 images per GPU (fused 0.6 % faster, two boxes agree); backward 1.409 vs
 // 1.404 ms at 256 images (within noise) and 0.632 vs 0.641 ms at 32 images (1.3 % faster, where
 // every deep layer qualifies). Read per call so a test can compare both paths in one process.
+// CDP_EXP_SKIP_BN_APPLY=1: TIMING EXPERIMENT ONLY, numerically wrong -- the fused finalize + apply
+// launches of the small layers are skipped (their outputs stay uninitialised), which bounds what
+// moving BatchNorm into the consumer GEMMs could save (docs/PERF.md, round 5)
+static bool exp_skip_bn_apply() {
+  const char* e = std::getenv("CDP_EXP_SKIP_BN_APPLY");
+  return e && e[0] == '1';
+}
 static bool bn_fin_enabled(bool bwd = false) {
   const char* e = std::getenv(bwd ? "CDP_BN_BWD_FIN" : "CDP_BN_FIN_ACT");
   return !(e && e[0] == '0');
@@ -1312,7 +1319,10 @@ std::vector<at::Tensor> conv_bn_act_fwd(const at::Tensor& x, const at::Tensor& w
     out_amax = new_act_max(N, C, out, st);
     am = act_out(out_amax, N);
   }
-  if (fused_fin)
+  if (fused_fin && exp_skip_bn_apply()) {
+    // timing experiment only (wrong numbers): no finalize + apply launch at all -- the ceiling of
+    // what applying BatchNorm in the consumer GEMM's operand load could save
+  } else if (fused_fin)
     bn_fin_act_launch(r[1].data_ptr<float>(), nparts, rpp, C, fptr(gamma), fptr(beta), fptr_mut(running_mean),
                       fptr_mut(running_var), nbt, (float)momentum, (float)eps, stats.data_ptr<float>(),
                       y.data_ptr<float>(), out.data_ptr<float>(), N, H, W, pool, relu, am, st);
@@ -1425,7 +1435,9 @@ std::vector<at::Tensor> conv_bn_act_bwd(const at::Tensor& gout_, const at::Tenso
     dy_amax = new_act_max(N, C, dy, st);
     am = act_out(dy_amax, N);
   }
-  if (fused_fin)
+  if (fused_fin && exp_skip_bn_apply()) {
+    // timing experiment only (wrong numbers), as in conv_bn_act_fwd
+  } else if (fused_fin)
     bn_bwd_fin_apply_launch(part.data_ptr<float>(), nparts, ps, y.data_ptr<float>(), gout.data_ptr<float>(),
                             stats.data_ptr<float>(), dy.data_ptr<float>(), dbeta.data_ptr<float>(),
                             dgamma.data_ptr<float>(), has_bias ? db.data_ptr<float>() : nullptr, N, H, W, C, pool,

@@ -107,7 +107,25 @@ RcclComm::RcclComm(const std::string& uid, int rank, int world, int device, doub
   // backward took 1.3-4.0 ms instead of 0.36-0.42 ms (compute dispatches ~57 us apart); on a pool
   // stream it took 0.40-0.42 ms, and a 300 us kernel per collective on the comm stream still fully
   // overlapped it. A high-priority stream holding work throttled compute as well (0.45 -> 2-3 ms).
-  stream_ = c10::hip::getStreamFromPool(/*isHighPriority=*/false, (c10::DeviceIndex)device).stream();
+  // CDP_COMM_STREAM selects the stream for A/B runs (scripts/diag/comm_queue.py): "pool" (default),
+  // "own" (non-blocking, normal priority, created here), "low" (non-blocking, the device's least
+  // priority), "cumask" (every CU, on a hardware queue of its own).
+  const char* kind = std::getenv("CDP_COMM_STREAM");
+  stream_kind_ = kind && *kind ? kind : "pool";
+  if (stream_kind_ == "own" || stream_kind_ == "low") {
+    int lo = 0, hi = 0;
+    HIP_CHECK(hipDeviceGetStreamPriorityRange(&lo, &hi));
+    HIP_CHECK(hipStreamCreateWithPriority(&stream_, hipStreamNonBlocking, stream_kind_ == "low" ? lo : 0));
+    own_stream_ = true;
+  } else if (stream_kind_ == "cumask") {
+    uint32_t mask[8];
+    for (auto& w : mask) w = 0xffffffffu;
+    HIP_CHECK(hipExtStreamCreateWithCUMask(&stream_, 8, mask));
+    own_stream_ = true;
+  } else {
+    TORCH_CHECK(stream_kind_ == "pool", "CDP_COMM_STREAM must be pool, own, low or cumask");
+    stream_ = c10::hip::getStreamFromPool(/*isHighPriority=*/false, (c10::DeviceIndex)device).stream();
+  }
   HIP_CHECK(hipEventCreateWithFlags(&start_ev_, hipEventDisableTiming));
   ncclComm_t c = nullptr;
   RCCL_CHECK(ncclCommInitRank(&c, world, id, rank));
@@ -139,7 +157,8 @@ RcclComm::~RcclComm() {
     for (auto e : free_events_) hipEventDestroy(e);
     free_events_.clear();
   }
-  if (start_ev_) hipEventDestroy(start_ev_);  // stream_ belongs to PyTorch's pool
+  if (start_ev_) hipEventDestroy(start_ev_);
+  if (own_stream_ && stream_) hipStreamDestroy(stream_);  // (a pool stream belongs to PyTorch)
 }
 
 std::string RcclComm::error() const {
@@ -189,6 +208,11 @@ hipStream_t RcclComm::begin() {
   check();
   TORCH_CHECK(comm_ != nullptr, "RCCL communicator is shut down");
   hipStream_t cur = c10::hip::getCurrentHIPStream().stream();
+  // the caller's work must not BE the comm stream (e.g. a PyTorch pool stream handed out again by
+  // torch.cuda.Stream()): the wait below would then order it behind itself, and unrelated work
+  // would queue behind the collectives
+  TORCH_CHECK(cur != stream_, "RCCL communicator: the current stream is the communicator's own stream (",
+              stream_kind_, "); run compute on another stream");
   HIP_CHECK(hipEventRecord(start_ev_, cur));
   HIP_CHECK(hipStreamWaitEvent(stream_, start_ev_, 0));
   return cur;

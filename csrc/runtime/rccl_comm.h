@@ -57,6 +57,7 @@ class RcclComm : public std::enable_shared_from_this<RcclComm> {
   int device() const { return device_; }
   int count();  // ranks in the communicator as RCCL sees them (ncclCommCount)
   hipStream_t stream() const { return stream_; }
+  const std::string& stream_kind() const { return stream_kind_; }
   bool healthy() const { return !failed_.load(); }
   std::string error() const;
   void abort(const std::string& why);
@@ -104,6 +105,8 @@ class RcclComm : public std::enable_shared_from_this<RcclComm> {
   double postop_delay_us_ = 0.0, postop_scale_ = 1.0;
   int rank_, world_, device_;
   hipStream_t stream_ = nullptr;
+  bool own_stream_ = false;  // created here (destroyed with the communicator), not PyTorch's pool
+  std::string stream_kind_;
   hipEvent_t start_ev_ = nullptr;
   std::mutex mu_;
   std::mutex ev_mu_;
