@@ -6,7 +6,7 @@
 set -o pipefail
 mkdir -p gpurun_out/abcs
 for rep in 1 2; do
-  for k in pool own low cumask; do
+  for k in pool own low; do
     CDP_COMM_STREAM=$k timeout -k 10 120 python3 scripts/diag/ddp_slowdown.py ddp > gpurun_out/abcs/eager_$k.$rep.log 2>&1 || { echo "$k eager failed"; tail -5 gpurun_out/abcs/eager_$k.$rep.log; exit 1; }
     echo "$k eager: $(grep -m3 'iter' gpurun_out/abcs/eager_$k.$rep.log | tail -1)"
     CDP_COMM_STREAM=$k CDP_BENCH_DDP_W1=1 CDP_REDUCER_TEST_POSTOP=0:1 timeout -k 10 180 python3 bench.py --local-batch 32 --steps 50 --warmup 5 --no-extra > gpurun_out/abcs/graph_$k.$rep.log 2>&1 || { echo "$k graph failed"; tail -5 gpurun_out/abcs/graph_$k.$rep.log; exit 1; }

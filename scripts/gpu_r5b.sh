@@ -9,5 +9,4 @@ if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "pytest rc=$rc (not a plain test fa
 timeout -k 10 300 python bench.py --steps 20 --warmup 5 > gpurun_out/b1.log 2>&1 || { echo "bench failed"; tail -30 gpurun_out/b1.log; exit 1; }
 tail -1 gpurun_out/b1.log
 timeout -k 10 120 python scripts/diag/resnet_copies.py > gpurun_out/rn_copies.md 2>&1 || { echo "resnet copies failed"; tail -20 gpurun_out/rn_copies.md; exit 1; }
-bash scripts/diag/comm_queue.sh && bash scripts/diag/ab_comm_stream.sh
-bash scripts/diag/ab_skip_bn.sh
+bash scripts/diag/comm_queue.sh
