@@ -620,7 +620,7 @@ def rank_main(args) -> int:
         }
         rec.update(extra)
         print(json.dumps(rec), flush=True)
-    if world > 1:
+    if dist.is_initialized():
         dist.destroy_process_group()
     faulthandler.cancel_dump_traceback_later()
     if replicas_identical is False:

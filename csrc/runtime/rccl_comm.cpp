@@ -100,18 +100,18 @@ RcclComm::RcclComm(const std::string& uid, int rank, int world, int device, doub
   ncclUniqueId id;
   std::memcpy(&id, uid.data(), sizeof(id));
   HIP_CHECK(hipSetDevice(device));
-  // The comm stream is one of PyTorch's low-priority pool streams, not a stream created here.
-  // Measured on MI355X (VGG-11 eager backward at 32 images, a collective per ~8 gradients at one
-  // rank, scripts/diag/queue_prio.py + comm_diag runs): with a stream of our own -- created with
-  // hipStreamCreateWithPriority before or after RCCL init, or as a full-CU-mask stream -- the
-  // backward took 1.3-4.0 ms instead of 0.36-0.42 ms (compute dispatches ~57 us apart); on a pool
-  // stream it took 0.40-0.42 ms, and a 300 us kernel per collective on the comm stream still fully
-  // overlapped it. A high-priority stream holding work throttled compute as well (0.45 -> 2-3 ms).
-  // CDP_COMM_STREAM selects the stream for A/B runs (scripts/diag/comm_queue.py): "pool" (default),
-  // "own" (non-blocking, normal priority, created here), "low" (non-blocking, the device's least
-  // priority), "cumask" (every CU, on a hardware queue of its own).
+  // The comm stream is the communicator's own non-blocking stream at NORMAL priority (0): private
+  // (PyTorch's pool never hands it to anyone else, unlike a pool stream, which torch.cuda.Stream()
+  // returns again after 32 calls) and placed the same way every time. Measured on MI355X
+  // (profiles/comm_stream_priority_r5.md, VGG-11 at 32 images, one rank):
+  //  * eager DDP backward span: own normal-priority stream 414-422 us, PyTorch pool stream 420-441,
+  //    a stream at the device's LEAST priority (+1 on ROCm) 2173-2392 us with compute dispatches
+  //    40-57 us apart -- the round-4 slowdown: its "own" stream was created at that least priority;
+  //  * captured DDP step (RCCL kernel + post-op per bucket): 0.552-0.555 / 0.559-0.565 / 0.553-0.555 ms;
+  //  * every side stream kind ran on its own hardware queue (rocprofv3 Queue_Id 2, compute on 1).
+  // CDP_COMM_STREAM = own (default) | pool | low | cumask selects the stream for such A/B runs.
   const char* kind = std::getenv("CDP_COMM_STREAM");
-  stream_kind_ = kind && *kind ? kind : "pool";
+  stream_kind_ = kind && *kind ? kind : "own";
   if (stream_kind_ == "own" || stream_kind_ == "low") {
     int lo = 0, hi = 0;
     HIP_CHECK(hipDeviceGetStreamPriorityRange(&lo, &hi));
@@ -123,7 +123,7 @@ RcclComm::RcclComm(const std::string& uid, int rank, int world, int device, doub
     HIP_CHECK(hipExtStreamCreateWithCUMask(&stream_, 8, mask));
     own_stream_ = true;
   } else {
-    TORCH_CHECK(stream_kind_ == "pool", "CDP_COMM_STREAM must be pool, own, low or cumask");
+    TORCH_CHECK(stream_kind_ == "pool", "CDP_COMM_STREAM must be own, pool, low or cumask");
     stream_ = c10::hip::getStreamFromPool(/*isHighPriority=*/false, (c10::DeviceIndex)device).stream();
   }
   HIP_CHECK(hipEventCreateWithFlags(&start_ev_, hipEventDisableTiming));

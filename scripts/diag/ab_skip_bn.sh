@@ -8,7 +8,7 @@ for rep in 1 2 3; do
   for lb in 32 64; do
     for v in 0 1; do
       CDP_EXP_SKIP_BN_APPLY=$v timeout -k 10 120 python3 bench.py --local-batch $lb --steps 50 --warmup 5 --no-extra > gpurun_out/skipbn/$lb.$v.$rep.log 2>&1 || { echo "lb $lb skip $v failed"; tail -5 gpurun_out/skipbn/$lb.$v.$rep.log; exit 1; }
-      python3 -c "import json; r=json.loads(open('gpurun_out/skipbn/$lb.$v.$rep.log').read().strip().splitlines()[-1]); print('images $lb skip_bn_apply=$v', r['ms_per_step'], 'ms')"
+      python3 -c "import json; r=json.loads([l for l in open('gpurun_out/skipbn/$lb.$v.$rep.log') if l.startswith('{')][-1]); print('images $lb skip_bn_apply=$v', r['ms_per_step'], 'ms')"
     done
   done
 done
