@@ -35,6 +35,7 @@ import time
 BASELINE_IMG_S = 322.9  # reference Part 1, single process, B=256 (measured, CPU)
 METRIC = "images/sec (whole node) VGG-11 CIFAR-shaped at 1/2/4/8 MI355X; scaling eff"
 REF_GLOBAL_BATCH = 256
+_GRAPH_FALLBACKS = []  # measurements that timed eager steps because a capture failed (see _Run._note_fallback)
 
 
 def parse(argv=None):
@@ -139,7 +140,7 @@ class _Run:
         self.ddp_w1 = os.environ.get("CDP_BENCH_DDP_W1") == "1" and world == 1
         self.sync_grads = sync_grads and (world > 1 or self.ddp_w1)
         cdp.utils.seed_everything(0)
-        model_name = model_name or args.model
+        self.model_name = model_name = model_name or args.model
         self.imagenet = model_name.startswith("resnet")
         size = args.dataset_size if dev.type == "cuda" else min(args.dataset_size, 8 * local_batch)
         size = max(size, local_batch * world)  # at least one batch per rank
@@ -258,6 +259,7 @@ class _Run:
             dbg("captured")
         except Exception as e:  # pragma: no cover - depends on the runtime
             print(f"[bench] hipGraph capture failed ({str(e)[:200]!r}); timing eager steps", file=sys.stderr)
+            self._note_fallback(f"capture failed on this rank: {str(e)[:160]}")
             ok = False
             self.graph = None
             self._recover_from_failed_capture()
@@ -274,6 +276,7 @@ class _Run:
             store.wait(keys)
             if any(store.get(k) != b"1" for k in keys) and self.graph is not None:
                 print("[bench] another rank could not capture; all ranks time eager steps", file=sys.stderr)
+                self._note_fallback("another rank could not capture")
                 self.graph.reset()
                 self.graph = None
                 self.graph_collectives = None
@@ -285,6 +288,12 @@ class _Run:
             for i in range(max(2, warmup)):
                 self.graph.replay()
             torch.cuda.synchronize()
+
+    def _note_fallback(self, reason):
+        """Record which measurement times eager steps instead of graph replays, and why (the record's
+        ``graph_fallbacks`` list; each entry's own ``hipgraph`` flag only says that it fell back)."""
+        _GRAPH_FALLBACKS.append({"model": self.model_name, "strategy": self.strategy, "local_batch": self.local_batch,
+                                 "sync_grads": self.sync_grads, "reason": reason})
 
     def _recover_from_failed_capture(self):
         """An invalidated capture leaves the thread's last HIP error set (the next launch would report
@@ -604,6 +613,7 @@ def rank_main(args) -> int:
                 "strategy": args.strategy if world > 1 else "single",
                 "comm": comm_kind,
                 "comm_fallback_reason": dist.comm_fallback_reason() if world > 1 else None,
+                "graph_fallbacks": _GRAPH_FALLBACKS,
                 # native-communicator collectives recorded inside the captured step (replayed every
                 # step); null when the step is not captured or collectives go through torch
                 "graph_collectives": graph_collectives if hipgraph else None,

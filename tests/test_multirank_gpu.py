@@ -117,3 +117,7 @@ def test_capture_failure_on_one_rank_makes_every_rank_eager():
     assert "another rank could not capture; all ranks time eager steps" in r.stderr, r.stderr[-3000:]
     rec = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
     assert rec["replicas_identical"] is True and rec["ranks_seen"] == 2
+    # the record names the measurement that fell back (rank 0 captured, its peer did not)
+    fb = rec["config"]["graph_fallbacks"]
+    assert fb and all(f["reason"] == "another rank could not capture" for f in fb), fb
+    assert {f["sync_grads"] for f in fb} == {False}, fb
