@@ -979,6 +979,17 @@ void bn_eval_stats_launch(int C, const float* gamma, const float* beta, const fl
                      stats);
 }
 
+// Timing experiment only (wrong numbers): CDP_EXP_SKIP_BN_APPLY=2 makes the fused finalize + apply
+// kernels merge one statistics partial instead of all of them, same grid and block shape -- the
+// ceiling of finalizing in the producer, which would leave the apply kernels 2 floats per channel.
+static int exp_merge_parts(int nparts) {
+  static const bool on = [] {
+    const char* e = std::getenv("CDP_EXP_SKIP_BN_APPLY");
+    return e && e[0] == '2';
+  }();
+  return on ? 1 : nparts;
+}
+
 // (up to 512 partials: 16-channel blocks above 32 partials, 32 M2-merge loads per thread)
 bool bn_fin_act_ok(int nparts, int C, bool residual) { return !residual && nparts <= FIN_MAXP16 && (C % 64) == 0; }
 
@@ -1006,7 +1017,7 @@ void bn_fin_act_launch(const float* part, int nparts, int rpp, int C, const floa
   const int M = N * H * W;
   const int cg = fin_cg(nparts);
   hipLaunchKernelGGL(cg == 64 ? bn_fin_act_kernel<64> : bn_fin_act_kernel<16>, dim3(grid), dim3(256), 0, st, part,
-                     nparts, rpp, M, C, gamma, beta, running_mean, running_var, nbt, momentum, eps, stats, y, out, N,
+                     exp_merge_parts(nparts), rpp, M, C, gamma, beta, running_mean, running_var, nbt, momentum, eps, stats, y, out, N,
                      H, W, pool ? 1 : 0, relu ? 1 : 0, grid / (C / cg),
                      make_fastdiv(out_pixels_per_image(H, W, pool)), am);
 }
@@ -1019,7 +1030,7 @@ void bn_bwd_fin_apply_launch(const float* part, int nparts, int ps, const float*
                              const float* stats, float* dy, float* gbeta, float* ggamma, float* gdb, int N, int H,
                              int W, int C, bool pool, bool relu, ActMaxOut am, hipStream_t st) {
   const int grid = bn_fin_act_grid(N, H, W, C, pool);
-  hipLaunchKernelGGL(bn_bwd_fin_apply_kernel, dim3(grid), dim3(256), 0, st, part, nparts, ps, y, gout, stats, dy,
+  hipLaunchKernelGGL(bn_bwd_fin_apply_kernel, dim3(grid), dim3(256), 0, st, part, exp_merge_parts(nparts), ps, y, gout, stats, dy,
                      gbeta, ggamma, gdb, N, H, W, C, pool ? 1 : 0, relu ? 1 : 0, grid / (C / 64),
                      make_fastdiv(out_pixels_per_image(H, W, pool)), am);
 }

@@ -915,7 +915,8 @@ std::string get_conv_gemm() {
 // partials are returned in a second tensor [nparts, Cout, 2] together with rows-per-part.
 std::vector<at::Tensor> conv2d_fwd(const at::Tensor& x_, const at::Tensor& w_, const c10::optional<at::Tensor>& bias,
                                    int64_t stride, int64_t pad, bool want_stats, const c10::optional<at::Tensor>& x_amax,
-                                   const c10::optional<at::Tensor>& w_amax) {
+                                   const c10::optional<at::Tensor>& w_amax, const c10::optional<at::Tensor>& bn_stats,
+                                   bool bn_relu) {
   check_f32_cuda(x_, "x");
   check_f32_cuda(w_, "weight");
   TORCH_CHECK(x_.dim() == 4 && w_.dim() == 4, "conv2d_fwd expects 4-D input and weight");
@@ -946,6 +947,18 @@ std::vector<at::Tensor> conv2d_fwd(const at::Tensor& x_, const at::Tensor& w_, c
   set_scales(p, xa, wa, false, Co, C);
   p.y = y.data_ptr<float>();
   p.bias = fptr(bias);
+  if (bn_stats.has_value() && bn_stats->defined()) {
+    // BatchNorm on the A load: x is the producer's raw conv output; the operand maxima given (or
+    // measured) must be those of the transformed activation
+    TORCH_CHECK(f16x2_mode() && x3_ok(p, false) && C % 32 == 0 && Kdim % 32 == 0 && C <= kMaxBnLoadC,
+                "conv2d_fwd: BatchNorm on the operand load needs the f16x2 engine, C % 32 == 0 and C <= ",
+                kMaxBnLoadC);
+    TORCH_CHECK(bn_stats->is_cuda() && bn_stats->scalar_type() == at::kFloat && bn_stats->numel() == 4 * C &&
+                    bn_stats->is_contiguous(),
+                "conv2d_fwd: bn_stats must be a contiguous fp32 [4, C] stats block");
+    p.bn_st = bn_stats->data_ptr<float>();
+    p.bn_relu = bn_relu ? 1 : 0;
+  }
   // BN partials: one per BM-row tile (splits == 1) or per reduction row block (split-K)
   std::function<float*(int)> alloc_part;
   if (want_stats)
