@@ -55,7 +55,8 @@ def test_bn_on_load_equals_materialized_apply(native, shape, relu):
         w = (torch.randn(Co, C, k, k, device=dev, generator=gen) / (C * k * k) ** 0.5).contiguous(
             memory_format=torch.channels_last)
         st = _stats(C, dev, gen)
-        act = torch.addcmul(st[3].view(1, C, 1, 1), y, st[2].view(1, C, 1, 1))
+        # fma(y, scale, shift) rounded once, as the kernels compute it (y * scale is exact in fp64)
+        act = (y.double() * st[2].double().view(1, C, 1, 1) + st[3].double().view(1, C, 1, 1)).float()
         if relu:
             act = act.clamp_min(0)
         act = act.contiguous(memory_format=torch.channels_last)
