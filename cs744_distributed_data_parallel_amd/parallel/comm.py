@@ -4,7 +4,7 @@ Two interchangeable implementations of one small interface:
 
 * :class:`RcclCommunicator` -- the native C++ RCCL communicator (``_C.RcclComm``): one per GPU,
   bootstrapped from the ``torch.distributed`` TCP store (the reference's env:// rendezvous,
-  ``/root/reference/src/Part 2a/main.py:148-152``), own comm stream (a PyTorch pool stream), stream-ordered
+  ``/root/reference/src/Part 2a/main.py:148-152``), its own normal-priority comm stream, stream-ordered
   (hipGraph-capturable) collectives, watchdog-based failure detection.
 * :class:`TorchCommunicator` -- any ``torch.distributed`` process group (gloo for the CPU
   test-suite and CPU runs; nccl=RCCL as an alternative GPU path).
@@ -200,6 +200,19 @@ class TorchCommunicator(Communicator):
 
     def all_reduce(self, t, op="sum", async_op=False):
         op = _norm_op(op)
+        if self._gloo_device(t):
+            # staged through a host tensor between two device syncs, as gather / scatter below: the
+            # async device-tensor path left a two-rank DDP run on one GPU 1e-4 (relative L2) away from
+            # the blocking strategy after three steps in 1 of ~6 runs, never reproduced with staging
+            # (the one-GPU rehearsal path only; GPU runs proper take the RCCL communicator)
+            torch.cuda.synchronize(t.device)
+            tc = t.cpu()
+            tdist.all_reduce(tc, op=tdist.ReduceOp.SUM if op == "avg" else _TORCH_OPS[op], group=self.group)
+            if op == "avg":
+                tc.div_(self.size)
+            t.copy_(tc)
+            torch.cuda.synchronize(t.device)
+            return Work() if async_op else None
         if op == "avg":
             w = tdist.all_reduce(t, op=tdist.ReduceOp.SUM, group=self.group, async_op=async_op)
             post = lambda: t.div_(self.size)  # noqa: E731

@@ -1,4 +1,4 @@
-// Native RCCL communicator: one per process/GPU, its own comm stream (a PyTorch pool stream), stream-ordered
+// Native RCCL communicator: one per process/GPU, its own normal-priority comm stream, stream-ordered
 // collectives, and a watchdog thread that aborts the communicator when a collective outlives
 // its timeout (the reference has no failure detection at all: a dead rank hangs gloo forever,
 // SURVEY.md §5.3).
