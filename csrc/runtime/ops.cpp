@@ -97,11 +97,15 @@ int split_planes() { return conv_gemm_mode() == 2 ? 1 : conv_gemm_mode() == 3 ? 
 //  * inside a hipGraph capture: every capture takes fresh chunks (from the graph's memory pool,
 //    kept alive with it) whose memset is captured, so each replay re-zeroes them before its
 //    producers run.
-// Everything is ordered on the current stream, like the caching allocator's reuse.
+// Everything is ordered on the current stream, like the caching allocator's reuse; a chunk taken up
+// on another stream than its last user's (its memset, or slots still being read) first makes the
+// new stream wait for that one.
 constexpr long long kSlotChunk = 1LL << 16;  // int32 slots per chunk (256 KB)
 struct SlotPool {
   std::vector<at::Tensor> ring;
   std::vector<long long> used;
+  std::vector<hipStream_t> last;  // stream of each chunk's latest memset / allocation
+  hipEvent_t ev = nullptr;
   int cur = -1;
   unsigned long long cap_id = 0;
   at::Tensor cap_cur;
@@ -142,6 +146,16 @@ at::Tensor alloc_slots(long long n, const at::Tensor& like, hipStream_t st) {
     return v;
   }
   TORCH_CHECK(cs == hipStreamCaptureStatusNone, "act max slots: stream capture invalidated");
+  // st waits for whatever chunk i's last stream has enqueued (no-op on the same stream)
+  auto order_after = [&](int i) {
+    const hipStream_t prev = P.last[i];
+    if (prev != st) {
+      if (!P.ev) TORCH_CHECK(hipEventCreateWithFlags(&P.ev, hipEventDisableTiming) == hipSuccess, "act max slots: event");
+      TORCH_CHECK(hipEventRecord(P.ev, prev) == hipSuccess && hipStreamWaitEvent(st, P.ev, 0) == hipSuccess,
+                  "act max slots: cross-stream ordering failed");
+      P.last[i] = st;
+    }
+  };
   if (P.cur < 0 || P.used[P.cur] + n > P.ring[P.cur].numel()) {
     int pick = -1;
     for (size_t i = 0; i < P.ring.size(); ++i)
@@ -152,14 +166,18 @@ at::Tensor alloc_slots(long long n, const at::Tensor& like, hipStream_t st) {
     if (pick < 0) {
       P.ring.push_back(fresh(std::max(kSlotChunk, n)));
       P.used.push_back(0);
+      P.last.push_back(st);
       pick = (int)P.ring.size() - 1;
     } else {
+      order_after(pick);  // the chunk's last readers finish before the re-zeroing
       TORCH_CHECK(hipMemsetAsync(P.ring[pick].data_ptr(), 0, (size_t)P.ring[pick].numel() * 4, st) == hipSuccess,
                   "act max slots: memset failed");
       slot_memsets().fetch_add(1, std::memory_order_relaxed);
       P.used[pick] = 0;
     }
     P.cur = pick;
+  } else {
+    order_after(P.cur);  // the chunk's memset precedes the new producer
   }
   at::Tensor v = P.ring[P.cur].narrow(0, P.used[P.cur], n);
   P.used[P.cur] += n;

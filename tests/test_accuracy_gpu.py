@@ -174,6 +174,30 @@ def test_act_max_matches_torch_per_image_and_channel():
     assert torch.equal(s2[37:37 + K * 200].view(torch.float32).view(K, 200).amax(0), t2.abs().amax(0))
 
 
+def test_act_max_slots_ordered_across_streams():
+    """Act max slots are views into chunks that one memset zeroes. A producer on another stream that
+    takes slots from a chunk whose memset is still queued behind a busy stream must wait for it, or
+    the late memset wipes what it wrote (csrc/runtime/ops.cpp alloc_slots, order_after)."""
+    if C().get_conv_gemm() != "f16x2":
+        pytest.skip("act max exists for the f16x2 engine only")
+    K = C().act_max_copies()
+    gen = torch.Generator(device="cuda").manual_seed(9)
+    tb = torch.randn(64, 4992, device="cuda", generator=gen)  # 64 + 8 x 4992 = 40000 slots: a new chunk
+    tc = torch.randn(32, 2496, device="cuda", generator=gen)  # 20032 more slots: the same chunk
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    s1.wait_stream(torch.cuda.current_stream())
+    s2.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s1):
+        C().gpu_sleep(3000.0)  # the chunk's memset and s1's pass queue behind 3 ms
+        mb = C().act_max(tb)
+    with torch.cuda.stream(s2):
+        mc = C().act_max(tc)
+    torch.cuda.synchronize()
+    assert torch.equal(mb[:64].view(torch.float32), tb.abs().amax(1))
+    assert torch.equal(mc[:32].view(torch.float32), tc.abs().amax(1))
+    assert torch.equal(mc[32:32 + K * 2496].view(torch.float32).view(K, 2496).amax(0), tc.abs().amax(0))
+
+
 @pytest.mark.parametrize("pool", [False, True])
 @pytest.mark.parametrize("N,Co,HW", [(32, 64, 16), (8, 512, 2), (256, 128, 8), (4, 2048, 2)])
 def test_bn_producers_write_exact_act_max(N, Co, HW, pool):
