@@ -100,7 +100,7 @@ int split_planes() { return conv_gemm_mode() == 2 ? 1 : conv_gemm_mode() == 3 ? 
 // Everything is ordered on the current stream, like the caching allocator's reuse; a chunk taken up
 // on another stream than its last user's (its memset, or slots still being read) first makes the
 // new stream wait for that one.
-constexpr long long kSlotChunk = 1LL << 16;  // int32 slots per chunk (256 KB)
+constexpr long long kSlotChunk = 1LL << 20;  // int32 slots per chunk (4 MB: one memset per ResNet-50 step)
 struct SlotPool {
   std::vector<at::Tensor> ring;
   std::vector<long long> used;

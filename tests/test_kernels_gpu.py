@@ -216,12 +216,15 @@ def test_linear(B, I, O):
         assert rel_err(a, r) < 2e-5
 
 
-def test_cross_entropy_and_accuracy():
+@pytest.mark.parametrize("B,K", [(256, 10), (64, 1000), (37, 1000), (5, 100), (3, 2000)])
+def test_cross_entropy_and_accuracy(B, K):
+    """Softmax cross-entropy (one thread per row for <= 64 classes, four rows per wave for <= 1024,
+    one row per wave beyond) and the correct count, against torch in fp64."""
     from cs744_distributed_data_parallel_amd.ops import functional as CF
 
     torch.manual_seed(5)
-    logits = torch.randn(256, 10, device="cuda", requires_grad=True)
-    t = torch.randint(0, 10, (256,), device="cuda")
+    logits = (3 * torch.randn(B, K, device="cuda")).requires_grad_()
+    t = torch.randint(0, K, (B,), device="cuda")
     loss = CF.cross_entropy(logits, t)
     lr = logits.detach().double().cpu().requires_grad_()
     ref = F.cross_entropy(lr, t.cpu())
