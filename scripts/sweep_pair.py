@@ -133,6 +133,7 @@ def main():
                                 print(f"  skip {cand}: {str(e).splitlines()[0]}", flush=True)
                                 continue
                             rows.append((cand["d"], cand["w"], round(t, 2)))
+                            print(f"    B={B} L{li} {which} {cand[which]} {t:.2f} us", flush=True)  # progress
                             if t < best * 0.995:
                                 best, cur = t, cand
             # the first timing of a layer runs cold: re-time the planner's and the best plan alternately
