@@ -320,6 +320,7 @@ def test_bench_self_launches_ranks_cpu():
     # self-verification: every rank holds the same parameters + momentum after the timed steps
     assert rec["replicas_identical"] is True
     assert rec["config"]["comm_fallback_reason"] is None and rec["config"]["graph_collectives"] is None
+    assert rec["config"]["graph_fallbacks"] == []  # CPU steps are eager by design, not by a failed capture
     blk = rec["strategies"]
     assert blk["local_batch"] == 8 and blk["global_batch"] == 16 and blk["no_sync"]["ms_per_step"] > 0
     for strat, part in (("gather_scatter", "Part 2a"), ("allreduce_blocking", "Part 2b"),
