@@ -159,7 +159,7 @@ class _ConvBNAct(torch.autograd.Function):
     def forward(ctx, x, w, b, gamma, beta, rm, rv, nbt, momentum, eps, training, stride, pad, pool, relu, residual,
                 res_sink=None, dx_sink=None, w_amax=None, w_t=None, bn_link=False):
         C = _native.lib()
-        out, y, stats, xsave, out_amax, x_amax, w_amax = C.conv_bn_act_fwd(
+        out, y, stats, xsave, out_amax, x_amax, w_amax, rmask = C.conv_bn_act_fwd(
             x, w, b, gamma, beta, rm, rv, nbt, momentum, eps, training, stride, pad, pool, relu, residual, _get_amax(x),
             w_amax,
         )
@@ -168,7 +168,9 @@ class _ConvBNAct(torch.autograd.Function):
         ctx.sinks = (res_sink, dx_sink)
         ctx.amax = (x_amax, w_amax)  # f16x2 engine only (else None): W and x are unchanged by backward
         ctx.w_t = w_t  # W^T from weight_prep (this step's weights), or None: dgrad transposes itself
-        zout = out if residual is not None else None
+        # a residual block's ReLU routing: its 1-bit-per-channel pass mask (1/16 of out's bytes) when
+        # the kernel wrote one, else out itself
+        zout = (rmask if rmask is not None else out) if residual is not None else None
         ctx.save_for_backward(xsave, w, y, stats, zout)  # xsave: x, or x zero-padded to 4k channels
         _set_amax(out, out_amax)
         # the producer of x handed over its BN (see _BNLink) if this block is its only consumer

@@ -319,7 +319,8 @@ __global__ __launch_bounds__(256) void bn_fin_act_kernel(const float* __restrict
 __global__ __launch_bounds__(256) void bn_act_fwd_kernel(const float* __restrict__ y, const float* __restrict__ stats,
                                                          const float* __restrict__ res, float* __restrict__ out,
                                                          int N, int H, int W, int C, int pool, int relu, int per,
-                                                         int qmode, FastDiv fd_C4, FastDiv fd_HWo, ActMaxOut am) {
+                                                         int qmode, FastDiv fd_C4, FastDiv fd_HWo, ActMaxOut am,
+                                                         unsigned char* __restrict__ rmask) {
   __shared__ ActMaxBlock<kMaxActC> sam;
   const int C4 = C >> 2;
   const int Ho = pool ? H / 2 : H, Wo = pool ? W / 2 : W;
@@ -351,6 +352,8 @@ __global__ __launch_bounds__(256) void bn_act_fwd_kernel(const float* __restrict
       if (relu) {
         z.x = fmaxf(z.x, 0.f); z.y = fmaxf(z.y, 0.f); z.z = fmaxf(z.z, 0.f); z.w = fmaxf(z.w, 0.f);
       }
+      if (rmask)  // the ReLU's pass mask for the backward (1 byte per float4 instead of re-reading out)
+        rmask[i] = (unsigned char)((z.x > 0.f ? 1 : 0) | (z.y > 0.f ? 2 : 0) | (z.z > 0.f ? 4 : 0) | (z.w > 0.f ? 8 : 0));
     } else {
       const int wo = pix % Wo;
       const int t = pix / Wo;
@@ -405,6 +408,11 @@ __device__ __forceinline__ void pool_relu_grad(float z0, float z1, float z2, flo
 
 #define F4GET(v, j) ((j) == 0 ? (v).x : (j) == 1 ? (v).y : (j) == 2 ? (v).z : (v).w)
 
+// the post-ReLU output's sign pattern of one float4 from its residual mask byte (bn_act_fwd_kernel)
+__device__ __forceinline__ float4 mask_f4(unsigned char m) {
+  return make_float4((float)(m & 1), (float)((m >> 1) & 1), (float)((m >> 2) & 1), (float)((m >> 3) & 1));
+}
+
 // Per (block, channel) partial sums of dz and dz*xhat, where dz is the gradient at the BN output,
 // and (PS == 3) of xhat itself, from which chan_finalize derives the conv-bias gradient
 // sum(dy) = -scale * sum(xhat) * sum(dz*xhat) / M without a second pass over dy.
@@ -413,7 +421,8 @@ template <int PS>
 __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const float* __restrict__ y, const float* __restrict__ gout,
                                                             const float* __restrict__ stats, float* __restrict__ part,
                                                             int N, int H, int W, int C, int pool, int relu,
-                                                            const float* __restrict__ zout) {
+                                                            const float* __restrict__ zout,
+                                                            const unsigned char* __restrict__ rmask) {
   __shared__ float4 red1[256], red2[256], red3[PS == 3 ? 256 : 1];
   const int C4 = C >> 2;
   const int tid = threadIdx.x;
@@ -439,7 +448,8 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const float* __restr
         const float4 g = ld4(gout + px * C + 4 * cq);
         if (!pool) {
           const float4 yv = ld4(y + px * C + 4 * cq);
-          const float4 z = zout ? ld4(zout + px * C + 4 * cq) : affine_act(yv, sc, sh, relu);
+          const float4 z = rmask ? mask_f4(rmask[px * C4 + cq])
+                                 : zout ? ld4(zout + px * C + 4 * cq) : affine_act(yv, sc, sh, relu);
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
             const float dz = (!relu || F4GET(z, e) > 0.f) ? F4GET(g, e) : 0.f;
@@ -583,7 +593,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const float* __restri
                                                            float* __restrict__ dbias_part, int N, int H, int W,
                                                            int C, int pool, int relu, const float* __restrict__ zout,
                                                            float* __restrict__ dres, FastDiv fd_IMG, FastDiv fd_HW,
-                                                           ActMaxOut am) {
+                                                           ActMaxOut am, const unsigned char* __restrict__ rmask) {
   __shared__ float4 red[256];
   __shared__ ActMaxBlock<kMaxActC> sam;
   const bool want = am.img != nullptr;
@@ -646,7 +656,8 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const float* __restri
         const float4 g = ld4(gout + px * C + 4 * cq);
         if (!pool) {
           const float4 yv = ld4(y + px * C + 4 * cq);
-          const float4 z = zout ? ld4(zout + px * C + 4 * cq) : affine_act(yv, sc, sh, relu);
+          const float4 z = rmask ? mask_f4(rmask[px * C4 + cq])
+                                 : zout ? ld4(zout + px * C + 4 * cq) : affine_act(yv, sc, sh, relu);
           float4 dz;
           dz.x = (!relu || z.x > 0.f) ? g.x : 0.f;
           dz.y = (!relu || z.y > 0.f) ? g.y : 0.f;
@@ -1040,7 +1051,7 @@ int bn_act_grid(int N, int H, int W, int C, bool pool) {
 }
 
 void bn_act_fwd_launch(const float* y, const float* stats, const float* res, float* out, int N, int H, int W, int C,
-                       bool pool, bool relu, hipStream_t st, ActMaxOut am) {
+                       bool pool, bool relu, hipStream_t st, ActMaxOut am, unsigned char* rmask) {
   const int C4 = C / 4;
   const long long total = (long long)N * out_pixels_per_image(H, W, pool) * C4;
   // contiguous per-block ranges, whole multiples of 256 float4 (and of C4: fixed channel quads)
@@ -1050,18 +1061,18 @@ void bn_act_fwd_launch(const float* y, const float* stats, const float* res, flo
   const long long per = std::max(unit, ((total + blocks - 1) / blocks + unit - 1) / unit * unit);
   hipLaunchKernelGGL(bn_act_fwd_kernel, dim3((unsigned)((total + per - 1) / per)), dim3(256), 0, st, y, stats, res,
                      out, N, H, W, C, pool ? 1 : 0, relu ? 1 : 0, (int)per, qmode, make_fastdiv(C4),
-                     make_fastdiv(out_pixels_per_image(H, W, pool)), am);
+                     make_fastdiv(out_pixels_per_image(H, W, pool)), am, pool ? nullptr : rmask);
 }
 
 void bn_bwd_reduce_launch(const float* y, const float* gout, const float* stats, float* part, int nblocks, int N,
                           int H, int W, int C, bool pool, bool relu, const float* zout, hipStream_t st,
-                          bool with_xsum) {
+                          bool with_xsum, const unsigned char* rmask) {
   if (with_xsum)
     hipLaunchKernelGGL(bn_bwd_reduce_kernel<3>, dim3(nblocks), dim3(256), 0, st, y, gout, stats, part, N, H, W, C,
-                       pool ? 1 : 0, relu ? 1 : 0, zout);
+                       pool ? 1 : 0, relu ? 1 : 0, zout, rmask);
   else
     hipLaunchKernelGGL(bn_bwd_reduce_kernel<2>, dim3(nblocks), dim3(256), 0, st, y, gout, stats, part, N, H, W, C,
-                       pool ? 1 : 0, relu ? 1 : 0, zout);
+                       pool ? 1 : 0, relu ? 1 : 0, zout, rmask);
 }
 
 void chan_finalize_launch(const float* part, int nparts, int C, float* out, float* g0, float* g1, bool accumulate,
@@ -1076,10 +1087,10 @@ void chan_finalize_launch(const float* part, int nparts, int C, float* out, floa
 
 void bn_bwd_apply_launch(const float* y, const float* gout, const float* stats, const float* sums, float* dy,
                          float* dbias_part, int nblocks, int N, int H, int W, int C, bool pool, bool relu,
-                         const float* zout, float* dres, hipStream_t st, ActMaxOut am) {
+                         const float* zout, float* dres, hipStream_t st, ActMaxOut am, const unsigned char* rmask) {
   hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(nblocks), dim3(256), 0, st, y, gout, stats, sums, dy, dbias_part, N,
                      H, W, C, pool ? 1 : 0, relu ? 1 : 0, zout, dres, make_fastdiv(out_pixels_per_image(H, W, pool)),
-                     make_fastdiv(H * W), am);
+                     make_fastdiv(H * W), am, rmask);
 }
 
 }  // namespace cdp

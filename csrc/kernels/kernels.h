@@ -237,17 +237,21 @@ void bn_bwd_fin_apply_launch(const float* part, int nparts, int ps, const float*
                              const float* stats, float* dy, float* gbeta, float* ggamma, float* gdb, int N, int H,
                              int W, int C, bool pool, bool relu, ActMaxOut am, hipStream_t st);
 int bn_act_grid(int N, int H, int W, int C, bool pool);
+// rmask (residual + ReLU blocks): one byte per float4 of the output, bit e = (output channel 4q+e > 0),
+// at the float4's index (pixel * C/4 + q). The backward reads it instead of the 16x larger output.
 void bn_act_fwd_launch(const float* y, const float* stats, const float* res, float* out, int N, int H, int W, int C,
-                       bool pool, bool relu, hipStream_t st, ActMaxOut am = ActMaxOut{nullptr, nullptr});
+                       bool pool, bool relu, hipStream_t st, ActMaxOut am = ActMaxOut{nullptr, nullptr},
+                       unsigned char* rmask = nullptr);
 void bn_bwd_reduce_launch(const float* y, const float* gout, const float* stats, float* part, int nblocks, int N,
                           int H, int W, int C, bool pool, bool relu, const float* zout, hipStream_t st,
-                          bool with_xsum = false);
+                          bool with_xsum = false, const unsigned char* rmask = nullptr);
 void chan_finalize_launch(const float* part, int nparts, int C, float* out, float* g0, float* g1, bool accumulate,
                           hipStream_t st, int ps = 2, float* gdb = nullptr, const float* scale = nullptr,
                           long long M = 0, int dbmode = 0);
 void bn_bwd_apply_launch(const float* y, const float* gout, const float* stats, const float* sums, float* dy,
                          float* dbias_part, int nblocks, int N, int H, int W, int C, bool pool, bool relu,
-                         const float* zout, float* dres, hipStream_t st, ActMaxOut am = ActMaxOut{nullptr, nullptr});
+                         const float* zout, float* dres, hipStream_t st, ActMaxOut am = ActMaxOut{nullptr, nullptr},
+                         const unsigned char* rmask = nullptr);
 
 // misc.hip
 void xent_fwd_launch(const float* logits, const long long* tgt, int B, int C, float* loss, long long* correct,

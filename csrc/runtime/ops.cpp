@@ -1249,7 +1249,7 @@ std::vector<at::Tensor> stem_bn_act_fwd(const at::Tensor& x_, const at::Tensor& 
   else
     bn_act_fwd_launch(y.data_ptr<float>(), stats.data_ptr<float>(), nullptr, out.data_ptr<float>(), N, H, W, Co, pool,
                       relu, st, am);
-  return {out, y, stats, x, out_amax, at::Tensor(), at::Tensor()};
+  return {out, y, stats, x, out_amax, at::Tensor(), at::Tensor(), at::Tensor()};
 }
 
 // ---------------------------------------------------------------- fused block forward
@@ -1357,10 +1357,19 @@ std::vector<at::Tensor> conv_bn_act_fwd(const at::Tensor& x, const at::Tensor& w
     bn_fin_act_launch(r[1].data_ptr<float>(), nparts, rpp, C, fptr(gamma), fptr(beta), fptr_mut(running_mean),
                       fptr_mut(running_var), nbt, (float)momentum, (float)eps, stats.data_ptr<float>(),
                       y.data_ptr<float>(), out.data_ptr<float>(), N, H, W, pool, relu, am, st);
-  else
+  // a residual block's ReLU pass mask (1 byte per float4): its backward reads this, not `out`
+  at::Tensor rmask;
+  static const bool mask_on = [] {
+    const char* e = std::getenv("CDP_RES_MASK");
+    return !(e && e[0] == '0');
+  }();
+  if (mask_on && has_res && relu && !fused_fin)
+    rmask = at::empty({(long long)N * H * W * (C / 4)}, opts.dtype(at::kByte));
+  if (!(fused_fin && exp_skip_bn_apply()) && !fused_fin)
     bn_act_fwd_launch(y.data_ptr<float>(), stats.data_ptr<float>(), res.defined() ? res.data_ptr<float>() : nullptr,
-                      out.data_ptr<float>(), N, H, W, C, pool, relu, st, am);
-  return {out, y, stats, xin, out_amax, xa, wa};
+                      out.data_ptr<float>(), N, H, W, C, pool, relu, st, am,
+                      rmask.defined() ? rmask.data_ptr<uint8_t>() : nullptr);
+  return {out, y, stats, xin, out_amax, xa, wa, rmask};
 }
 
 // ---------------------------------------------------------------- fused block backward
@@ -1391,8 +1400,20 @@ std::vector<at::Tensor> conv_bn_act_bwd(const at::Tensor& gout_, const at::Tenso
     if (o.has_value() && o->defined()) return *o;
     return cl ? at::empty(shape, opts.memory_format(at::MemoryFormat::ChannelsLast)) : at::empty(shape, opts);
   };
+  // the residual block's ReLU: its pass mask (uint8, conv_bn_act_fwd's 8th output) or its output
   at::Tensor zout;
-  if (zout_.has_value() && zout_->defined()) zout = nhwc(*zout_);
+  const unsigned char* rmask = nullptr;
+  if (zout_.has_value() && zout_->defined()) {
+    if (zout_->scalar_type() == at::kByte) {
+      zout = *zout_;
+      TORCH_CHECK(zout.is_cuda() && zout.is_contiguous() && zout.numel() == (long long)N * H * W * (C / 4),
+                  "conv_bn_act_bwd: the residual ReLU mask must hold one byte per float4 of the output");
+      rmask = zout.data_ptr<uint8_t>();
+    } else {
+      zout = nhwc(*zout_);
+    }
+  }
+  const float* zout_f = zout.defined() && !rmask ? zout.data_ptr<float>() : nullptr;
   const int nblk = bn_bwd_grid(N, H, W, C, pool);
   // The conv-bias gradient sum(dy) comes out of the finalize of the statistics reduction
   // (chan_finalize dbmode): in training mode from one extra partial, sum(xhat); in eval mode as
@@ -1411,8 +1432,7 @@ std::vector<at::Tensor> conv_bn_act_bwd(const at::Tensor& gout_, const at::Tenso
   } else {
     part = at::empty({nblk, C, ps}, opts);
     bn_bwd_reduce_launch(y.data_ptr<float>(), gout.data_ptr<float>(), stats.data_ptr<float>(),
-                         part.data_ptr<float>(), nblk, N, H, W, C, pool, relu,
-                         zout.defined() ? zout.data_ptr<float>() : nullptr, st, ps == 3);
+                         part.data_ptr<float>(), nblk, N, H, W, C, pool, relu, zout_f, st, ps == 3, rmask);
   }
   const int nparts = (int)part.size(0);
   at::Tensor sums = at::empty({2, C}, opts);
@@ -1476,8 +1496,8 @@ std::vector<at::Tensor> conv_bn_act_bwd(const at::Tensor& gout_, const at::Tenso
   else
     bn_bwd_apply_launch(y.data_ptr<float>(), gout.data_ptr<float>(), stats.data_ptr<float>(),
                         sums.data_ptr<float>(), dy.data_ptr<float>(), sep_db ? dbpart.data_ptr<float>() : nullptr,
-                        nblk, N, H, W, C, pool, relu, zout.defined() ? zout.data_ptr<float>() : nullptr,
-                        dres.defined() ? dres.data_ptr<float>() : nullptr, st, am);
+                        nblk, N, H, W, C, pool, relu, zout_f,
+                        dres.defined() ? dres.data_ptr<float>() : nullptr, st, am, rmask);
   const c10::optional<at::Tensor> dya = dy_amax.defined() ? c10::optional<at::Tensor>(dy_amax) : c10::nullopt;
   if (sep_db)
     chan_finalize_launch(dbpart.data_ptr<float>(), nblk, C, nullptr, db.data_ptr<float>(), nullptr, false, st);

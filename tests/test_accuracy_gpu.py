@@ -218,7 +218,7 @@ def test_bn_producers_write_exact_act_max(N, Co, HW, pool):
     b = torch.randn(Co, device="cuda", generator=gen)
     g = torch.rand(Co, device="cuda", generator=gen) + 0.5
     be = torch.randn(Co, device="cuda", generator=gen)
-    out, _, _, _, amax, _, _ = C().conv_bn_act_fwd(x, w, b, g, be, None, None, None, 0.1, 1e-5, True, 1, 1, pool,
+    out, _, _, _, amax, _, _, _ = C().conv_bn_act_fwd(x, w, b, g, be, None, None, None, 0.1, 1e-5, True, 1, 1, pool,
                                                    True, None)
     torch.cuda.synchronize()
     assert torch.equal(amax[:N].view(torch.float32), out.abs().amax(dim=(1, 2, 3)))
@@ -242,7 +242,7 @@ def test_bn_backward_producers_write_act_max(N, Co, HW, pool, fused, monkeypatch
     b = torch.randn(Co, device="cuda", generator=gen)
     g = torch.rand(Co, device="cuda", generator=gen) + 0.5
     be = torch.randn(Co, device="cuda", generator=gen)
-    out, y, stats, xs, _, xa, wa = C().conv_bn_act_fwd(x, w, b, g, be, None, None, None, 0.1, 1e-5, True, 1, 1, pool,
+    out, y, stats, xs, _, xa, wa, _ = C().conv_bn_act_fwd(x, w, b, g, be, None, None, None, 0.1, 1e-5, True, 1, 1, pool,
                                                        True, None)
     gout = cl(torch.randn(out.shape, device="cuda", generator=gen))
     r = C().conv_bn_act_bwd(gout, xs, w, y, stats, 1, 1, pool, True, True, True, None, True, None, None, None, None,
