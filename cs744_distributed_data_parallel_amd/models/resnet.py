@@ -13,11 +13,16 @@ strided gather (forward) and the divisibility-masked transposed gather (data gra
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.nn as nn
 
 from ..ops import functional as CF
 from ..utils.arena import install_load_hooks
+
+# CDP_DEFER_DS=0: materialize the downsample branch's BatchNorm output (A/B)
+_DEFER_DS = os.environ.get("CDP_DEFER_DS", "1") != "0"
 
 
 class BasicBlock(nn.Module):
@@ -39,7 +44,9 @@ class BasicBlock(nn.Module):
             out = CF.conv_bn_act(x, self.conv1, self.bn1, relu=True, dx_sink=sink)
             if self.downsample is None:
                 return CF.conv_bn_act(out, self.conv2, self.bn2, relu=True, residual=x, res_sink=sink)
-            idt = CF.conv_bn_act(x, self.downsample[0], self.downsample[1], relu=False, dx_sink=sink)
+            # the downsample's BatchNorm is applied inside conv2's residual add (defer_apply)
+            idt = CF.conv_bn_act(x, self.downsample[0], self.downsample[1], relu=False, dx_sink=sink,
+                                 defer_apply=_DEFER_DS)
             return CF.conv_bn_act(out, self.conv2, self.bn2, relu=True, residual=idt)
         idt = x if self.downsample is None else self.downsample(x)
         out = self.relu(self.bn1(self.conv1(x)))
@@ -72,7 +79,9 @@ class Bottleneck(nn.Module):
             out = CF.conv_bn_act(out, self.conv2, self.bn2, relu=True)
             if self.downsample is None:
                 return CF.conv_bn_act(out, self.conv3, self.bn3, relu=True, residual=x, res_sink=sink)
-            idt = CF.conv_bn_act(x, self.downsample[0], self.downsample[1], relu=False, dx_sink=sink)
+            # the downsample's BatchNorm is applied inside conv3's residual add (defer_apply)
+            idt = CF.conv_bn_act(x, self.downsample[0], self.downsample[1], relu=False, dx_sink=sink,
+                                 defer_apply=_DEFER_DS)
             return CF.conv_bn_act(out, self.conv3, self.bn3, relu=True, residual=idt)
         idt = x if self.downsample is None else self.downsample(x)
         out = self.relu(self.bn1(self.conv1(x)))

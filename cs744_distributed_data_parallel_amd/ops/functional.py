@@ -157,12 +157,18 @@ def _get_link(t):
 class _ConvBNAct(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, b, gamma, beta, rm, rv, nbt, momentum, eps, training, stride, pad, pool, relu, residual,
-                res_sink=None, dx_sink=None, w_amax=None, w_t=None, bn_link=False):
+                res_sink=None, dx_sink=None, w_amax=None, w_t=None, bn_link=False, defer_apply=False):
         C = _native.lib()
+        # a residual that is a deferred BatchNorm branch (defer_apply below): its raw conv output and
+        # stats go to this block's apply pass instead of the (never written) placeholder
+        lazy = _get_deferred(residual) if residual is not None else None
         out, y, stats, xsave, out_amax, x_amax, w_amax, rmask = C.conv_bn_act_fwd(
-            x, w, b, gamma, beta, rm, rv, nbt, momentum, eps, training, stride, pad, pool, relu, residual, _get_amax(x),
-            w_amax,
+            x, w, b, gamma, beta, rm, rv, nbt, momentum, eps, training, stride, pad, pool, relu,
+            residual if lazy is None else None, _get_amax(x), w_amax,
+            None if lazy is None else lazy[0], None if lazy is None else lazy[1], defer_apply,
         )
+        if defer_apply:  # statistics only: `out` is a shape-only placeholder nothing may read
+            out._cdp_deferred_bn = (y, stats, out._version)
         ctx.cfg = (stride, pad, pool, relu, training, b is not None, residual is not None)
         ctx.params = (w, b, gamma, beta)
         ctx.sinks = (res_sink, dx_sink)
@@ -237,8 +243,18 @@ class _ConvBNAct(torch.autograd.Function):
             dbeta if ctx.needs_input_grad[4] else None,
             None, None, None, None, None, None, None, None, None, None,
             dres if has_res else None,
-            None, None, None, None, None,
+            None, None, None, None, None, None,
         )
+
+
+def _get_deferred(t):
+    """(raw conv output, stats) of a defer_apply placeholder that is still unmodified, else None."""
+    tag = getattr(t, "_cdp_deferred_bn", None)
+    if tag is None:
+        return None
+    if tag[2] != t._version:
+        raise RuntimeError("a deferred BatchNorm placeholder was modified in place; it holds no values")
+    return tag[0], tag[1]
 
 
 def _bwd_fuse_on() -> bool:
@@ -248,7 +264,7 @@ def _bwd_fuse_on() -> bool:
 
 
 def conv_bn_act(x, conv, bn, relu: bool = True, pool: bool = False, residual=None, res_sink=None, dx_sink=None,
-                w_amax=None, w_t=None, bn_link: bool = False):
+                w_amax=None, w_t=None, bn_link: bool = False, defer_apply: bool = False):
     """``[maxpool2x2](act(bn(conv(x)) [+ residual]))`` for an ``nn.Conv2d`` / ``nn.BatchNorm2d`` pair.
 
     ``pool`` is the reference's ``MaxPool2d(kernel_size=2, stride=2)``; ``relu`` its
@@ -259,6 +275,10 @@ def conv_bn_act(x, conv, bn, relu: bool = True, pool: bool = False, residual=Non
     ``w_t``: ``conv.weight``'s W^T from :func:`weight_prep` (else backward transposes it).
     ``bn_link``: the caller guarantees the result feeds exactly one op, the next ``conv_bn_act``
     (a VGG chain); its backward then reduces this block's BN statistics for it (:class:`_BNLink`).
+    ``defer_apply`` (GPU path; no ``relu`` / ``pool`` / ``residual``): compute the conv and the BN
+    statistics only and return a shape-only placeholder, to be passed as the ``residual`` of exactly
+    one ``conv_bn_act``, which then applies this BatchNorm inside its own apply pass (a ResNet
+    downsample branch: its normalized output is never written or read back).
     """
     stride = conv.stride[0]
     pad = conv.padding[0]
@@ -287,6 +307,7 @@ def conv_bn_act(x, conv, bn, relu: bool = True, pool: bool = False, residual=Non
             w_amax if w_amax is not None else getattr(conv, "_cdp_wamax", None),
             w_t if w_t is not None else getattr(conv, "_cdp_wt", None),
             bn_link,
+            defer_apply,
         )
     y = F.conv2d(x, conv.weight, conv.bias, conv.stride, conv.padding)
     y = bn(y)

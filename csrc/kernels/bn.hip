@@ -320,7 +320,9 @@ __global__ __launch_bounds__(256) void bn_act_fwd_kernel(const float* __restrict
                                                          const float* __restrict__ res, float* __restrict__ out,
                                                          int N, int H, int W, int C, int pool, int relu, int per,
                                                          int qmode, FastDiv fd_C4, FastDiv fd_HWo, ActMaxOut am,
-                                                         unsigned char* __restrict__ rmask) {
+                                                         unsigned char* __restrict__ rmask,
+                                                         const float* __restrict__ res_y,
+                                                         const float* __restrict__ res_st) {
   __shared__ ActMaxBlock<kMaxActC> sam;
   const int C4 = C >> 2;
   const int Ho = pool ? H / 2 : H, Wo = pool ? W / 2 : W;
@@ -347,6 +349,10 @@ __global__ __launch_bounds__(256) void bn_act_fwd_kernel(const float* __restrict
       z = affine_act(ld4(y + (long long)pix * C + 4 * c4), sc, sh, false);
       if (res) {
         const float4 r = ld4(res + (long long)pix * C + 4 * c4);
+        z.x += r.x; z.y += r.y; z.z += r.z; z.w += r.w;
+      } else if (res_y) {  // the downsample branch's BatchNorm, applied here instead of materialized
+        const float4 r = affine_act(ld4(res_y + (long long)pix * C + 4 * c4), ld4(res_st + 2 * C + 4 * c4),
+                                    ld4(res_st + 3 * C + 4 * c4), false);
         z.x += r.x; z.y += r.y; z.z += r.z; z.w += r.w;
       }
       if (relu) {
@@ -1051,7 +1057,8 @@ int bn_act_grid(int N, int H, int W, int C, bool pool) {
 }
 
 void bn_act_fwd_launch(const float* y, const float* stats, const float* res, float* out, int N, int H, int W, int C,
-                       bool pool, bool relu, hipStream_t st, ActMaxOut am, unsigned char* rmask) {
+                       bool pool, bool relu, hipStream_t st, ActMaxOut am, unsigned char* rmask, const float* res_y,
+                       const float* res_st) {
   const int C4 = C / 4;
   const long long total = (long long)N * out_pixels_per_image(H, W, pool) * C4;
   // contiguous per-block ranges, whole multiples of 256 float4 (and of C4: fixed channel quads)
@@ -1061,7 +1068,7 @@ void bn_act_fwd_launch(const float* y, const float* stats, const float* res, flo
   const long long per = std::max(unit, ((total + blocks - 1) / blocks + unit - 1) / unit * unit);
   hipLaunchKernelGGL(bn_act_fwd_kernel, dim3((unsigned)((total + per - 1) / per)), dim3(256), 0, st, y, stats, res,
                      out, N, H, W, C, pool ? 1 : 0, relu ? 1 : 0, (int)per, qmode, make_fastdiv(C4),
-                     make_fastdiv(out_pixels_per_image(H, W, pool)), am, pool ? nullptr : rmask);
+                     make_fastdiv(out_pixels_per_image(H, W, pool)), am, pool ? nullptr : rmask, res_y, res_st);
 }
 
 void bn_bwd_reduce_launch(const float* y, const float* gout, const float* stats, float* part, int nblocks, int N,

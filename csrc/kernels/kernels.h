@@ -239,9 +239,11 @@ void bn_bwd_fin_apply_launch(const float* part, int nparts, int ps, const float*
 int bn_act_grid(int N, int H, int W, int C, bool pool);
 // rmask (residual + ReLU blocks): one byte per float4 of the output, bit e = (output channel 4q+e > 0),
 // at the float4's index (pixel * C/4 + q). The backward reads it instead of the 16x larger output.
+// res_y / res_st: the residual as a raw conv output and its BN stats block, normalized on the fly
+// (res_y * scale + shift, no activation) instead of a materialized `res`
 void bn_act_fwd_launch(const float* y, const float* stats, const float* res, float* out, int N, int H, int W, int C,
                        bool pool, bool relu, hipStream_t st, ActMaxOut am = ActMaxOut{nullptr, nullptr},
-                       unsigned char* rmask = nullptr);
+                       unsigned char* rmask = nullptr, const float* res_y = nullptr, const float* res_st = nullptr);
 void bn_bwd_reduce_launch(const float* y, const float* gout, const float* stats, float* part, int nblocks, int N,
                           int H, int W, int C, bool pool, bool relu, const float* zout, hipStream_t st,
                           bool with_xsum = false, const unsigned char* rmask = nullptr);

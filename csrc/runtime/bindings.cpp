@@ -38,7 +38,11 @@ PYBIND11_MODULE(_C, m) {
   m.def("conv_bn_act_fwd", &conv_bn_act_fwd, py::arg("x"), py::arg("w"), py::arg("b"), py::arg("gamma"),
         py::arg("beta"), py::arg("running_mean"), py::arg("running_var"), py::arg("num_batches_tracked"),
         py::arg("momentum"), py::arg("eps"), py::arg("training"), py::arg("stride"), py::arg("pad"), py::arg("pool"),
-        py::arg("relu"), py::arg("residual"), py::arg("x_amax") = py::none(), py::arg("w_amax") = py::none());
+        py::arg("relu"), py::arg("residual"), py::arg("x_amax") = py::none(), py::arg("w_amax") = py::none(),
+        py::arg("res_y") = py::none(), py::arg("res_stats") = py::none(), py::arg("defer_apply") = false,
+        "fused conv + BN [+ residual] [+ ReLU] [+ 2x2 max-pool] forward; returns (out, y, stats, x_saved, out_amax, "
+        "x_amax, w_amax, relu_mask). defer_apply: statistics only, out a shape-only placeholder; res_y / res_stats: "
+        "the residual as such a deferred branch's raw output and stats, normalized inside this block's apply pass");
   m.def("act_max", &act_max_of, py::arg("t"),
         "f16x2 engine: an activation's per-image / per-channel |max| slots by the standalone pass (int32 [N + "
         "copies * C], float bits; undefined tensor for other engines)");

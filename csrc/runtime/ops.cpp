@@ -1288,11 +1288,14 @@ std::vector<at::Tensor> conv_bn_act_fwd(const at::Tensor& x, const at::Tensor& w
                                         double eps, bool training, int64_t stride, int64_t pad, bool pool, bool relu,
                                         const c10::optional<at::Tensor>& residual,
                                         const c10::optional<at::Tensor>& x_amax,
-                                        const c10::optional<at::Tensor>& w_amax) {
+                                        const c10::optional<at::Tensor>& w_amax,
+                                        const c10::optional<at::Tensor>& res_y,
+                                        const c10::optional<at::Tensor>& res_stats, bool defer_apply) {
   // RGB stem (3x3 / stride 1 / pad 1, Cin <= 4, training BN): one exact-fp32 MFMA kernel reading
   // the raw NHWC input, no channel padding, no operand scales (stem.hip)
+  const bool lazy_res = res_y.has_value() && res_y->defined();
   if (stem_enabled() && stem_ok((int)x.size(1), (int)w.size(2), (int)w.size(3), stride, pad, (int)w.size(0)) &&
-      training && !(residual.has_value() && residual->defined()))
+      training && !(residual.has_value() && residual->defined()) && !lazy_res && !defer_apply)
     return stem_bn_act_fwd(x, w, b, gamma, beta, running_mean, running_var, num_batches_tracked, momentum, eps, pool,
                            relu);
   // other stems: zero-pad 3 -> 4 channels so the float4 gather path runs (the padded input is what
@@ -1315,7 +1318,8 @@ std::vector<at::Tensor> conv_bn_act_fwd(const at::Tensor& x, const at::Tensor& w
   auto opts = y.options();
   at::Tensor stats = at::empty({4, C}, opts);
   hipStream_t st = cur_stream();
-  const bool has_res = residual.has_value() && residual->defined();
+  const bool has_res = (residual.has_value() && residual->defined()) || lazy_res;
+  TORCH_CHECK(!(lazy_res && residual.has_value() && residual->defined()), "conv_bn_act_fwd: residual or res_y, not both");
   // few statistics partials (the deep layers): finalize and apply in one launch (bn_fin_act_kernel)
   bool fused_fin = false;
   int nparts = 0, rpp = 0;
@@ -1327,7 +1331,7 @@ std::vector<at::Tensor> conv_bn_act_fwd(const at::Tensor& x, const at::Tensor& w
       TORCH_CHECK(num_batches_tracked->scalar_type() == at::kLong, "num_batches_tracked must be int64");
       nbt = reinterpret_cast<long long*>(num_batches_tracked->data_ptr<int64_t>());
     }
-    fused_fin = bn_fin_enabled() && bn_fin_act_ok(nparts, C, has_res);
+    fused_fin = bn_fin_enabled() && bn_fin_act_ok(nparts, C, has_res) && !defer_apply;
     if (!fused_fin)
       bn_finalize_launch(r[1].data_ptr<float>(), nparts, rpp, N * H * W, C, fptr(gamma), fptr(beta),
                          fptr_mut(running_mean), fptr_mut(running_var), nbt, (float)momentum, (float)eps,
@@ -1337,10 +1341,28 @@ std::vector<at::Tensor> conv_bn_act_fwd(const at::Tensor& x, const at::Tensor& w
     bn_eval_stats_launch(C, fptr(gamma), fptr(beta), running_mean->data_ptr<float>(), running_var->data_ptr<float>(),
                          (float)eps, stats.data_ptr<float>(), st);
   }
-  at::Tensor res;
+  if (defer_apply) {
+    // statistics only: the consumer applies this BatchNorm itself (a downsample branch, added inside
+    // the residual block's apply pass through res_y / res_stats). `out` is a shape-only placeholder
+    // for autograd (one element, expanded): nothing may read it.
+    TORCH_CHECK(!pool && !relu && !has_res, "conv_bn_act_fwd: defer_apply is for a plain BatchNorm (no pool, "
+                                            "activation or residual)");
+    at::Tensor ph = at::empty({1}, opts).expand({N, C, H, W});
+    return {ph, y, stats, xin, at::Tensor(), xa, wa, at::Tensor()};
+  }
+  at::Tensor res, ry, rst;
   if (has_res) {
     TORCH_CHECK(!pool, "residual + pool not supported");
-    res = nhwc(*residual);
+    if (lazy_res) {
+      ry = nhwc(*res_y);
+      TORCH_CHECK(res_stats.has_value() && res_stats->defined() && res_stats->numel() == 4 * C &&
+                      res_stats->is_contiguous() && ry.size(0) == N && ry.size(1) == C && ry.size(2) == H &&
+                      ry.size(3) == W,
+                  "conv_bn_act_fwd: res_y must match the output and res_stats be its [4, C] stats block");
+      rst = *res_stats;
+    } else {
+      res = nhwc(*residual);
+    }
   }
   at::Tensor out = at::empty({N, C, pool ? H / 2 : H, pool ? W / 2 : W},
                              opts.memory_format(at::MemoryFormat::ChannelsLast));
@@ -1368,7 +1390,8 @@ std::vector<at::Tensor> conv_bn_act_fwd(const at::Tensor& x, const at::Tensor& w
   if (!(fused_fin && exp_skip_bn_apply()) && !fused_fin)
     bn_act_fwd_launch(y.data_ptr<float>(), stats.data_ptr<float>(), res.defined() ? res.data_ptr<float>() : nullptr,
                       out.data_ptr<float>(), N, H, W, C, pool, relu, st, am,
-                      rmask.defined() ? rmask.data_ptr<uint8_t>() : nullptr);
+                      rmask.defined() ? rmask.data_ptr<uint8_t>() : nullptr, ry.defined() ? ry.data_ptr<float>() : nullptr,
+                      rst.defined() ? rst.data_ptr<float>() : nullptr);
   return {out, y, stats, xin, out_amax, xa, wa, rmask};
 }
 

@@ -39,7 +39,10 @@ std::vector<at::Tensor> conv_bn_act_fwd(const at::Tensor& x, const at::Tensor& w
                                         double eps, bool training, int64_t stride, int64_t pad, bool pool, bool relu,
                                         const c10::optional<at::Tensor>& residual,
                                         const c10::optional<at::Tensor>& x_amax = c10::nullopt,
-                                        const c10::optional<at::Tensor>& w_amax = c10::nullopt);
+                                        const c10::optional<at::Tensor>& w_amax = c10::nullopt,
+                                        const c10::optional<at::Tensor>& res_y = c10::nullopt,
+                                        const c10::optional<at::Tensor>& res_stats = c10::nullopt,
+                                        bool defer_apply = false);
 at::Tensor act_max_of(const at::Tensor& t);
 int64_t act_max_memsets();
 int64_t act_max_copies();
