@@ -9,6 +9,7 @@
 //   RandomCrop(32,4)+HFlip+Normalize    /root/reference/src/Part 1/main.py:82-93
 //   torch.mean(torch.stack(inputs), 0)  /root/reference/src/Part 2a/main.py:122
 #include <algorithm>
+#include <stdexcept>
 
 #include "act_max.h"
 #include "common.h"
@@ -735,18 +736,22 @@ __global__ __launch_bounds__(256) void avgpool_bwd_kernel(const float* __restric
 // MaxPool2d(k, s, p) forward on NHWC with int32 argmax (flat h*W+w), and backward (scatter-add).
 // Max-pool on NHWC, float4 along C. The argmax is kept as the window-local tap index (uint8,
 // first max wins in (dh, dw) scan order like ATen), a quarter of an int32 index map.
+// 32-bit indices with multiply-shift division (the launchers check the sizes): the 64-bit divisions
+// the index decode took before were ~40 instructions each, four per element, in passes that are
+// otherwise bandwidth-bound
 __global__ __launch_bounds__(256) void maxpool_fwd_kernel(const float* __restrict__ x, int N, int H, int W, int C,
                                                           int k, int s, int pd, int Ho, int Wo, float* __restrict__ y,
-                                                          unsigned char* __restrict__ arg) {
+                                                          unsigned char* __restrict__ arg, FastDiv fd_C4, FastDiv fd_Wo,
+                                                          FastDiv fd_Ho) {
   const int C4 = C >> 2;
-  const long long total = (long long)N * Ho * Wo * C4;
-  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long long)gridDim.x * blockDim.x) {
-    const int c4 = (int)(i % C4);
-    const long long pix = i / C4;
-    const int wo = (int)(pix % Wo);
-    const long long t = pix / Wo;
-    const int ho = (int)(t % Ho);
-    const int n = (int)(t / Ho);
+  const int total = N * Ho * Wo * C4;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+    const int pix = fdiv(i, fd_C4);
+    const int c4 = i - pix * C4;
+    const int t = fdiv(pix, fd_Wo);
+    const int wo = pix - t * Wo;
+    const int n = fdiv(t, fd_Ho);
+    const int ho = t - n * Ho;
     float m[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
     int am[4] = {-1, -1, -1, -1};
     const float* base = x + (long long)n * H * W * C + 4 * c4;
@@ -767,8 +772,8 @@ __global__ __launch_bounds__(256) void maxpool_fwd_kernel(const float* __restric
           }
       }
     }
-    st4(y + pix * C + 4 * c4, make_float4(m[0], m[1], m[2], m[3]));
-    *reinterpret_cast<uchar4*>(arg + pix * C + 4 * c4) =
+    st4(y + (long long)pix * C + 4 * c4, make_float4(m[0], m[1], m[2], m[3]));
+    *reinterpret_cast<uchar4*>(arg + (long long)pix * C + 4 * c4) =
         make_uchar4((unsigned char)am[0], (unsigned char)am[1], (unsigned char)am[2], (unsigned char)am[3]);
   }
 }
@@ -778,16 +783,17 @@ __global__ __launch_bounds__(256) void maxpool_fwd_kernel(const float* __restric
 __global__ __launch_bounds__(256) void maxpool_bwd_kernel(const float* __restrict__ gy,
                                                           const unsigned char* __restrict__ arg, int N, int H, int W,
                                                           int C, int k, int s, int pd, int Ho, int Wo,
-                                                          float* __restrict__ gx) {
+                                                          float* __restrict__ gx, FastDiv fd_C4, FastDiv fd_W,
+                                                          FastDiv fd_H) {
   const int C4 = C >> 2;
-  const long long total = (long long)N * H * W * C4;
-  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long long)gridDim.x * blockDim.x) {
-    const int c4 = (int)(i % C4);
-    const long long pix = i / C4;
-    const int w = (int)(pix % W);
-    const long long t = pix / W;
-    const int h = (int)(t % H);
-    const int n = (int)(t / H);
+  const int total = N * H * W * C4;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+    const int pix = fdiv(i, fd_C4);
+    const int c4 = i - pix * C4;
+    const int t = fdiv(pix, fd_W);
+    const int w = pix - t * W;
+    const int n = fdiv(t, fd_H);
+    const int h = t - n * H;
     // windows ho with ho*s - pd <= h <= ho*s - pd + k - 1
     const int ho0 = max(0, (h + pd - k + s) / s), ho1 = min(Ho - 1, (h + pd) / s);
     const int wo0 = max(0, (w + pd - k + s) / s), wo1 = min(Wo - 1, (w + pd) / s);
@@ -803,7 +809,7 @@ __global__ __launch_bounds__(256) void maxpool_bwd_kernel(const float* __restric
         if (a.z == tap) g[2] += v.z;
         if (a.w == tap) g[3] += v.w;
       }
-    st4(gx + pix * C + 4 * c4, make_float4(g[0], g[1], g[2], g[3]));
+    st4(gx + (long long)pix * C + 4 * c4, make_float4(g[0], g[1], g[2], g[3]));
   }
 }
 
@@ -937,13 +943,15 @@ void avgpool_bwd_launch(const float* gy, int N, int HW, int C, float* gx, hipStr
 }
 void maxpool_fwd_launch(const float* x, int N, int H, int W, int C, int k, int s, int p, int Ho, int Wo, float* y,
                         unsigned char* arg, hipStream_t st) {
+  if ((long long)N * H * W * (C / 4) >= (1LL << 31)) throw std::runtime_error("maxpool: tensor too large");
   hipLaunchKernelGGL(maxpool_fwd_kernel, dim3(grid_for((long long)N * Ho * Wo * (C / 4))), dim3(256), 0, st, x, N,
-                     H, W, C, k, s, p, Ho, Wo, y, arg);
+                     H, W, C, k, s, p, Ho, Wo, y, arg, make_fastdiv(C / 4), make_fastdiv(Wo), make_fastdiv(Ho));
 }
 void maxpool_bwd_launch(const float* gy, const unsigned char* arg, int N, int H, int W, int C, int k, int s, int p,
                         int Ho, int Wo, float* gx, hipStream_t st) {
+  if ((long long)N * H * W * (C / 4) >= (1LL << 31)) throw std::runtime_error("maxpool: tensor too large");
   hipLaunchKernelGGL(maxpool_bwd_kernel, dim3(grid_for((long long)N * H * W * (C / 4))), dim3(256), 0, st, gy, arg,
-                     N, H, W, C, k, s, p, Ho, Wo, gx);
+                     N, H, W, C, k, s, p, Ho, Wo, gx, make_fastdiv(C / 4), make_fastdiv(W), make_fastdiv(H));
 }
 
 void wtrans_sub_launch(const float* w, float* wt, int Co, int KH, int KW, int Ci, int kh0, int kw0, int nkh, int nkw,
