@@ -140,17 +140,28 @@ constexpr int FIN_MAXP16 = 512;    // forward, 16-channel blocks (16 merge threa
 // A fused-finalize block's row r (pooled window or pixel) of y: the 2x2 window's four pixels (pool)
 // or the pixel in v[0], channels n0..n0+3.
 constexpr int kFinRPT = 4;  // rows per thread loaded before the statistics merge
-__device__ __forceinline__ long long fin_row_off(long long r, int pool, int H, int W, int Ho, int Wo, int C, int n0) {
+// (pooled) pixel index -> (n, ho, wo) by multiply-shift division (32-bit indices: the launchers'
+// tensors stay below 2^31 pooled pixels); 64-bit '/' and '%' here cost ~40 instructions each per row
+struct PoolDiv {
+  FastDiv wo, ho;
+};
+inline PoolDiv make_pooldiv(int Wo, int Ho) { return PoolDiv{make_fastdiv(Wo), make_fastdiv(Ho)}; }
+__device__ __forceinline__ void pool_decode(int r, int Wo, int Ho, const PoolDiv& pd, int& n, int& ho, int& wo) {
+  const int t = fdiv(r, pd.wo);
+  wo = r - t * Wo;
+  n = fdiv(t, pd.ho);
+  ho = t - n * Ho;
+}
+__device__ __forceinline__ long long fin_row_off(long long r, int pool, int H, int W, int Ho, int Wo, int C, int n0,
+                                                 const PoolDiv& pd) {
   if (!pool) return r * C + n0;
-  const int wo = (int)(r % Wo);
-  const long long t = r / Wo;
-  const int ho = (int)(t % Ho);
-  const int n = (int)(t / Ho);
+  int n, ho, wo;
+  pool_decode((int)r, Wo, Ho, pd, n, ho, wo);
   return (((long long)n * H + 2 * ho) * W + 2 * wo) * C + n0;
 }
 __device__ __forceinline__ void fin_load_row(const float* __restrict__ y, float4 (&v)[4], long long r, int pool, int H,
-                                             int W, int Ho, int Wo, int C, int n0) {
-  const float* b = y + fin_row_off(r, pool, H, W, Ho, Wo, C, n0);
+                                             int W, int Ho, int Wo, int C, int n0, const PoolDiv& pd) {
+  const float* b = y + fin_row_off(r, pool, H, W, Ho, Wo, C, n0, pd);
   v[0] = ld4(b);
   if (pool) {
     v[1] = ld4(b + C);
@@ -161,11 +172,11 @@ __device__ __forceinline__ void fin_load_row(const float* __restrict__ y, float4
 // rows ra, ra + rs, ... (the first kFinRPT of this thread); rows past r1 load row 0 (unused)
 __device__ __forceinline__ void fin_prefetch(const float* __restrict__ y, float4 (&pv)[kFinRPT][4], long long ra,
                                              long long r1, int pool, int H, int W, int Ho, int Wo, int C, int n0,
-                                             int rs = 16) {
+                                             const PoolDiv& pd, int rs = 16) {
 #pragma unroll
   for (int i = 0; i < kFinRPT; ++i) {
     const long long r = ra + rs * i;
-    fin_load_row(y, pv[i], r < r1 ? r : 0, pool, H, W, Ho, Wo, C, n0);
+    fin_load_row(y, pv[i], r < r1 ? r : 0, pool, H, W, Ho, Wo, C, n0, pd);
   }
 }
 // CG channels per block: 64 (4 merge threads per channel) or 16 (16 merge threads per channel: a
@@ -178,7 +189,7 @@ __global__ __launch_bounds__(256) void bn_fin_act_kernel(const float* __restrict
                                                          float eps, float* __restrict__ stats,
                                                          const float* __restrict__ y, float* __restrict__ out, int N,
                                                          int H, int W, int pool, int relu, int chunks, FastDiv fd_HWo,
-                                                         ActMaxOut am) {
+                                                         ActMaxOut am, PoolDiv pd) {
   constexpr int TQ = 256 / CG;  // merge threads per channel
   constexpr int CQ = CG / 4;    // phase 2: channel quads x RL row lanes
   constexpr int RL = 256 / CQ;
@@ -202,7 +213,7 @@ __global__ __launch_bounds__(256) void bn_fin_act_kernel(const float* __restrict
   const long long r0 = (long long)chunk * per, r1 = min(rows, r0 + per);
   const int img0 = fdiv((int)min(r0, rows - 1), fd_HWo);
   float4 pv[kFinRPT][4];
-  fin_prefetch(y, pv, r0 + rl, r1, pool, H, W, Ho, Wo, C, n0, RL);
+  fin_prefetch(y, pv, r0 + rl, r1, pool, H, W, Ho, Wo, C, n0, pd, RL);
   // phase 1: thread (ch, q) merges partials b = q + TQ k -- one batch of buffer loads
   // (only the batches of 8 loads that hold partials are issued: kp = ceil(nparts / TQ) rounded up to 8)
   constexpr int KP = (CG == 16 ? FIN_MAXP16 : FIN_MAXP) / TQ;
@@ -299,7 +310,7 @@ __global__ __launch_bounds__(256) void bn_fin_act_kernel(const float* __restrict
     if (r0 + rl + RL * i < r1) emit(r0 + rl + RL * i, pv[i]);
   for (long long r = r0 + rl + RL * kFinRPT; r < r1; r += RL) {
     float4 v[4];
-    fin_load_row(y, v, r, pool, H, W, Ho, Wo, C, n0);
+    fin_load_row(y, v, r, pool, H, W, Ho, Wo, C, n0, pd);
     emit(r, v);
   }
   if (want) {
@@ -322,7 +333,7 @@ __global__ __launch_bounds__(256) void bn_act_fwd_kernel(const float* __restrict
                                                          int qmode, FastDiv fd_C4, FastDiv fd_HWo, ActMaxOut am,
                                                          unsigned char* __restrict__ rmask,
                                                          const float* __restrict__ res_y,
-                                                         const float* __restrict__ res_st) {
+                                                         const float* __restrict__ res_st, PoolDiv pd) {
   __shared__ ActMaxBlock<kMaxActC> sam;
   const int C4 = C >> 2;
   const int Ho = pool ? H / 2 : H, Wo = pool ? W / 2 : W;
@@ -361,10 +372,8 @@ __global__ __launch_bounds__(256) void bn_act_fwd_kernel(const float* __restrict
       if (rmask)  // the ReLU's pass mask for the backward (1 byte per float4 instead of re-reading out)
         rmask[i] = (unsigned char)((z.x > 0.f ? 1 : 0) | (z.y > 0.f ? 2 : 0) | (z.z > 0.f ? 4 : 0) | (z.w > 0.f ? 8 : 0));
     } else {
-      const int wo = pix % Wo;
-      const int t = pix / Wo;
-      const int ho = t % Ho;
-      const int n = t / Ho;
+      int n, ho, wo;
+      pool_decode(pix, Wo, Ho, pd, n, ho, wo);
       const float* base = y + (((long long)n * H + 2 * ho) * W + 2 * wo) * C + 4 * c4;
       const float4 z0 = affine_act(ld4(base), sc, sh, relu);
       const float4 z1 = affine_act(ld4(base + C), sc, sh, relu);
@@ -428,7 +437,7 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const float* __restr
                                                             const float* __restrict__ stats, float* __restrict__ part,
                                                             int N, int H, int W, int C, int pool, int relu,
                                                             const float* __restrict__ zout,
-                                                            const unsigned char* __restrict__ rmask) {
+                                                            const unsigned char* __restrict__ rmask, PoolDiv pd) {
   __shared__ float4 red1[256], red2[256], red3[PS == 3 ? 256 : 1];
   const int C4 = C >> 2;
   const int tid = threadIdx.x;
@@ -466,10 +475,8 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const float* __restr
             if (e == 3) { a1.w += dz; a2.w += dz * xh; a3.w += xh; }
           }
         } else {
-          const int wo = (int)(px % Wo);
-          const long long t = px / Wo;
-          const int ho = (int)(t % Ho);
-          const int n = (int)(t / Ho);
+          int n, ho, wo;
+          pool_decode((int)px, Wo, Ho, pd, n, ho, wo);
           const float* base = y + (((long long)n * H + 2 * ho) * W + 2 * wo) * C + 4 * cq;
           const float4 y0 = ld4(base), y1 = ld4(base + C), y2 = ld4(base + (long long)W * C),
                        y3 = ld4(base + (long long)W * C + C);
@@ -599,7 +606,8 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const float* __restri
                                                            float* __restrict__ dbias_part, int N, int H, int W,
                                                            int C, int pool, int relu, const float* __restrict__ zout,
                                                            float* __restrict__ dres, FastDiv fd_IMG, FastDiv fd_HW,
-                                                           ActMaxOut am, const unsigned char* __restrict__ rmask) {
+                                                           ActMaxOut am, const unsigned char* __restrict__ rmask,
+                                                           PoolDiv pd) {
   __shared__ float4 red[256];
   __shared__ ActMaxBlock<kMaxActC> sam;
   const bool want = am.img != nullptr;
@@ -672,10 +680,8 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const float* __restri
           if (dres) st4(dres + px * C + 4 * cq, dz);
           emit(px * C + 4 * cq, yv, dz);
         } else {
-          const int wo = (int)(px % Wo);
-          const long long t = px / Wo;
-          const int ho = (int)(t % Ho);
-          const int n = (int)(t / Ho);
+          int n, ho, wo;
+          pool_decode((int)px, Wo, Ho, pd, n, ho, wo);
           const long long o0 = (((long long)n * H + 2 * ho) * W + 2 * wo) * C + 4 * cq;
           const long long o1 = o0 + C, o2 = o0 + (long long)W * C, o3 = o2 + C;
           const float4 y0 = ld4(y + o0), y1 = ld4(y + o1), y2 = ld4(y + o2), y3 = ld4(y + o3);
@@ -741,7 +747,7 @@ __global__ __launch_bounds__(256) void bn_bwd_fin_apply_kernel(
     const float* __restrict__ part, int nparts, int PS, const float* __restrict__ y,
     const float* __restrict__ gout, const float* __restrict__ stats, float* __restrict__ dy, float* gbeta,
     float* ggamma, float* gdb, int N, int H, int W, int C, int pool, int relu, int chunks, FastDiv fd_HWo,
-    ActMaxOut am) {
+    ActMaxOut am, PoolDiv pd) {
   __shared__ double red[3][4][64];
   __shared__ float s_k1[64], s_k2[64];
   __shared__ ActMaxBlock<64> sam;  // per-image / per-channel |max| of the block's dy
@@ -763,7 +769,7 @@ __global__ __launch_bounds__(256) void bn_bwd_fin_apply_kernel(
   const long long r0 = (long long)chunk * per, r1 = min(rows, r0 + per);
   const int img0 = fdiv((int)min(r0, rows - 1), fd_HWo);
   float4 pv[kFinRPT][4], pg[kFinRPT];
-  fin_prefetch(y, pv, r0 + rl, r1, pool, H, W, Ho, Wo, C, n0);
+  fin_prefetch(y, pv, r0 + rl, r1, pool, H, W, Ho, Wo, C, n0, pd);
 #pragma unroll
   for (int i = 0; i < kFinRPT; ++i) {
     const long long r = r0 + rl + 16 * i;
@@ -854,7 +860,7 @@ __global__ __launch_bounds__(256) void bn_bwd_fin_apply_kernel(
       dz.w = (!relu || z.w > 0.f) ? g.w : 0.f;
       emit(r * C + n0, yv, dz);
     } else {
-      const long long o0 = fin_row_off(r, pool, H, W, Ho, Wo, C, n0);
+      const long long o0 = fin_row_off(r, pool, H, W, Ho, Wo, C, n0, pd);
       const long long o1 = o0 + C, o2 = o0 + (long long)W * C, o3 = o2 + C;
       const float4 y0 = v[0], y1 = v[1], y2 = v[2], y3 = v[3];
       const float4 z0 = affine_act(y0, sc, sh, relu), z1 = affine_act(y1, sc, sh, relu),
@@ -880,7 +886,7 @@ __global__ __launch_bounds__(256) void bn_bwd_fin_apply_kernel(
     if (r0 + rl + 16 * i < r1) row(r0 + rl + 16 * i, pv[i], pg[i]);
   for (long long r = r0 + rl + 16 * kFinRPT; r < r1; r += 16) {
     float4 v[4];
-    fin_load_row(y, v, r, pool, H, W, Ho, Wo, C, n0);
+    fin_load_row(y, v, r, pool, H, W, Ho, Wo, C, n0, pd);
     row(r, v, ld4(gout + r * C + n0));
   }
   if (want) {
@@ -1036,7 +1042,7 @@ void bn_fin_act_launch(const float* part, int nparts, int rpp, int C, const floa
   hipLaunchKernelGGL(cg == 64 ? bn_fin_act_kernel<64> : bn_fin_act_kernel<16>, dim3(grid), dim3(256), 0, st, part,
                      exp_merge_parts(nparts), rpp, M, C, gamma, beta, running_mean, running_var, nbt, momentum, eps, stats, y, out, N,
                      H, W, pool ? 1 : 0, relu ? 1 : 0, grid / (C / cg),
-                     make_fastdiv(out_pixels_per_image(H, W, pool)), am);
+                     make_fastdiv(out_pixels_per_image(H, W, pool)), am, make_pooldiv(W / 2, H / 2));
 }
 
 bool bn_bwd_fin_apply_ok(int nparts, int C, int H, int W, bool pool) {
@@ -1049,7 +1055,7 @@ void bn_bwd_fin_apply_launch(const float* part, int nparts, int ps, const float*
   const int grid = bn_fin_act_grid(N, H, W, C, pool);
   hipLaunchKernelGGL(bn_bwd_fin_apply_kernel, dim3(grid), dim3(256), 0, st, part, exp_merge_parts(nparts), ps, y, gout, stats, dy,
                      gbeta, ggamma, gdb, N, H, W, C, pool ? 1 : 0, relu ? 1 : 0, grid / (C / 64),
-                     make_fastdiv(out_pixels_per_image(H, W, pool)), am);
+                     make_fastdiv(out_pixels_per_image(H, W, pool)), am, make_pooldiv(W / 2, H / 2));
 }
 
 int bn_act_grid(int N, int H, int W, int C, bool pool) {
@@ -1068,7 +1074,8 @@ void bn_act_fwd_launch(const float* y, const float* stats, const float* res, flo
   const long long per = std::max(unit, ((total + blocks - 1) / blocks + unit - 1) / unit * unit);
   hipLaunchKernelGGL(bn_act_fwd_kernel, dim3((unsigned)((total + per - 1) / per)), dim3(256), 0, st, y, stats, res,
                      out, N, H, W, C, pool ? 1 : 0, relu ? 1 : 0, (int)per, qmode, make_fastdiv(C4),
-                     make_fastdiv(out_pixels_per_image(H, W, pool)), am, pool ? nullptr : rmask, res_y, res_st);
+                     make_fastdiv(out_pixels_per_image(H, W, pool)), am, pool ? nullptr : rmask, res_y, res_st,
+                     make_pooldiv(W / 2, H / 2));
 }
 
 void bn_bwd_reduce_launch(const float* y, const float* gout, const float* stats, float* part, int nblocks, int N,
@@ -1076,10 +1083,10 @@ void bn_bwd_reduce_launch(const float* y, const float* gout, const float* stats,
                           bool with_xsum, const unsigned char* rmask) {
   if (with_xsum)
     hipLaunchKernelGGL(bn_bwd_reduce_kernel<3>, dim3(nblocks), dim3(256), 0, st, y, gout, stats, part, N, H, W, C,
-                       pool ? 1 : 0, relu ? 1 : 0, zout, rmask);
+                       pool ? 1 : 0, relu ? 1 : 0, zout, rmask, make_pooldiv(W / 2, H / 2));
   else
     hipLaunchKernelGGL(bn_bwd_reduce_kernel<2>, dim3(nblocks), dim3(256), 0, st, y, gout, stats, part, N, H, W, C,
-                       pool ? 1 : 0, relu ? 1 : 0, zout, rmask);
+                       pool ? 1 : 0, relu ? 1 : 0, zout, rmask, make_pooldiv(W / 2, H / 2));
 }
 
 void chan_finalize_launch(const float* part, int nparts, int C, float* out, float* g0, float* g1, bool accumulate,
@@ -1097,7 +1104,7 @@ void bn_bwd_apply_launch(const float* y, const float* gout, const float* stats, 
                          const float* zout, float* dres, hipStream_t st, ActMaxOut am, const unsigned char* rmask) {
   hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(nblocks), dim3(256), 0, st, y, gout, stats, sums, dy, dbias_part, N,
                      H, W, C, pool ? 1 : 0, relu ? 1 : 0, zout, dres, make_fastdiv(out_pixels_per_image(H, W, pool)),
-                     make_fastdiv(H * W), am, rmask);
+                     make_fastdiv(H * W), am, rmask, make_pooldiv(W / 2, H / 2));
 }
 
 }  // namespace cdp

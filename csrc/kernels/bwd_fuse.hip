@@ -139,10 +139,10 @@ __global__ __launch_bounds__(256) void bwd_reduce_kernel(BwdReduceArgs a) {
             f4add(a3, e, xh);
           }
         } else {
-          const int wo = m % Wo;
-          const int t = m / Wo;
-          const int ho = t % Ho;
-          const int nn = t / Ho;
+          const int t = fdiv(m, a.bn_fd_wo);
+          const int wo = m - t * Wo;
+          const int nn = fdiv(t, a.bn_fd_ho);
+          const int ho = t - nn * Ho;
           const float* base = a.bn_y + (((long long)nn * H + 2 * ho) * W + 2 * wo) * C + n;
           const float4 v0 = ld4(base), v1 = ld4(base + C), v2 = ld4(base + (long long)W * C),
                        v3 = ld4(base + (long long)W * C + C);
@@ -223,6 +223,10 @@ __global__ __launch_bounds__(256) void bwd_reduce_kernel(BwdReduceArgs a) {
 int bwd_reduce_rows_per_part() { return RBD; }
 
 void bwd_reduce_launch(BwdReduceArgs a, hipStream_t st) {
+  if (a.bn_part && a.bn_pool) {
+    a.bn_fd_wo = make_fastdiv(a.bn_W / 2);
+    a.bn_fd_ho = make_fastdiv(a.bn_H / 2);
+  }
   a.nbd = 0;
   a.d_nbx = 0;
   if (a.d_slab) {

@@ -201,6 +201,7 @@ struct BwdReduceArgs {
   const float* bn_stats;
   float* bn_part;
   int bn_H, bn_W, bn_pool, bn_relu, bn_ps;
+  FastDiv bn_fd_wo, bn_fd_ho;  // pooled width / height divisors (set by bwd_reduce_launch)
   // job W: w_dst[i] = sum_z w_slab[z][i] over w_n4 float4s
   const float4* w_slab;
   float4* w_dst;
