@@ -710,25 +710,27 @@ __global__ __launch_bounds__(256) void small_linear_bwd_kernel(const float* __re
   }
 }
 
-// global average pool over HW of NHWC -> [N][C]; and its backward
+// global average pool over HW of NHWC -> [N][C]; and its backward (32-bit index decode by
+// multiply-shift: the launchers check the sizes)
 __global__ __launch_bounds__(256) void avgpool_fwd_kernel(const float* __restrict__ x, int N, int HW, int C,
-                                                          float* __restrict__ y) {
-  const long long total = (long long)N * C;
-  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long long)gridDim.x * blockDim.x) {
-    const int c = (int)(i % C);
-    const long long n = i / C;
+                                                          float* __restrict__ y, FastDiv fd_C) {
+  const int total = N * C;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+    const int n = fdiv(i, fd_C);
+    const int c = i - n * C;
     float s = 0.f;
-    for (int k = 0; k < HW; ++k) s += x[(n * HW + k) * C + c];
+    for (int k = 0; k < HW; ++k) s += x[((long long)n * HW + k) * C + c];
     y[i] = s / (float)HW;
   }
 }
 __global__ __launch_bounds__(256) void avgpool_bwd_kernel(const float* __restrict__ gy, int N, int HW, int C,
-                                                          float* __restrict__ gx) {
-  const long long total = (long long)N * HW * C;
+                                                          float* __restrict__ gx, FastDiv fd_C, FastDiv fd_HW) {
+  const int total = N * HW * C;
   const float inv = 1.f / (float)HW;
-  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long long)gridDim.x * blockDim.x) {
-    const int c = (int)(i % C);
-    const long long n = i / ((long long)HW * C);
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+    const int pix = fdiv(i, fd_C);
+    const int c = i - pix * C;
+    const int n = fdiv(pix, fd_HW);
     gx[i] = gy[n * C + c] * inv;
   }
 }
@@ -936,10 +938,14 @@ void small_linear_bwd_launch(const float* dy, const float* x, const float* w, in
                      nbx, nbw);
 }
 void avgpool_fwd_launch(const float* x, int N, int HW, int C, float* y, hipStream_t st) {
-  hipLaunchKernelGGL(avgpool_fwd_kernel, dim3(grid_for((long long)N * C)), dim3(256), 0, st, x, N, HW, C, y);
+  if ((long long)N * HW * C >= (1LL << 31)) throw std::runtime_error("avgpool: tensor too large");
+  hipLaunchKernelGGL(avgpool_fwd_kernel, dim3(grid_for((long long)N * C)), dim3(256), 0, st, x, N, HW, C, y,
+                     make_fastdiv(C));
 }
 void avgpool_bwd_launch(const float* gy, int N, int HW, int C, float* gx, hipStream_t st) {
-  hipLaunchKernelGGL(avgpool_bwd_kernel, dim3(grid_for((long long)N * HW * C)), dim3(256), 0, st, gy, N, HW, C, gx);
+  if ((long long)N * HW * C >= (1LL << 31)) throw std::runtime_error("avgpool: tensor too large");
+  hipLaunchKernelGGL(avgpool_bwd_kernel, dim3(grid_for((long long)N * HW * C)), dim3(256), 0, st, gy, N, HW, C, gx,
+                     make_fastdiv(C), make_fastdiv(HW));
 }
 void maxpool_fwd_launch(const float* x, int N, int H, int W, int C, int k, int s, int p, int Ho, int Wo, float* y,
                         unsigned char* arg, hipStream_t st) {
