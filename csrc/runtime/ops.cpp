@@ -100,7 +100,8 @@ int split_planes() { return conv_gemm_mode() == 2 ? 1 : conv_gemm_mode() == 3 ? 
 // Everything is ordered on the current stream, like the caching allocator's reuse; a chunk taken up
 // on another stream than its last user's (its memset, or slots still being read) first makes the
 // new stream wait for that one.
-constexpr long long kSlotChunk = 1LL << 20;  // int32 slots per chunk (4 MB: one memset per ResNet-50 step)
+constexpr long long kSlotChunk = 1LL << 16;     // int32 slots per eager chunk (256 KB)
+constexpr long long kCapSlotChunk = 1LL << 18;  // ... per captured chunk (1 MB: one memset node for a VGG-11 step)
 struct SlotPool {
   std::vector<at::Tensor> ring;
   std::vector<long long> used;
@@ -110,6 +111,7 @@ struct SlotPool {
   unsigned long long cap_id = 0;
   at::Tensor cap_cur;
   long long cap_used = 0;
+  long long cap_total = 0, cap_hint = 0;  // slots taken by the current / largest earlier capture
   std::vector<at::Tensor> cap_keep;
 };
 
@@ -135,12 +137,19 @@ at::Tensor alloc_slots(long long n, const at::Tensor& like, hipStream_t st) {
   unsigned long long id = 0;
   TORCH_CHECK(hipStreamGetCaptureInfo(st, &cs, &id) == hipSuccess, "act max slots: capture query failed");
   if (cs == hipStreamCaptureStatusActive) {
+    // a capture's first chunk is sized by the largest earlier capture (a re-captured step takes one
+    // chunk, i.e. one captured memset of just its slots; ResNet-50 took eight 256 KB ones)
+    if (id != P.cap_id) {
+      P.cap_hint = std::max(P.cap_hint, P.cap_total);
+      P.cap_total = 0;
+    }
     if (id != P.cap_id || !P.cap_cur.defined() || P.cap_used + n > P.cap_cur.numel()) {
-      P.cap_cur = fresh(std::max(kSlotChunk, n));
+      P.cap_cur = fresh(std::max(std::max(kCapSlotChunk, n), id != P.cap_id ? P.cap_hint : 0LL));
       P.cap_keep.push_back(P.cap_cur);
       P.cap_used = 0;
       P.cap_id = id;
     }
+    P.cap_total += n;
     at::Tensor v = P.cap_cur.narrow(0, P.cap_used, n);
     P.cap_used += n;
     return v;

@@ -182,10 +182,10 @@ def test_act_max_slots_ordered_across_streams():
         pytest.skip("act max exists for the f16x2 engine only")
     K = C().act_max_copies()
     gen = torch.Generator(device="cuda").manual_seed(9)
-    # slot chunks hold 2^20 slots: 0.61 of one, twice, makes the second start a chunk of its own
-    tx = torch.randn(64, 79992, device="cuda", generator=gen)  # 64 + 8 x 79992 = 640000 slots
-    tb = torch.randn(64, 79992, device="cuda", generator=gen)  # 640000 more: a new chunk, zeroed on s1
-    tc = torch.randn(32, 37496, device="cuda", generator=gen)  # 300000 more: the same chunk, used on s2
+    # eager slot chunks hold 2^16 slots: 0.61 of one, twice, makes the second start a chunk of its own
+    tx = torch.randn(64, 4992, device="cuda", generator=gen)  # 64 + 8 x 4992 = 40000 slots
+    tb = torch.randn(64, 4992, device="cuda", generator=gen)  # 40000 more: a new chunk, zeroed on s1
+    tc = torch.randn(32, 2336, device="cuda", generator=gen)  # 18720 more: the same chunk, used on s2
     mx = C().act_max(tx)
     s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
     s1.wait_stream(torch.cuda.current_stream())
@@ -199,7 +199,7 @@ def test_act_max_slots_ordered_across_streams():
     assert torch.equal(mb[:64].view(torch.float32), tb.abs().amax(1))
     assert torch.equal(mx[:64].view(torch.float32), tx.abs().amax(1))
     assert torch.equal(mc[:32].view(torch.float32), tc.abs().amax(1))
-    assert torch.equal(mc[32:32 + K * 37496].view(torch.float32).view(K, 37496).amax(0), tc.abs().amax(0))
+    assert torch.equal(mc[32:32 + K * 2336].view(torch.float32).view(K, 2336).amax(0), tc.abs().amax(0))
 
 
 @pytest.mark.parametrize("pool", [False, True])
