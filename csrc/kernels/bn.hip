@@ -432,13 +432,16 @@ __device__ __forceinline__ float4 mask_f4(unsigned char m) {
 // and (PS == 3) of xhat itself, from which chan_finalize derives the conv-bias gradient
 // sum(dy) = -scale * sum(xhat) * sum(dz*xhat) / M without a second pass over dy.
 // Block = 256 threads; for C4 <= 256 threads split as ppb pixel lanes x C4 channel quads.
-template <int PS>
+// POOL is a template parameter: the pooled branch's four pixels per thread need ~130 VGPRs, which
+// the unpooled instantiation (most of ResNet's BN passes) would otherwise carry at half the occupancy.
+template <int PS, bool POOL>
 __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const float* __restrict__ y, const float* __restrict__ gout,
                                                             const float* __restrict__ stats, float* __restrict__ part,
-                                                            int N, int H, int W, int C, int pool, int relu,
+                                                            int N, int H, int W, int C, int relu,
                                                             const float* __restrict__ zout,
                                                             const unsigned char* __restrict__ rmask, PoolDiv pd) {
   __shared__ float4 red1[256], red2[256], red3[PS == 3 ? 256 : 1];
+  constexpr int pool = POOL ? 1 : 0;
   const int C4 = C >> 2;
   const int tid = threadIdx.x;
   const int cq_per_thread = (C4 + 255) / 256;  // 1 or 2
@@ -600,16 +603,19 @@ __global__ __launch_bounds__(256) void chan_finalize_kernel(const float* __restr
 // one pixel; for odd H/W under pooling the uncovered border gets dz = 0. Block b walks the
 // contiguous (pooled) pixel range [b * per, (b + 1) * per), per = ceil(npix / gridDim.x), and folds
 // the per-image / per-channel |max| of the dy it writes into am (act_max.h).
+// (POOL: as bn_bwd_reduce_kernel)
+template <bool POOL>
 __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const float* __restrict__ y, const float* __restrict__ gout,
                                                            const float* __restrict__ stats,
                                                            const float* __restrict__ sums, float* __restrict__ dy,
                                                            float* __restrict__ dbias_part, int N, int H, int W,
-                                                           int C, int pool, int relu, const float* __restrict__ zout,
+                                                           int C, int relu, const float* __restrict__ zout,
                                                            float* __restrict__ dres, FastDiv fd_IMG, FastDiv fd_HW,
                                                            ActMaxOut am, const unsigned char* __restrict__ rmask,
                                                            PoolDiv pd) {
   __shared__ float4 red[256];
   __shared__ ActMaxBlock<kMaxActC> sam;
+  constexpr int pool = POOL ? 1 : 0;
   const bool want = am.img != nullptr;
   if (want) {
     sam.init(threadIdx.x, 256);
@@ -1081,12 +1087,10 @@ void bn_act_fwd_launch(const float* y, const float* stats, const float* res, flo
 void bn_bwd_reduce_launch(const float* y, const float* gout, const float* stats, float* part, int nblocks, int N,
                           int H, int W, int C, bool pool, bool relu, const float* zout, hipStream_t st,
                           bool with_xsum, const unsigned char* rmask) {
-  if (with_xsum)
-    hipLaunchKernelGGL(bn_bwd_reduce_kernel<3>, dim3(nblocks), dim3(256), 0, st, y, gout, stats, part, N, H, W, C,
-                       pool ? 1 : 0, relu ? 1 : 0, zout, rmask, make_pooldiv(W / 2, H / 2));
-  else
-    hipLaunchKernelGGL(bn_bwd_reduce_kernel<2>, dim3(nblocks), dim3(256), 0, st, y, gout, stats, part, N, H, W, C,
-                       pool ? 1 : 0, relu ? 1 : 0, zout, rmask, make_pooldiv(W / 2, H / 2));
+  auto k = with_xsum ? (pool ? bn_bwd_reduce_kernel<3, true> : bn_bwd_reduce_kernel<3, false>)
+                     : (pool ? bn_bwd_reduce_kernel<2, true> : bn_bwd_reduce_kernel<2, false>);
+  hipLaunchKernelGGL(k, dim3(nblocks), dim3(256), 0, st, y, gout, stats, part, N, H, W, C, relu ? 1 : 0, zout, rmask,
+                     make_pooldiv(W / 2, H / 2));
 }
 
 void chan_finalize_launch(const float* part, int nparts, int C, float* out, float* g0, float* g1, bool accumulate,
@@ -1102,8 +1106,8 @@ void chan_finalize_launch(const float* part, int nparts, int C, float* out, floa
 void bn_bwd_apply_launch(const float* y, const float* gout, const float* stats, const float* sums, float* dy,
                          float* dbias_part, int nblocks, int N, int H, int W, int C, bool pool, bool relu,
                          const float* zout, float* dres, hipStream_t st, ActMaxOut am, const unsigned char* rmask) {
-  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(nblocks), dim3(256), 0, st, y, gout, stats, sums, dy, dbias_part, N,
-                     H, W, C, pool ? 1 : 0, relu ? 1 : 0, zout, dres, make_fastdiv(out_pixels_per_image(H, W, pool)),
+  hipLaunchKernelGGL(pool ? bn_bwd_apply_kernel<true> : bn_bwd_apply_kernel<false>, dim3(nblocks), dim3(256), 0, st,
+                     y, gout, stats, sums, dy, dbias_part, N, H, W, C, relu ? 1 : 0, zout, dres, make_fastdiv(out_pixels_per_image(H, W, pool)),
                      make_fastdiv(H * W), am, rmask, make_pooldiv(W / 2, H / 2));
 }
 
