@@ -181,15 +181,16 @@ __device__ __forceinline__ void fin_prefetch(const float* __restrict__ y, float4
 }
 // CG channels per block: 64 (4 merge threads per channel) or 16 (16 merge threads per channel: a
 // quarter of the merge work per thread, 4x the blocks repeating it)
-template <int CG>
+template <int CG, bool POOL>
 __global__ __launch_bounds__(256) void bn_fin_act_kernel(const float* __restrict__ part, int nparts, int rpp, int M,
                                                          int C, const float* __restrict__ gamma,
                                                          const float* __restrict__ beta, float* running_mean,
                                                          float* running_var, long long* nbt, float momentum,
                                                          float eps, float* __restrict__ stats,
                                                          const float* __restrict__ y, float* __restrict__ out, int N,
-                                                         int H, int W, int pool, int relu, int chunks, FastDiv fd_HWo,
+                                                         int H, int W, int relu, int chunks, FastDiv fd_HWo,
                                                          ActMaxOut am, PoolDiv pd) {
+  constexpr int pool = POOL ? 1 : 0;  // (as bn_bwd_reduce_kernel)
   constexpr int TQ = 256 / CG;  // merge threads per channel
   constexpr int CQ = CG / 4;    // phase 2: channel quads x RL row lanes
   constexpr int RL = 256 / CQ;
@@ -749,11 +750,13 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const float* __restri
 // chan_finalize_kernel); the chunk-0 blocks publish dgamma, dbeta and the conv-bias gradient; then
 // the block writes dy = scale*(dz - sum(dz)/M - xhat*sum(dz*xhat)/M) for its rows, with the
 // pool / ReLU routing recomputed from y. Training mode only (no residual, even map under pooling).
+template <bool POOL>
 __global__ __launch_bounds__(256) void bn_bwd_fin_apply_kernel(
     const float* __restrict__ part, int nparts, int PS, const float* __restrict__ y,
     const float* __restrict__ gout, const float* __restrict__ stats, float* __restrict__ dy, float* gbeta,
-    float* ggamma, float* gdb, int N, int H, int W, int C, int pool, int relu, int chunks, FastDiv fd_HWo,
+    float* ggamma, float* gdb, int N, int H, int W, int C, int relu, int chunks, FastDiv fd_HWo,
     ActMaxOut am, PoolDiv pd) {
+  constexpr int pool = POOL ? 1 : 0;
   __shared__ double red[3][4][64];
   __shared__ float s_k1[64], s_k2[64];
   __shared__ ActMaxBlock<64> sam;  // per-image / per-channel |max| of the block's dy
@@ -1045,9 +1048,11 @@ void bn_fin_act_launch(const float* part, int nparts, int rpp, int C, const floa
   const int grid = bn_fin_act_grid(N, H, W, C, pool, nparts);
   const int M = N * H * W;
   const int cg = fin_cg(nparts);
-  hipLaunchKernelGGL(cg == 64 ? bn_fin_act_kernel<64> : bn_fin_act_kernel<16>, dim3(grid), dim3(256), 0, st, part,
+  auto k = cg == 64 ? (pool ? bn_fin_act_kernel<64, true> : bn_fin_act_kernel<64, false>)
+                    : (pool ? bn_fin_act_kernel<16, true> : bn_fin_act_kernel<16, false>);
+  hipLaunchKernelGGL(k, dim3(grid), dim3(256), 0, st, part,
                      exp_merge_parts(nparts), rpp, M, C, gamma, beta, running_mean, running_var, nbt, momentum, eps, stats, y, out, N,
-                     H, W, pool ? 1 : 0, relu ? 1 : 0, grid / (C / cg),
+                     H, W, relu ? 1 : 0, grid / (C / cg),
                      make_fastdiv(out_pixels_per_image(H, W, pool)), am, make_pooldiv(W / 2, H / 2));
 }
 
@@ -1059,8 +1064,9 @@ void bn_bwd_fin_apply_launch(const float* part, int nparts, int ps, const float*
                              const float* stats, float* dy, float* gbeta, float* ggamma, float* gdb, int N, int H,
                              int W, int C, bool pool, bool relu, ActMaxOut am, hipStream_t st) {
   const int grid = bn_fin_act_grid(N, H, W, C, pool);
-  hipLaunchKernelGGL(bn_bwd_fin_apply_kernel, dim3(grid), dim3(256), 0, st, part, exp_merge_parts(nparts), ps, y, gout, stats, dy,
-                     gbeta, ggamma, gdb, N, H, W, C, pool ? 1 : 0, relu ? 1 : 0, grid / (C / 64),
+  hipLaunchKernelGGL(pool ? bn_bwd_fin_apply_kernel<true> : bn_bwd_fin_apply_kernel<false>, dim3(grid), dim3(256), 0,
+                     st, part, exp_merge_parts(nparts), ps, y, gout, stats, dy, gbeta, ggamma, gdb, N, H, W, C,
+                     relu ? 1 : 0, grid / (C / 64),
                      make_fastdiv(out_pixels_per_image(H, W, pool)), am, make_pooldiv(W / 2, H / 2));
 }
 
