@@ -336,6 +336,17 @@ def test_pooling_ops():
     yt.backward(gt)
     reft.backward(gt.double().cpu())
     assert rel_err(yt, reft) < 1e-6 and rel_err(xtn.grad, xtr.grad) < 1e-6
+    # the backward's <= 2x2-window path (k <= 2s) and its general loop (k = 3, s = 1)
+    for k, s, p in [(2, 2, 0), (3, 1, 1), (3, 2, 0)]:
+        xk = torch.randn(2, 32, 9, 11, device="cuda")
+        xkn = cl(xk).requires_grad_()
+        yk = CF.max_pool2d(xkn, k, s, p)
+        xkr = xk.double().cpu().requires_grad_()
+        refk = F.max_pool2d(xkr, k, s, p)
+        gk = torch.randn_like(yk)
+        yk.backward(gk)
+        refk.backward(gk.double().cpu())
+        assert rel_err(yk, refk) < 1e-6 and rel_err(xkn.grad, xkr.grad) < 1e-6, (k, s, p)
     x2 = cl(torch.randn(4, 128, 7, 7, device="cuda")).requires_grad_()
     p = CF.global_avg_pool(x2)
     x2r = x2.detach().double().cpu().requires_grad_()
