@@ -111,7 +111,8 @@ def test_capture_failure_on_one_rank_makes_every_rank_eager():
         env.pop(k, None)
     r = subprocess.run([sys.executable, os.path.join(repo, "bench.py"), "--gpus", "2", "--dist-backend", "gloo",
                         "--strategy", "allreduce_blocking", "--steps", "2", "--warmup", "1", "--local-batch", "8",
-                        "--dataset-size", "64"], env=env, capture_output=True, text=True, timeout=240, cwd=repo)
+                        "--dataset-size", "64", "--extras", "no_sync,strong_no_sync"],
+                       env=env, capture_output=True, text=True, timeout=240, cwd=repo)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
     assert "hipGraph capture failed" in r.stderr, r.stderr[-3000:]
     assert "another rank could not capture; all ranks time eager steps" in r.stderr, r.stderr[-3000:]

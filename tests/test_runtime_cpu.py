@@ -384,6 +384,60 @@ def test_bench_failing_rank_fails_the_launcher():
     assert not [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
 
 
+@pytest.mark.parametrize("fault,phase", [("raise", "strong_allreduce_blocking"), ("hang", "strong_bucketed_overlap"),
+                                         ("crash", "no_sync")])
+def test_bench_failed_extra_keeps_the_headline(fault, phase):
+    """A secondary measurement that raises, hangs or crashes on ONE rank (CDP_BENCH_FAULT) costs only
+    its own block: the run exits 0 in bounded time with one JSON line carrying the headline, the named
+    error in the failed block, and every other phase (before and after it) measured."""
+    import time
+
+    t0 = time.monotonic()
+    r = _bench(["--gpus", "2", "--device", "cpu", "--steps", "1", "--warmup", "1", "--local-batch", "2",
+                "--global-batch", "4", "--dataset-size", "16",
+                "--extras", "no_sync,strong_allreduce_blocking,strong_bucketed_overlap"],
+               env_extra={"CDP_BENCH_FAULT": f"{phase}:1:{fault}", "CDP_BENCH_PHASE_LIMIT_S": "30"}, timeout=300)
+    assert time.monotonic() - t0 < 180
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    rec = json.loads(lines[0])
+    assert rec["value"] > 0 and rec["ranks_seen"] == 2 and rec["replicas_identical"] is True
+    st = {p["name"]: p for p in rec["phases"]}
+    assert list(st) == ["headline", "no_sync", "strong_allreduce_blocking", "strong_bucketed_overlap"]
+    assert st[phase]["status"] == "error"
+    assert all(p["status"] == "ok" for n, p in st.items() if n != phase), st
+    err = st[phase]["error"]
+    if fault == "raise":
+        assert "rank 1: RuntimeError: injected fault" in err, err
+    elif fault == "hang":
+        assert "timeout" in err, err
+    else:
+        assert "rank 1: worker exited with -9" in err, err
+    if phase == "no_sync":
+        assert rec["no_sync"]["error"] == err and "exposed_comm_ms" not in rec
+    else:
+        blk = rec["strategies"][phase[len("strong_"):]]
+        assert blk["error"] == err and "ms_per_step" not in blk
+    others = [s for s in ("allreduce_blocking", "bucketed_overlap") if s != phase[len("strong_"):]]
+    for s in others:
+        assert rec["strategies"][s]["replicas_identical"] is True
+
+
+def test_bench_time_budget_skips_extras():
+    """When the budget is spent before an extra could finish, that extra is skipped by agreement (every
+    rank the same way) and the headline is still printed."""
+    r = _bench(["--gpus", "2", "--device", "cpu", "--steps", "1", "--warmup", "1", "--local-batch", "2",
+                "--global-batch", "4", "--dataset-size", "16", "--extras", "no_sync,strong_allreduce_blocking"],
+               env_extra={"CDP_BENCH_BUDGET_S": "1", "CDP_BENCH_PHASE_LIMIT_S": "30"}, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    rec = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    st = {p["name"]: p["status"] for p in rec["phases"]}
+    assert st["headline"] == "ok"
+    assert st["no_sync"].startswith("skipped: time budget") and st["strong_allreduce_blocking"].startswith("skipped")
+    assert rec["value"] > 0
+
+
 @pytest.mark.parametrize("strategy", ["ddp", "allreduce_blocking"])
 def test_bench_detects_diverged_replicas(strategy):
     """One rank's gradient perturbed after the sync (CDP_BENCH_CORRUPT_RANK=1): the replicas differ
