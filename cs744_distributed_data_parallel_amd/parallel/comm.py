@@ -201,6 +201,9 @@ class TorchCommunicator(Communicator):
     def all_reduce(self, t, op="sum", async_op=False):
         op = _norm_op(op)
         if self._gloo_device(t):
+            if torch.cuda.is_current_stream_capturing():
+                raise RuntimeError("gloo all_reduce of a device tensor is host-staged (two device syncs) and "
+                                   "cannot run inside a hipGraph capture")
             # staged through a host tensor between two device syncs, as gather / scatter below: the
             # async device-tensor path left a two-rank DDP run on one GPU 1e-4 (relative L2) away from
             # the blocking strategy after three steps in 1 of ~6 runs, never reproduced with staging

@@ -55,6 +55,19 @@ struct ActMaxBlock {
     add_ch(c0 + 2, v.z);
     add_ch(c0 + 3, v.w);
   }
+  // channel quad c0..c0+3 of C: into LDS when the table holds C channels, else straight into the
+  // block's global channel copy (a layer wider than the table; publish() then gets nch = 0)
+  __device__ void add_ch4_any(int c0, float4 v, int C, const ActMaxOut& o, int copy) {
+    if (C <= NCH) {
+      add_ch4(c0, v);
+      return;
+    }
+    unsigned* dst = o.ch + (long long)copy * C + c0;
+    const float e[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (__float_as_uint(e[j])) glb_max_u32(&dst[j], __float_as_uint(e[j]));
+  }
   // global slot publication: img0 = first image of the window, channels [c0, c0 + nch) of C
   __device__ void publish(const ActMaxOut& o, int img0, int N, int c0, int nch, int C, int copy, int tid,
                           int nthreads) {

@@ -360,7 +360,8 @@ __global__ __launch_bounds__(256) void bn_act_fwd_kernel(const float* __restrict
       run.add(fdiv(pix, fd_HWo), absmax4(z), sam, img0, am);
       if (qmode == 1 || (qmode == 2 && !(k & 1))) cm[0] = absmax4(cm[0], z);
       else if (qmode == 2) cm[1] = absmax4(cm[1], z);
-      else sam.add_ch4(4 * c4, make_float4(fabsf(z.x), fabsf(z.y), fabsf(z.z), fabsf(z.w)));
+      else sam.add_ch4_any(4 * c4, make_float4(fabsf(z.x), fabsf(z.y), fabsf(z.z), fabsf(z.w)), C, am,
+                           blockIdx.x % kActCopies);
     }
   };
   if (!pool) {
@@ -426,7 +427,7 @@ __global__ __launch_bounds__(256) void bn_act_fwd_kernel(const float* __restrict
       if (i0 + tid + 256 < i1) sam.add_ch4(4 * (tid + 256), cm[1]);
     }
     __syncthreads();
-    sam.publish(am, img0, N, 0, C, C, blockIdx.x % kActCopies, tid, 256);
+    sam.publish(am, img0, N, 0, C <= kMaxActC ? C : 0, C, blockIdx.x % kActCopies, tid, 256);
   }
 }
 
@@ -746,7 +747,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const float* __restri
           emit(px * C + 4 * cq, ld4(y + px * C + 4 * cq), f4zero());
         }
       }
-      if (want) sam.add_ch4(4 * cq, cm);
+      if (want) sam.add_ch4_any(4 * cq, cm, C, am, blockIdx.x % kActCopies);
     }
     red[tid] = acc;
     __syncthreads();
@@ -765,7 +766,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const float* __restri
   if (want) {
     run.flush(sam, img0, am);
     __syncthreads();
-    sam.publish(am, img0, N, 0, C, C, blockIdx.x % kActCopies, tid, 256);
+    sam.publish(am, img0, N, 0, C <= kMaxActC ? C : 0, C, blockIdx.x % kActCopies, tid, 256);
   }
 }
 

@@ -29,22 +29,16 @@ namespace {
 
 using namespace x3conv;
 
-template <int BM, int BN, int MODE, bool DGRAD, int NP = 3, bool BNA = false>
+template <int BM, int BN, int MODE, bool DGRAD, int NP = 3>
 __global__ __launch_bounds__(waves_m<BM>() * 128, (NP == 2 && BM + BN <= 256) ? 2 : (BM + BN >= 256) ? 1 : 2) void
 conv_x3_kernel(ConvGemmParams p) {
   __shared__ __attribute__((aligned(16))) __bf16 smem[conv_x3_smem_elems<BM, BN, NP>()];
-  conv_x3_body<BM, BN, MODE, DGRAD, NP, BNA>(p, smem, blockIdx.x, gridDim.x);
+  conv_x3_body<BM, BN, MODE, DGRAD, NP>(p, smem, blockIdx.x, gridDim.x);
 }
 
 template <int BM, int BN, int MODE, bool DGRAD>
 void launch_x3(const ConvGemmParams& p, int ntiles, int np, hipStream_t st) {
   const dim3 blk(waves_m<BM>() * 128), grd(ntiles * p.splits);
-  if constexpr (MODE == 0 && !DGRAD) {
-    if (p.bn_st) {  // BatchNorm on the A load: f16x2 only (the caller checks)
-      hipLaunchKernelGGL((conv_x3_kernel<BM, BN, MODE, DGRAD, 2, true>), grd, blk, 0, st, p);
-      return;
-    }
-  }
   if (np == 1) hipLaunchKernelGGL((conv_x3_kernel<BM, BN, MODE, DGRAD, 1>), grd, blk, 0, st, p);
   else if (np == 2) hipLaunchKernelGGL((conv_x3_kernel<BM, BN, MODE, DGRAD, 2>), grd, blk, 0, st, p);
   else hipLaunchKernelGGL((conv_x3_kernel<BM, BN, MODE, DGRAD, 3>), grd, blk, 0, st, p);

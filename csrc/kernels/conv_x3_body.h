@@ -63,11 +63,9 @@ constexpr int conv_x3_smem_elems() { return 2 * NP * (BM + BN) * LDH; }
 // The kernel body as a device function: `smem` holds conv_x3_smem_elems() bf16 (the caller's one
 // LDS array), `vbid` / `nvb` are this workgroup's id and the count of workgroups running this
 // GEMM (a launch may carry other work beside it: bwd_pair.hip).
-// BNA: BatchNorm (+ReLU) applied to A as it is loaded (p.bn_st; forward MODE 0 only)
-template <int BM, int BN, int MODE, bool DGRAD, int NP = 3, bool BNA = false>
+template <int BM, int BN, int MODE, bool DGRAD, int NP = 3>
 __device__ __forceinline__ void conv_x3_body(const ConvGemmParams& p, __bf16* __restrict__ smem, int vbid, int nvb) {
   static_assert(NP >= 1 && NP <= 3, "planes");
-  static_assert(!BNA || (MODE == 0 && !DGRAD), "BatchNorm on load: forward, whole-tap K-tiles");
   constexpr unsigned ES = 2u;  // log2 bytes per element of the (fp32) global operands
   constexpr int WM = waves_m<BM>();  // waves along M (2 x WM waves)
   constexpr int NT = WM * 128;       // threads
@@ -100,15 +98,6 @@ __device__ __forceinline__ void conv_x3_body(const ConvGemmParams& p, __bf16* __
 
   const int kq = (tid & 3) * 8;  // this thread's 8 consecutive k within the tile
   const int rrow = tid >> 2;     // + RS i
-
-  // BatchNorm on load: the layer's per-channel scale / shift in LDS (read per K-tile at split time)
-  __shared__ float s_bn[BNA ? 2 * kMaxBnLoadC : 1];
-  if constexpr (BNA) {
-    for (int c = tid; c < p.C; c += NT) {
-      s_bn[c] = p.bn_st[2 * p.C + c];
-      s_bn[kMaxBnLoadC + c] = p.bn_st[3 * p.C + c];
-    }
-  }
 
   // buffers (host guarantees < 2 GiB each): out-of-range offsets read as zero
   const unsigned xplane = ((unsigned)p.N * (unsigned)HWC) << ES;
@@ -228,25 +217,16 @@ __device__ __forceinline__ void conv_x3_body(const ConvGemmParams& p, __bf16* __
   // memory. Issuing them unconditionally (no branch around the prefetch) lets the compiler wait
   // with vmcnt(#newer loads) for the older tile instead of vmcnt(0) at a control-flow merge,
   // which would have drained the prefetch of the next tile.
-  // BatchNorm on load: which of a register set's A rows hit the image (padding taps must stay 0,
-  // not become relu(shift)) and the set's first channel
-  unsigned bn_ok0 = 0, bn_ok1 = 0;
-  int bn_c0 = 0, bn_c1 = 0;
-  auto load_tile = [&](int kt, auto& va, auto& vb, bool valid, unsigned& bok, int& bc0) {
+  auto load_tile = [&](int kt, auto& va, auto& vb, bool valid) {
     const int r0 = kt * BK;
     if (MODE == 0) {
       // the whole K-tile lies in one filter tap (C % 32 == 0): tap decode is wave-uniform
       const int tap = fdiv(r0, p.fd_C);
       const int c0 = r0 - tap * p.C;
       const int kh = fdiv(tap, p.fd_KW), kw = tap - kh * p.KW;
-      if constexpr (BNA) {
-        bok = 0;
-        bc0 = c0;
-      }
 #pragma unroll
       for (int i = 0; i < A_LD; ++i) {
         const unsigned o = valid ? a_voff(i, kh, kw, c0) : kOOB;
-        if constexpr (BNA) bok |= (o != kOOB ? 1u : 0u) << i;
         put4(va[i], 0, bload4(xr, o));
         put4(va[i], 4, bload4(xr, o + 16u));
       }
@@ -298,27 +278,8 @@ __device__ __forceinline__ void conv_x3_body(const ConvGemmParams& p, __bf16* __
     }
   };
 
-  auto store_tile = [&](auto& va, const auto& vb, __bf16* st, unsigned bok, int bc0) {
+  auto store_tile = [&](const auto& va, const auto& vb, __bf16* st) {
     const int cp = chunk_pos(rrow, tid & 3) * 8;  // rrow + RS i has the same (row >> 2) & 3
-    if constexpr (BNA) {
-      // the same 8 channels for every row of this thread: [relu](x * scale + shift), zero off-image
-      float sc[8], sh[8];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        sc[j] = s_bn[bc0 + kq + j];
-        sh[j] = s_bn[kMaxBnLoadC + bc0 + kq + j];
-      }
-#pragma unroll
-      for (int i = 0; i < A_LD; ++i) {
-        const bool ok = (bok >> i) & 1u;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          float z = __builtin_fmaf(va[i][j], sc[j], sh[j]);
-          if (p.bn_relu) z = fmaxf(z, 0.f);
-          va[i][j] = ok ? z : 0.f;
-        }
-      }
-    }
 #pragma unroll
     for (int i = 0; i < A_LD; ++i) {
       __bf16* d = st + (rrow + RS * i) * LDH + cp;
@@ -444,23 +405,22 @@ __device__ __forceinline__ void conv_x3_body(const ConvGemmParams& p, __bf16* __
   // (loaded into registers one iteration earlier) is split into stage (t+1)&1 and tile t+2 is
   // being fetched into the other register set.
   if (kt_begin < kt_end) {
-    load_tile(kt_begin, va0, vb0, true, bn_ok0, bn_c0);
-    load_tile(kt_begin + 1, va1, vb1, kt_begin + 1 < kt_end, bn_ok1, bn_c1);
+    load_tile(kt_begin, va0, vb0, true);
+    load_tile(kt_begin + 1, va1, vb1, kt_begin + 1 < kt_end);
     finish_scales();
-    if constexpr (BNA) __syncthreads();  // the scale / shift table
-    store_tile(va0, vb0, smem, bn_ok0, bn_c0);
+    store_tile(va0, vb0, smem);
     __syncthreads();
     int kt = kt_begin;
     for (; kt + 1 < kt_end; kt += 2) {
-      load_tile(kt + 2, va0, vb0, kt + 2 < kt_end, bn_ok0, bn_c0);
+      load_tile(kt + 2, va0, vb0, kt + 2 < kt_end);
       compute(smem);
-      store_tile(va1, vb1, smem + STAGE, bn_ok1, bn_c1);
+      store_tile(va1, vb1, smem + STAGE);
       __syncthreads();
-      load_tile(kt + 3, va1, vb1, kt + 3 < kt_end, bn_ok1, bn_c1);
+      load_tile(kt + 3, va1, vb1, kt + 3 < kt_end);
       compute(smem + STAGE);
       // unconditional (past the last tile it stores stale registers into a stage nothing reads),
       // so the split can interleave with the MFMAs above
-      store_tile(va0, vb0, smem, bn_ok0, bn_c0);
+      store_tile(va0, vb0, smem);
       __syncthreads();
     }
     if (kt < kt_end) compute(smem);  // odd tile count: the last tile sits in stage 0

@@ -72,13 +72,7 @@ struct ConvGemmParams {
   const unsigned* a_img;
   const float* b_row;
   int b_np, b_stride;
-  // BatchNorm applied on the A load (forward, MODE 0, f16x2 only): x is the producer's raw conv
-  // output and the GEMM reads [relu](x * scale[c] + shift[c]) with scale / shift = bn_st + 2C / 3C
-  // (a BN stats block [mean | invstd | scale | shift] x C); padding taps stay zero. nullptr = off.
-  const float* bn_st;
-  int bn_relu;
 };
-constexpr int kMaxBnLoadC = 512;  // channels of an A operand with BatchNorm on load (LDS table; VGG, ResNet bottleneck widths)
 
 struct WgradParams {
   const float* dy;  // [M][Cout]

@@ -25,10 +25,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("clear_hip_error", [] { return std::string(hipGetErrorName(hipGetLastError())); },
         "reset the thread's last HIP error (e.g. after an invalidated stream capture) and return its name");
   m.def("conv2d_fwd", &conv2d_fwd, py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("stride"), py::arg("pad"),
-        py::arg("want_stats") = false, py::arg("x_amax") = py::none(), py::arg("w_amax") = py::none(),
-        py::arg("bn_stats") = py::none(), py::arg("bn_relu") = true,
-        "bn_stats ([4, C]: mean | invstd | scale | shift): the GEMM reads [relu](x * scale + shift) -- "
-        "BatchNorm applied on the operand load (f16x2, 3x3 / 1x1 forward with C % 32 == 0)");
+        py::arg("want_stats") = false, py::arg("x_amax") = py::none(), py::arg("w_amax") = py::none());
   m.def("conv2d_dgrad", &conv2d_dgrad, py::arg("dy"), py::arg("w"), py::arg("in_shape"), py::arg("stride"),
         py::arg("pad"), py::arg("addend") = py::none(), py::arg("dy_amax") = py::none(), py::arg("w_amax") = py::none(),
         py::arg("w_t") = py::none());
@@ -106,7 +103,13 @@ PYBIND11_MODULE(_C, m) {
           return reinterpret_cast<intptr_t>(st);
         },
         py::arg("priority") = 0, py::arg("nonblocking") = true, py::arg("cu_mask") = false,
-        "diagnostics: a raw HIP stream (never destroyed) for torch.cuda.ExternalStream");
+        "diagnostics: a raw HIP stream for torch.cuda.ExternalStream; the caller destroys it with "
+        "destroy_stream before the process exits (HIP's own teardown must not meet a live CU-masked queue)");
+  m.def("destroy_stream", [](intptr_t s) {
+    hipStream_t st = reinterpret_cast<hipStream_t>(s);
+    TORCH_CHECK(hipStreamSynchronize(st) == hipSuccess && hipStreamDestroy(st) == hipSuccess,
+                "hipStreamDestroy failed");
+  });
   m.def("stream_priority_range", [] {
     int lo = 0, hi = 0;
     hipDeviceGetStreamPriorityRange(&lo, &hi);

@@ -98,8 +98,10 @@ int split_planes() { return conv_gemm_mode() == 2 ? 1 : conv_gemm_mode() == 3 ? 
 //    kept alive with it) whose memset is captured, so each replay re-zeroes them before its
 //    producers run.
 // Everything is ordered on the current stream, like the caching allocator's reuse; a chunk taken up
-// on another stream than its last user's (its memset, or slots still being read) first makes the
-// new stream wait for that one.
+// on another stream than its last allocating stream (its memset and producers) first makes the new
+// stream wait for that one. Readers are assumed to run on the allocating stream, or to be ordered
+// before its next work (the consumer GEMMs of this runtime run on the producer's stream); a caller
+// reading slots on another stream must keep the slot tensor alive until that read has completed.
 constexpr long long kSlotChunk = 1LL << 16;     // int32 slots per eager chunk (256 KB)
 constexpr long long kCapSlotChunk = 1LL << 18;  // ... per captured chunk (1 MB: one memset node for a VGG-11 step)
 struct SlotPool {
@@ -112,7 +114,13 @@ struct SlotPool {
   at::Tensor cap_cur;
   long long cap_used = 0;
   long long cap_total = 0, cap_hint = 0;  // slots taken by the current / largest earlier capture
-  std::vector<at::Tensor> cap_keep;
+  // a capture's chunks stay referenced until that capture has ended: freed earlier, their blocks
+  // could be handed to a later allocation of the SAME capture (the graph's private pool) while the
+  // captured memset and producers still address them. Once the capture is over, the pool keeps the
+  // blocks for the graph's lifetime, so the references are dropped when the next
+  // capture starts (not at an eager call: one on another stream cannot tell whether the capture is
+  // still running) -- at most one capture's chunks are held, however often the step is re-captured.
+  std::vector<std::pair<unsigned long long, at::Tensor>> cap_keep;
 };
 
 std::atomic<long long>& slot_memsets() {
@@ -136,6 +144,10 @@ at::Tensor alloc_slots(long long n, const at::Tensor& like, hipStream_t st) {
   hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
   unsigned long long id = 0;
   TORCH_CHECK(hipStreamGetCaptureInfo(st, &cs, &id) == hipSuccess, "act max slots: capture query failed");
+  if (cs == hipStreamCaptureStatusActive && id != P.cap_id && !P.cap_keep.empty()) {
+    P.cap_keep.clear();  // a new capture: the earlier ones have ended (their pools keep the blocks)
+    P.cap_cur = at::Tensor();
+  }
   if (cs == hipStreamCaptureStatusActive) {
     // a capture's first chunk is sized by the largest earlier capture (a re-captured step takes one
     // chunk, i.e. one captured memset of just its slots; ResNet-50 took eight 256 KB ones)
@@ -145,7 +157,7 @@ at::Tensor alloc_slots(long long n, const at::Tensor& like, hipStream_t st) {
     }
     if (id != P.cap_id || !P.cap_cur.defined() || P.cap_used + n > P.cap_cur.numel()) {
       P.cap_cur = fresh(std::max(std::max(kCapSlotChunk, n), id != P.cap_id ? P.cap_hint : 0LL));
-      P.cap_keep.push_back(P.cap_cur);
+      P.cap_keep.emplace_back(id, P.cap_cur);
       P.cap_used = 0;
       P.cap_id = id;
     }
@@ -942,8 +954,7 @@ std::string get_conv_gemm() {
 // partials are returned in a second tensor [nparts, Cout, 2] together with rows-per-part.
 std::vector<at::Tensor> conv2d_fwd(const at::Tensor& x_, const at::Tensor& w_, const c10::optional<at::Tensor>& bias,
                                    int64_t stride, int64_t pad, bool want_stats, const c10::optional<at::Tensor>& x_amax,
-                                   const c10::optional<at::Tensor>& w_amax, const c10::optional<at::Tensor>& bn_stats,
-                                   bool bn_relu) {
+                                   const c10::optional<at::Tensor>& w_amax) {
   check_f32_cuda(x_, "x");
   check_f32_cuda(w_, "weight");
   TORCH_CHECK(x_.dim() == 4 && w_.dim() == 4, "conv2d_fwd expects 4-D input and weight");
@@ -974,18 +985,6 @@ std::vector<at::Tensor> conv2d_fwd(const at::Tensor& x_, const at::Tensor& w_, c
   set_scales(p, xa, wa, false, Co, C);
   p.y = y.data_ptr<float>();
   p.bias = fptr(bias);
-  if (bn_stats.has_value() && bn_stats->defined()) {
-    // BatchNorm on the A load: x is the producer's raw conv output; the operand maxima given (or
-    // measured) must be those of the transformed activation
-    TORCH_CHECK(f16x2_mode() && x3_ok(p, false) && C % 32 == 0 && Kdim % 32 == 0 && C <= kMaxBnLoadC,
-                "conv2d_fwd: BatchNorm on the operand load needs the f16x2 engine, C % 32 == 0 and C <= ",
-                kMaxBnLoadC);
-    TORCH_CHECK(bn_stats->is_cuda() && bn_stats->scalar_type() == at::kFloat && bn_stats->numel() == 4 * C &&
-                    bn_stats->is_contiguous(),
-                "conv2d_fwd: bn_stats must be a contiguous fp32 [4, C] stats block");
-    p.bn_st = bn_stats->data_ptr<float>();
-    p.bn_relu = bn_relu ? 1 : 0;
-  }
   // BN partials: one per BM-row tile (splits == 1) or per reduction row block (split-K)
   std::function<float*(int)> alloc_part;
   if (want_stats)

@@ -16,8 +16,7 @@ std::string get_conv_gemm();
 std::vector<at::Tensor> conv2d_fwd(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tensor>& bias,
                                    int64_t stride, int64_t pad, bool want_stats,
                                    const c10::optional<at::Tensor>& x_amax = c10::nullopt,
-                                   const c10::optional<at::Tensor>& w_amax = c10::nullopt,
-                                   const c10::optional<at::Tensor>& bn_stats = c10::nullopt, bool bn_relu = true);
+                                   const c10::optional<at::Tensor>& w_amax = c10::nullopt);
 at::Tensor conv2d_dgrad(const at::Tensor& dy, const at::Tensor& w, std::vector<int64_t> in_shape, int64_t stride,
                         int64_t pad, const c10::optional<at::Tensor>& addend,
                         const c10::optional<at::Tensor>& dy_amax = c10::nullopt,

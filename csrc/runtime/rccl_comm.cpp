@@ -109,7 +109,8 @@ RcclComm::RcclComm(const std::string& uid, int rank, int world, int device, doub
   //    40-57 us apart -- the round-4 slowdown: its "own" stream was created at that least priority;
   //  * captured DDP step (RCCL kernel + post-op per bucket): 0.552-0.555 / 0.559-0.565 / 0.553-0.555 ms;
   //  * every side stream kind ran on its own hardware queue (rocprofv3 Queue_Id 2, compute on 1).
-  // CDP_COMM_STREAM = own (default) | pool | low | cumask selects the stream for such A/B runs.
+  // CDP_COMM_STREAM = own (default) | pool | low selects the stream for such A/B runs. (A CU-masked
+  // stream kind was dropped: it brought no gain and its diagnostic run crashed at process exit.)
   const char* kind = std::getenv("CDP_COMM_STREAM");
   stream_kind_ = kind && *kind ? kind : "own";
   if (stream_kind_ == "own" || stream_kind_ == "low") {
@@ -117,13 +118,8 @@ RcclComm::RcclComm(const std::string& uid, int rank, int world, int device, doub
     HIP_CHECK(hipDeviceGetStreamPriorityRange(&lo, &hi));
     HIP_CHECK(hipStreamCreateWithPriority(&stream_, hipStreamNonBlocking, stream_kind_ == "low" ? lo : 0));
     own_stream_ = true;
-  } else if (stream_kind_ == "cumask") {
-    uint32_t mask[8];
-    for (auto& w : mask) w = 0xffffffffu;
-    HIP_CHECK(hipExtStreamCreateWithCUMask(&stream_, 8, mask));
-    own_stream_ = true;
   } else {
-    TORCH_CHECK(stream_kind_ == "pool", "CDP_COMM_STREAM must be own, pool, low or cumask");
+    TORCH_CHECK(stream_kind_ == "pool", "CDP_COMM_STREAM must be own, pool or low");
     stream_ = c10::hip::getStreamFromPool(/*isHighPriority=*/false, (c10::DeviceIndex)device).stream();
   }
   HIP_CHECK(hipEventCreateWithFlags(&start_ev_, hipEventDisableTiming));

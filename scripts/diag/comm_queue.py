@@ -41,8 +41,16 @@ import cs744_distributed_data_parallel_amd as cdp  # noqa: E402
 
 C = cdp._native.lib()
 side = None
+raw = []  # raw HIP streams of this run, destroyed before the interpreter (and HIP) tear down
+
+
+def ext_stream(*a):
+    raw.append(C.create_stream(*a))
+    return torch.cuda.ExternalStream(raw[-1])
+
+
 if kind == "own_first":
-    side = torch.cuda.ExternalStream(C.create_stream(0, True, False))
+    side = ext_stream(0, True, False)
 B = 32
 hz = C.gpu_wall_clock_khz() * 1e3
 print("stream priority range (least, greatest):", C.stream_priority_range(), flush=True)
@@ -53,11 +61,11 @@ torch.cuda.Stream()  # PyTorch's pool is initialised from here on
 if kind == "pool":
     side = torch.cuda.Stream()
 elif kind == "own":
-    side = torch.cuda.ExternalStream(C.create_stream(0, True, False))
+    side = ext_stream(0, True, False)
 elif kind == "own_low":
-    side = torch.cuda.ExternalStream(C.create_stream(C.stream_priority_range()[0], True, False))
+    side = ext_stream(C.stream_priority_range()[0], True, False)
 elif kind == "cumask":
-    side = torch.cuda.ExternalStream(C.create_stream(0, True, True))
+    side = ext_stream(0, True, True)
 
 torch.manual_seed(0)
 model = cdp.VGG11().cuda()
@@ -99,3 +107,8 @@ for it in range(4):
     torch.cuda.synchronize()
     st = sorted(ts.cpu().tolist()[:n])
     print(f"{kind} iter {it}: backward span {(st[-1] - st[0]) / hz * 1e6:.0f} us", flush=True)
+torch.cuda.synchronize()
+side = None
+for s_ in raw:
+    C.destroy_stream(s_)
+print("side streams destroyed", flush=True)

@@ -203,7 +203,7 @@ def test_act_max_slots_ordered_across_streams():
 
 
 @pytest.mark.parametrize("pool", [False, True])
-@pytest.mark.parametrize("N,Co,HW", [(32, 64, 16), (8, 512, 2), (256, 128, 8), (4, 2048, 2)])
+@pytest.mark.parametrize("N,Co,HW", [(32, 64, 16), (8, 512, 2), (256, 128, 8), (4, 2048, 2), (4, 4096, 2)])
 def test_bn_producers_write_exact_act_max(N, Co, HW, pool):
     """The fused block forward's output carries the exact per-image / per-channel |max| of what its
     BatchNorm-apply kernel wrote (bn_fin_act or bn_act_fwd, whichever the shape takes)."""
@@ -227,7 +227,7 @@ def test_bn_producers_write_exact_act_max(N, Co, HW, pool):
 
 @pytest.mark.parametrize("fused", ["1", "0"])
 @pytest.mark.parametrize("pool", [False, True])
-@pytest.mark.parametrize("N,Co,HW", [(16, 128, 8), (8, 512, 4)])
+@pytest.mark.parametrize("N,Co,HW", [(16, 128, 8), (8, 512, 4), (2, 4096, 4)])
 def test_bn_backward_producers_write_act_max(N, Co, HW, pool, fused, monkeypatch):
     """The fused block backward's dy act max (bn_bwd_fin_apply or bn_bwd_apply) matches the
     per-image / per-channel |max| of dy recomputed by torch in fp32 from the same statistics (to
