@@ -55,6 +55,7 @@ class SGD(Optimizer):
         self.fused_prep = True  # emit the next step's weight preparation from the step (one arena pass)
         self._step_counter = None  # a device step counter this step advances (DeviceLoader.advance_with)
         self._counter_pending = None
+        self._overlap = None  # this iteration's per-bucket steps, run by a DDP reducer (bucket_steps)
         all_params = [p for g in self.param_groups for p in g["params"]]
         if flat and all_params and all_params[0].is_cuda:
             self._arena = arena_for(all_params)
@@ -126,6 +127,14 @@ class SGD(Optimizer):
         if closure is not None:
             with torch.enable_grad():
                 loss = closure()
+        if self._overlap is not None:
+            ov, self._overlap = self._overlap, None
+            done = ov["reducer"].stepped_buckets()
+            if done == ov["n"]:
+                self._finish_overlapped(ov)
+                return loss
+            if done:
+                raise RuntimeError(f"overlapped optimizer step: only {done} of {ov['n']} buckets were stepped")
         self._counter_pending = self._step_counter
         for gi, group in enumerate(self.param_groups):
             params = [p for p in group["params"] if p.grad is not None]
@@ -146,6 +155,73 @@ class SGD(Optimizer):
             self._counter_pending = None
         self._steps += 1
         return loss
+
+    # ------------------------------------------------------------------ overlapped step (DDP)
+    def bucket_steps(self, ranges, reducer):
+        """Split this iteration's step over gradient buckets (``DistributedDataParallel.overlap_optimizer``).
+
+        ``ranges``: the buckets' flat arena ranges in launch order. Returns one keyword dict per
+        bucket for the reducer's ``set_bucket_step`` -- the SGD of that range, run on the reducer's
+        step stream right after the bucket's all-reduce -- or None when the step cannot be split
+        this iteration (several param groups, parameters outside one arena run, first and later
+        momentum steps mixed, no native kernels). The next ``step()`` then only does the
+        bookkeeping, provided the reducer stepped every bucket; hyperparameters are those at the
+        time of this call (the forward), the first-step momentum rule (buf = d_p) is kept."""
+        if self._arena is None or len(self.param_groups) != 1 or _native.force_reference():
+            return None
+        group = self.param_groups[0]
+        params, arena = group["params"], self._arena
+        if len(params) != len(arena.params) or any(not p.is_cuda for p in params):
+            return None
+        rng = arena.contiguous_range(params)
+        ranges = [(int(s), int(e)) for s, e in ranges]
+        if rng is None or not ranges or ranges[0][0] != rng[0] or ranges[-1][1] != rng[1]:
+            return None
+        if any(ranges[k][1] != ranges[k + 1][0] for k in range(len(ranges) - 1)):
+            return None
+        m = group["momentum"]
+        first = True
+        if m != 0.0:
+            mviews = arena.momentum_views()
+            bufs = [self.state[p].get("momentum_buffer") for p in params]
+            if any(b is not None and b.data_ptr() != mviews[p._cdp_index].data_ptr() for b, p in zip(bufs, params)):
+                return None  # e.g. loaded buffers not yet adopted: a normal step moves them in
+            firsts = [b is None for b in bufs]
+            if any(firsts) and not all(firsts):
+                return None
+            first = all(firsts)
+        plan = arena.prep_plan_ranges(ranges) if self.fused_prep else None
+        mom = arena.momentum_buffer() if m != 0.0 else None
+        lr_t = self._lr_tensor
+        out = []
+        for k, (s, e) in enumerate(ranges):
+            a = dict(p=arena.data[s:e], g=arena.grad[s:e], buf=mom[s:e] if mom is not None else None, lr_t=lr_t,
+                     lr=group["lr"], momentum=m, dampening=group["dampening"], wd=group["weight_decay"],
+                     nesterov=group["nesterov"], first=first, maximize=group["maximize"],
+                     counter=self._step_counter if k == len(ranges) - 1 else None)
+            sub = plan["subs"][k] if plan is not None else None
+            if sub is not None:
+                a.update(desc=sub["desc"], meta=sub["meta"], amax=plan["amax"])
+            out.append(a)
+        self._overlap = {"reducer": reducer, "n": len(out), "first": first and m != 0.0, "prep": plan is not None,
+                         "params": list(params)}
+        return out
+
+    def cancel_bucket_steps(self):
+        self._overlap = None
+
+    def _finish_overlapped(self, ov):
+        """Bookkeeping of a step the reducer ran bucket by bucket (no kernel here)."""
+        arena = self._arena
+        if ov["first"]:
+            mviews = arena.momentum_views()
+            for p in ov["params"]:
+                self.state[p]["momentum_buffer"] = mviews[p._cdp_index]
+        arena.prep_valid = None
+        if ov["prep"]:
+            arena.prep_mark_valid()
+        self._counter_pending = None  # advanced by the last bucket's kernel
+        self._steps += 1
 
     def advance_each_step(self, counter: torch.Tensor):
         """Advance ``counter`` (a device int64 step counter, e.g. a DeviceLoader's) by one in every
@@ -229,6 +305,18 @@ class SGD(Optimizer):
         ctr, self._counter_pending = self._counter_pending, None
         if plan is None:
             C.sgd_step(arena.data[s:e], arena.grad[s:e], mom, lr_t, lr, m, damp, wd, 1.0, nest, first, maxim, ctr)
+            return
+        if "subs" in plan:  # the split plan of an overlapped step (same buffers): its ranges in turn
+            last = len(plan["ranges"]) - 1
+            for k, ((a, b), sub) in enumerate(zip(plan["ranges"], plan["subs"])):
+                mk = mom[a - s:b - s] if mom is not None else None
+                c = ctr if k == last else None
+                if sub is None:
+                    C.sgd_step(arena.data[a:b], arena.grad[a:b], mk, lr_t, lr, m, damp, wd, 1.0, nest, first, maxim, c)
+                else:
+                    C.sgd_step_prep(arena.data[a:b], arena.grad[a:b], mk, lr_t, lr, m, damp, wd, 1.0, nest, first,
+                                    maxim, sub["desc"], sub["meta"], plan["amax"], c)
+            arena.prep_mark_valid()
             return
         C.sgd_step_prep(arena.data[s:e], arena.grad[s:e], mom, lr_t, lr, m, damp, wd, 1.0, nest, first, maxim,
                         plan["desc"], plan["meta"], plan["amax"], ctr)

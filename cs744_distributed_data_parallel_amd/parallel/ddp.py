@@ -96,6 +96,30 @@ class DistributedDataParallel(nn.Module):
         )
         self._rebuild = rebuild_buckets
         self._rebuilt = False
+        self._step_opt = None
+
+    def overlap_optimizer(self, optimizer):
+        """Opt-in: run ``optimizer``'s step bucket by bucket inside backward, each bucket's SGD on the
+        reducer's step stream right after that bucket's all-reduce (so it overlaps the remaining
+        buckets' communication and backward compute, instead of following the last bucket on the
+        compute stream). ``optimizer.step()`` then only completes the bookkeeping. Applies to
+        iterations with gradient sync on the RCCL communicator once the buckets are rebuilt in ready
+        order (before that, and under ``no_sync``, the step runs whole as usual). The result is
+        bitwise the end-of-step SGD's. Needs this package's ``SGD`` over the module's parameters."""
+        if not hasattr(optimizer, "bucket_steps"):
+            raise TypeError("overlap_optimizer needs cs744_distributed_data_parallel_amd.SGD")
+        self._step_opt = optimizer
+        return self
+
+    def _register_bucket_steps(self):
+        opt, red = self._step_opt, self.reducer
+        red.set_bucket_steps(None)
+        opt.cancel_bucket_steps()
+        if not red.can_step_buckets():
+            return
+        steps = opt.bucket_steps(red.bucket_ranges, red)
+        if steps is not None:
+            red.set_bucket_steps(steps)
 
     # ------------------------------------------------------------------ construction-time sync
     def _verify_shapes(self, params):
@@ -147,6 +171,8 @@ class DistributedDataParallel(nn.Module):
         if grad_sync:
             self.require_forward_param_sync = True
             self.reducer.prepare_for_backward(_tensors_in(out, []))
+            if self._step_opt is not None:
+                self._register_bucket_steps()
         else:
             self.require_forward_param_sync = False
         return out
@@ -167,6 +193,7 @@ class DistributedDataParallel(nn.Module):
 
     def _get_ddp_logging_data(self):
         return {
+            "overlapped_step_buckets": self.reducer.stepped_buckets() if self._step_opt is not None else 0,
             "bucket_sizes": self.reducer.bucket_sizes_bytes(),
             "num_buckets": self.reducer.num_buckets,
             "native_reducer": self.reducer.native,

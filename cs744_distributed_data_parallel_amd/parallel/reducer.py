@@ -346,6 +346,20 @@ class GradReducer:
     def disarm(self):
         self._impl.disarm()
 
+    def can_step_buckets(self) -> bool:
+        """Per-bucket optimizer steps need the native reducer on the RCCL communicator (collectives
+        on a stream the step stream can wait on) and buckets that are arena ranges in launch order."""
+        return self.native and isinstance(self.comm, RcclCommunicator) and bool(self.arena_in_ready_order)
+
+    def set_bucket_steps(self, steps):
+        """Register this backward's per-bucket SGD launches (``SGD.bucket_steps``); None clears."""
+        self._impl.clear_bucket_steps()
+        for b, kw in enumerate(steps or []):
+            self._impl.set_bucket_step(b, **kw)
+
+    def stepped_buckets(self) -> int:
+        return int(self._impl.stepped_buckets) if self.native else 0
+
     def set_trace(self, on: bool = True):
         """Record ('h', param) at every gradient-ready hook, ('l', bucket) at every bucket
         launch and ('f', -1) at the end-of-backward callback (see :meth:`trace_log`)."""

@@ -226,8 +226,12 @@ class FlatArena:
             return None
         weights, want = req
         key = self._prep_key(weights, want)
-        if self._prep_plan is not None and self._prep_plan[0] == key and self._prep_plan[2] == (start, end):
-            return self._prep_plan[1]
+        if self._prep_plan is not None and self._prep_plan[0] == key:
+            rng = self._prep_plan[2]
+            if rng == (start, end):
+                return self._prep_plan[1]
+            if isinstance(rng[0], tuple) and rng[0][0] == start and rng[-1][1] == end:
+                return self._prep_plan[1]  # a split plan tiling this range (its sub-plans run in turn)
         if any(getattr(w, "_cdp_arena", None) is not self for w in weights):
             return None
         offs = [self.offsets[w._cdp_index] for w in weights]
@@ -249,6 +253,54 @@ class FlatArena:
         plan = {"desc": desc, "meta": meta, "amax": amax, "amax_views": views,
                 "wts": [t if f else None for t, f in zip(wts, want)], "weights": list(weights)}
         self._prep_plan = (key, plan, (start, end))
+        return plan
+
+    def prep_plan_ranges(self, ranges):
+        """The fused-step plan split over consecutive flat ranges (the buckets of an overlapped
+        optimizer step, each stepped by its own launch): ONE maxima tensor and one W^T per weight in
+        the request's order, as :meth:`prep_lookup` hands them to the forward, plus one sub-plan per
+        range covering the weights inside it (None for a range with no prepared weight). None when
+        a weight straddles two ranges or the request does not lie in them."""
+        req = self.prep_request
+        if req is None:
+            return None
+        ranges = tuple((int(s), int(e)) for s, e in ranges)
+        weights, want = req
+        key = self._prep_key(weights, want)
+        if self._prep_plan is not None and self._prep_plan[0] == key and self._prep_plan[2] == ranges:
+            return self._prep_plan[1]
+        if any(getattr(w, "_cdp_arena", None) is not self for w in weights):
+            return None
+        if any(w.dim() != 4 or not w.is_contiguous(memory_format=torch.channels_last) for w in weights):
+            return None
+        offs = [self.offsets[w._cdp_index] for w in weights]
+        where = []
+        for o, w in zip(offs, weights):
+            r = [k for k, (s, e) in enumerate(ranges) if s <= o and o + w.numel() <= e]
+            if len(r) != 1:
+                return None
+            where.append(r[0])
+        from .. import _native
+
+        sizes = [weight_max_elems(w.shape[0], w.shape[1]) for w in weights]
+        starts = [sum(sizes[:k]) for k in range(len(sizes))]
+        amax = torch.empty(max(1, sum(sizes)), device=self.device, dtype=self.dtype)
+        wts = [None] * len(weights)
+        subs = []
+        for k, (s, e) in enumerate(ranges):
+            idx = [j for j, r in enumerate(where) if r == k]
+            if not idx:
+                subs.append(None)
+                continue
+            r = _native.lib().sgd_prep_plan(self.data, s, e, [weights[j].data for j in idx], [bool(want[j]) for j in idx],
+                                            amax, [starts[j] for j in idx])
+            subs.append({"desc": r[0], "meta": r[1]})
+            for t, j in zip(r[3:], idx):
+                wts[j] = t if want[j] else None
+        views = [amax.narrow(0, st, n) for st, n in zip(starts, sizes)]
+        plan = {"amax": amax, "amax_views": views, "wts": wts, "weights": list(weights), "subs": subs,
+                "ranges": ranges}
+        self._prep_plan = (key, plan, ranges)
         return plan
 
     def prep_refresh(self) -> bool:

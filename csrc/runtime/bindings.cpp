@@ -70,7 +70,8 @@ PYBIND11_MODULE(_C, m) {
         py::arg("momentum"), py::arg("dampening"), py::arg("wd"), py::arg("grad_scale"), py::arg("nesterov"),
         py::arg("first"), py::arg("maximize"), py::arg("counter") = py::none());
   m.def("sgd_prep_plan", &sgd_prep_plan, py::arg("flat"), py::arg("start"), py::arg("end"), py::arg("weights"),
-        py::arg("want_t"), "plan of the fused SGD + weight-preparation step over an arena range");
+        py::arg("want_t"), py::arg("amax_out") = py::none(), py::arg("amax_offsets") = std::vector<int64_t>{},
+        "plan of the fused SGD + weight-preparation step over an arena range");
   m.def("sgd_step_prep", &sgd_step_prep, py::arg("p"), py::arg("g"), py::arg("buf"), py::arg("lr_t"), py::arg("lr"),
         py::arg("momentum"), py::arg("dampening"), py::arg("wd"), py::arg("grad_scale"), py::arg("nesterov"),
         py::arg("first"), py::arg("maximize"), py::arg("desc"), py::arg("meta"), py::arg("amax"),
@@ -147,6 +148,8 @@ PYBIND11_MODULE(_C, m) {
       .def("set_timeout", &RcclComm::set_timeout)
       .def("set_test_postop", &RcclComm::set_test_postop, py::arg("delay_us"), py::arg("scale"),
            "test hook: delay + scale after every all_reduce, inside its completion event")
+      .def("set_test_postop_model", &RcclComm::set_test_postop_model, py::arg("alpha_us"), py::arg("gbps"),
+           py::arg("world"), "test hook: modelled ring all-reduce time after every all_reduce (one-GPU stand-in)")
       .def("timeout", &RcclComm::timeout)
       .def("captured_collectives", &RcclComm::captured_collectives)
       .def("eager_collectives", &RcclComm::eager_collectives)
@@ -181,5 +184,13 @@ PYBIND11_MODULE(_C, m) {
       .def("trace_log", &Reducer::trace_log)
       .def_property_readonly("iterations", &Reducer::iterations)
       .def_property_readonly("launched_total", &Reducer::launched_total)
-      .def_property_readonly("num_buckets", &Reducer::num_buckets);
+      .def_property_readonly("num_buckets", &Reducer::num_buckets)
+      .def("set_bucket_step", &Reducer::set_bucket_step, py::arg("bucket"), py::arg("p"), py::arg("g"), py::arg("buf"),
+           py::arg("lr_t"), py::arg("lr"), py::arg("momentum"), py::arg("dampening"), py::arg("wd"), py::arg("nesterov"),
+           py::arg("first"), py::arg("maximize"), py::arg("desc") = py::none(), py::arg("meta") = py::none(),
+           py::arg("amax") = py::none(), py::arg("counter") = py::none(),
+           "SGD over bucket b's arena range, run on the reducer's step stream as soon as b's all-reduce completes "
+           "(held for the next backward only)")
+      .def("clear_bucket_steps", &Reducer::clear_bucket_steps)
+      .def_property_readonly("stepped_buckets", &Reducer::stepped_buckets);
 }

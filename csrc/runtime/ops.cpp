@@ -1749,10 +1749,17 @@ void sgd_step(at::Tensor p, const at::Tensor& g, c10::optional<at::Tensor> buf, 
 // {descriptor (device bytes), meta (cpu int64: nseg, nblk_w, nchunk), weight maxima (device;
 // weight_max_elems floats per weight, back to back, as weight_prep lays them out), W^T per weight
 // (undefined where not wanted)}. Built once per arena layout, outside any capture.
+// With amax_out / amax_offsets the maxima go to caller-owned storage at the given float offsets
+// (one per weight): the per-bucket plans of an overlapped optimizer step share ONE maxima tensor,
+// laid out as the forward expects, and each writes only its own weights' part of it.
 std::vector<at::Tensor> sgd_prep_plan(const at::Tensor& flat, int64_t s, int64_t e, const std::vector<at::Tensor>& ws,
-                                      const std::vector<bool>& want_t) {
+                                      const std::vector<bool>& want_t, const c10::optional<at::Tensor>& amax_out,
+                                      const std::vector<int64_t>& amax_offsets) {
   check_f32_cuda(flat, "arena");
   TORCH_CHECK(ws.size() == want_t.size() && !ws.empty(), "sgd_prep_plan: one want_t flag per weight");
+  const bool ext = amax_out.has_value() && amax_out->defined();
+  TORCH_CHECK(!ext || amax_offsets.size() == ws.size(), "sgd_prep_plan: one maxima offset per weight");
+  if (ext) check_f32_cuda(*amax_out, "amax_out");
   TORCH_CHECK(0 <= s && s < e && e <= flat.numel() && (s % 4) == 0, "sgd_prep_plan: bad range");
   const float* base = flat.data_ptr<float>() + s;
   std::vector<SgdPrepSeg> segs;
@@ -1772,7 +1779,13 @@ std::vector<at::Tensor> sgd_prep_plan(const at::Tensor& flat, int64_t s, int64_t
     at::Tensor wt;
     if (want_t[i]) wt = at::empty({Ci, (long long)T * Co}, flat.options());
     outs.push_back(wt);
-    segs.push_back(SgdPrepSeg{off, wt.defined() ? wt.data_ptr<float>() : nullptr, Co, T, Ci, blk, ptot});
+    long long pofs = ptot;
+    if (ext) {
+      pofs = amax_offsets[i];
+      TORCH_CHECK(pofs >= 0 && pofs + weight_max_elems(Co, Ci) <= amax_out->numel(),
+                  "sgd_prep_plan: maxima offset outside amax_out");
+    }
+    segs.push_back(SgdPrepSeg{off, wt.defined() ? wt.data_ptr<float>() : nullptr, Co, T, Ci, blk, pofs});
     blk += ((Co + 31) / 32) * ((Ci + 31) / 32);
     ptot += weight_max_elems(Co, Ci);
     covered.push_back({off, off + (w.numel() + 3) / 4 * 4});
@@ -1798,7 +1811,7 @@ std::vector<at::Tensor> sgd_prep_plan(const at::Tensor& flat, int64_t s, int64_t
   if (!chunks.empty()) std::memcpy(host.data_ptr<uint8_t>() + seg_bytes, chunks.data(), bytes - seg_bytes);
   at::Tensor desc = host.to(flat.device());
   at::Tensor meta = at::tensor({(int64_t)segs.size(), (int64_t)blk, (int64_t)chunks.size()}, at::kLong);
-  at::Tensor amax = at::empty({std::max(ptot, 1LL)}, flat.options());
+  at::Tensor amax = ext ? *amax_out : at::empty({std::max(ptot, 1LL)}, flat.options());
   std::vector<at::Tensor> r = {desc, meta, amax};
   for (auto& t : outs) r.push_back(t);
   return r;

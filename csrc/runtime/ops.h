@@ -72,7 +72,9 @@ std::vector<at::Tensor> linear_bwd(const at::Tensor& gy, const at::Tensor& x, co
 at::Tensor xent_fwd(const at::Tensor& logits, const at::Tensor& target, const c10::optional<at::Tensor>& correct);
 at::Tensor xent_bwd(const at::Tensor& gloss, const at::Tensor& logits, const at::Tensor& target);
 std::vector<at::Tensor> sgd_prep_plan(const at::Tensor& flat, int64_t s, int64_t e, const std::vector<at::Tensor>& ws,
-                                      const std::vector<bool>& want_t);
+                                      const std::vector<bool>& want_t,
+                                      const c10::optional<at::Tensor>& amax_out = c10::nullopt,
+                                      const std::vector<int64_t>& amax_offsets = {});
 void sgd_step_prep(at::Tensor p, const at::Tensor& g, c10::optional<at::Tensor> buf, const c10::optional<at::Tensor>& lr_t,
                    double lr, double momentum, double dampening, double wd, double grad_scale, bool nesterov, bool first,
                    bool maximize, const at::Tensor& desc, const at::Tensor& meta, at::Tensor amax,

@@ -286,12 +286,16 @@ std::shared_ptr<RcclWork> RcclComm::all_reduce(at::Tensor t, const std::string& 
   // kernel is issued (the stream ordering and the work object stay). At world size 1 RCCL's
   // kernels were measured to hold back the compute stream's dispatches for ~50 us each
   // (scripts/diag/ready_timing.py); the test post-op keeps the collective so its ordering tests run.
-  const bool postop = postop_delay_us_ > 0.0 || postop_scale_ != 1.0;
+  const bool model = postop_w_ > 1 && postop_gbps_ > 0.0;
+  const bool postop = postop_delay_us_ > 0.0 || postop_scale_ != 1.0 || model;
   if (world_ > 1 || postop)
     RCCL_CHECK(ncclAllReduce(t.data_ptr(), t.data_ptr(), t.numel(), to_nccl(t.scalar_type()), to_op(op), comm_, stream_));
   if (postop) {
     TORCH_CHECK(t.scalar_type() == at::kFloat, "test post-op needs fp32 tensors");
-    delay_scale_launch(t.data_ptr<float>(), t.numel(), (float)postop_scale_, postop_delay_us_, stream_);
+    double delay = postop_delay_us_;
+    if (model)
+      delay = postop_alpha_us_ + 2.0 * (postop_w_ - 1) / postop_w_ * (double)t.numel() * 4.0 / (postop_gbps_ * 1e3);
+    delay_scale_launch(t.data_ptr<float>(), t.numel(), (float)postop_scale_, delay, stream_);
   }
   return end(cur, async, {t}, "all_reduce");
 }

@@ -39,6 +39,8 @@ class RcclWork {
   // Block the host until the collective finished (raises on communicator failure / timeout).
   void synchronize();
   bool is_completed();
+  // the completion event (recorded on the communicator stream after the collective)
+  hipEvent_t event() const { return done_->ev; }
 
  private:
   std::shared_ptr<RcclComm> comm_;
@@ -88,6 +90,15 @@ class RcclComm : public std::enable_shared_from_this<RcclComm> {
     postop_delay_us_ = delay_us;
     postop_scale_ = scale;
   }
+  // Modelled-xGMI variant (one GPU standing in for a W-rank node): every all_reduce's post-op
+  // spins alpha_us + 2 (W - 1) / W * bytes / (GBps * 1e3) us -- a ring all-reduce's time at that
+  // per-link bandwidth -- so bucket timelines and overlap can be measured without peers.
+  void set_test_postop_model(double alpha_us, double gbps, int w) {
+    postop_alpha_us_ = alpha_us;
+    postop_gbps_ = gbps;
+    postop_w_ = w;
+    postop_scale_ = 1.0;
+  }
 
   hipEvent_t get_event();
   void put_event(hipEvent_t e);
@@ -103,6 +114,8 @@ class RcclComm : public std::enable_shared_from_this<RcclComm> {
   // a freed comm.
   std::atomic<ncclComm_t> comm_{nullptr};
   double postop_delay_us_ = 0.0, postop_scale_ = 1.0;
+  double postop_alpha_us_ = 0.0, postop_gbps_ = 0.0;
+  int postop_w_ = 0;
   int rank_, world_, device_;
   hipStream_t stream_ = nullptr;
   bool own_stream_ = false;  // created here (destroyed with the communicator), not PyTorch's pool

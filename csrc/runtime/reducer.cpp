@@ -32,6 +32,8 @@
 #include <unordered_set>
 
 #include "../kernels/kernels.h"
+#include "ops.h"
+#include <c10/hip/HIPGuard.h>
 #include <c10/hip/HIPStream.h>
 
 namespace cdp {
@@ -92,7 +94,79 @@ Reducer::Reducer(std::vector<at::Tensor> params, std::vector<at::Tensor> grad_vi
   }
 }
 
-Reducer::~Reducer() { remove_hooks(); }
+Reducer::~Reducer() {
+  remove_hooks();
+  if (step_done_) hipEventDestroy(step_done_);
+  if (step_stream_) {
+    hipStreamSynchronize(step_stream_);
+    hipStreamDestroy(step_stream_);
+  }
+}
+
+void Reducer::set_bucket_step(int64_t b, at::Tensor p, at::Tensor g, c10::optional<at::Tensor> buf,
+                              c10::optional<at::Tensor> lr_t, double lr, double momentum, double dampening, double wd,
+                              bool nesterov, bool first, bool maximize, c10::optional<at::Tensor> desc,
+                              c10::optional<at::Tensor> meta, c10::optional<at::Tensor> amax,
+                              c10::optional<at::Tensor> counter) {
+  std::lock_guard<std::mutex> gl(mu_);
+  TORCH_CHECK(rccl_, "overlapped optimizer step: needs the RCCL communicator (stream-ordered collectives)");
+  TORCH_CHECK(b >= 0 && b < (int64_t)bucket_views_.size(), "set_bucket_step: bad bucket ", b);
+  TORCH_CHECK(g.data_ptr() == bucket_views_[b].data_ptr() && g.numel() == bucket_views_[b].numel(),
+              "set_bucket_step: the gradient range must be bucket ", b, "'s own arena range");
+  TORCH_CHECK(p.is_cuda() && p.numel() == g.numel() && p.is_contiguous(), "set_bucket_step: parameter range");
+  TORCH_CHECK(!desc.has_value() || (meta.has_value() && amax.has_value()), "set_bucket_step: incomplete prep plan");
+  if (steps_.size() != bucket_views_.size()) steps_.assign(bucket_views_.size(), BucketStep{});
+  BucketStep& s = steps_[b];
+  s.set = true;
+  s.p = std::move(p);
+  s.g = std::move(g);
+  s.buf = std::move(buf);
+  s.lr_t = std::move(lr_t);
+  s.lr = lr;
+  s.momentum = momentum;
+  s.dampening = dampening;
+  s.wd = wd;
+  s.nesterov = nesterov;
+  s.first = first;
+  s.maximize = maximize;
+  s.desc = std::move(desc);
+  s.meta = std::move(meta);
+  s.amax = std::move(amax);
+  s.counter = std::move(counter);
+}
+
+// The SGD of bucket b on the step stream, ordered after b's all-reduce (its completion event). The
+// parameters of b are no longer read by this backward: a bucket is launched only after every one of
+// its gradients is ready, i.e. after the backward kernels of those layers (data gradient included,
+// both are enqueued before autograd accumulates the weight gradient) were enqueued on the compute
+// stream, and the all-reduce is ordered after them.
+void Reducer::run_step(int b) {
+  BucketStep& s = steps_[b];
+  const int dev = s.p.get_device();
+  if (!step_stream_) {
+    TORCH_CHECK(hipStreamCreateWithPriority(&step_stream_, hipStreamNonBlocking, 0) == hipSuccess &&
+                    hipEventCreateWithFlags(&step_done_, hipEventDisableTiming) == hipSuccess,
+                "reducer: step stream creation failed");
+  }
+  TORCH_CHECK(hipStreamWaitEvent(step_stream_, works_[b]->event(), 0) == hipSuccess, "reducer: step stream wait");
+  {
+    c10::hip::HIPStreamGuard guard(c10::hip::getStreamFromExternal(step_stream_, (c10::DeviceIndex)dev));
+    if (roctx_) {
+      char name[48];
+      std::snprintf(name, sizeof(name), "cdp.bucket_step[%d]", b);
+      roctxRangePushA(name);
+    }
+    if (s.desc.has_value())
+      sgd_step_prep(s.p, s.g, s.buf, s.lr_t, s.lr, s.momentum, s.dampening, s.wd, 1.0, s.nesterov, s.first, s.maximize,
+                    *s.desc, *s.meta, *s.amax, s.counter);
+    else
+      sgd_step(s.p, s.g, s.buf, s.lr_t, s.lr, s.momentum, s.dampening, s.wd, 1.0, s.nesterov, s.first, s.maximize,
+               s.counter);
+    if (roctx_) roctxRangePop();
+  }
+  if (trace_) log_event("s", (int64_t)b);
+  ++stepped_now_;
+}
 
 void Reducer::log_event(const char* kind, int64_t idx) {
   timespec ts;
@@ -111,6 +185,7 @@ void Reducer::reset_state() {
   std::fill(ready_flag_.begin(), ready_flag_.end(), 0);
   next_launch_ = 0;
   callback_queued_ = false;
+  stepped_now_ = 0;
   for (auto& w : works_) w.reset();
   for (auto& w : pg_works_) w.reset();
 }
@@ -196,6 +271,7 @@ void Reducer::launch(int b) {
   }
   if (rccl_) {
     works_[b] = rccl_->all_reduce(v, average_ ? "avg" : "sum", /*async=*/true);
+    if (b < (int)steps_.size() && steps_[b].set) run_step(b);
   } else {
     std::vector<at::Tensor> ts{v};
     pg_works_[b] = pg_->allreduce(ts);
@@ -240,6 +316,14 @@ void Reducer::finalize() {
   if (rccl_) {
     // all buckets run in order on the communicator stream: waiting on the last one covers them all
     if (!works_.empty() && works_.back()) works_.back()->wait();
+    if (stepped_now_ > 0) {
+      // ... and the bucket steps in order on the step stream: the compute stream (the next forward
+      // reads the stepped weights) waits for the last one
+      const hipStream_t cur = c10::hip::getCurrentHIPStream().stream();
+      TORCH_CHECK(hipEventRecord(step_done_, step_stream_) == hipSuccess &&
+                      hipStreamWaitEvent(cur, step_done_, 0) == hipSuccess,
+                  "reducer: step stream join failed");
+    }
   } else {
     for (size_t b = 0; b < pg_works_.size(); ++b) {
       if (!pg_works_[b]) continue;
@@ -260,6 +344,8 @@ void Reducer::finalize() {
   ++iterations_;
   armed_ = false;
   next_launch_ = 0;
+  stepped_last_ = stepped_now_;
+  steps_.clear();  // registered per backward
 }
 
 std::vector<int64_t> Reducer::ready_order() const {

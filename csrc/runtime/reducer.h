@@ -53,12 +53,41 @@ class Reducer {
   void disarm() {
     std::lock_guard<std::mutex> g(mu_);
     armed_ = false;
+    steps_.clear();
   }
+  // Overlapped optimizer step (opt-in, RCCL path): the SGD of bucket b's arena range is enqueued on
+  // the reducer's own step stream right behind b's all-reduce, so it runs while later buckets are
+  // still being reduced (and backward still computes), instead of after the last one. Registered
+  // per backward (the hyperparameters / first-step flag of that iteration); the end-of-backward
+  // callback orders the compute stream after the last bucket's step and drops the registrations.
+  void set_bucket_step(int64_t b, at::Tensor p, at::Tensor g, c10::optional<at::Tensor> buf,
+                       c10::optional<at::Tensor> lr_t, double lr, double momentum, double dampening, double wd,
+                       bool nesterov, bool first, bool maximize, c10::optional<at::Tensor> desc,
+                       c10::optional<at::Tensor> meta, c10::optional<at::Tensor> amax, c10::optional<at::Tensor> counter);
+  void clear_bucket_steps() {
+    std::lock_guard<std::mutex> g(mu_);
+    steps_.clear();
+  }
+  // buckets whose step ran in the last completed backward
+  int64_t stepped_buckets() const { return stepped_last_; }
 
  private:
   void reset_state();
   void mark_ready_locked(size_t i, bool from_hook);
   void launch(int b);
+  void run_step(int b);
+
+  struct BucketStep {
+    bool set = false;
+    at::Tensor p, g;
+    c10::optional<at::Tensor> buf, lr_t, desc, meta, amax, counter;
+    double lr = 0, momentum = 0, dampening = 0, wd = 0;
+    bool nesterov = false, first = false, maximize = false;
+  };
+  std::vector<BucketStep> steps_;
+  hipStream_t step_stream_ = nullptr;
+  hipEvent_t step_done_ = nullptr;
+  int64_t stepped_now_ = 0, stepped_last_ = 0;
 
   std::vector<at::Tensor> params_, grad_views_, bucket_views_;
   std::shared_ptr<RcclComm> rccl_;
