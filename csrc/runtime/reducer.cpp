@@ -29,6 +29,8 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <tuple>
+#include <unordered_map>
 #include <unordered_set>
 
 #include "../kernels/kernels.h"
@@ -94,14 +96,27 @@ Reducer::Reducer(std::vector<at::Tensor> params, std::vector<at::Tensor> grad_vi
   }
 }
 
-Reducer::~Reducer() {
-  remove_hooks();
-  if (step_done_) hipEventDestroy(step_done_);
-  if (step_stream_) {
-    hipStreamSynchronize(step_stream_);
-    hipStreamDestroy(step_stream_);
-  }
+Reducer::~Reducer() { remove_hooks(); }
+
+namespace {
+// One step stream (and its join event) per device for the process, shared by every reducer: a
+// reducer is re-created when the caller switches streams (rebind_if_stream_changed, e.g. at the start
+// of a hipGraph capture), and destroying or synchronizing a stream there would invalidate the capture.
+std::pair<hipStream_t, hipEvent_t> device_step_stream(int dev) {
+  static std::mutex mu;
+  static std::unordered_map<int, std::pair<hipStream_t, hipEvent_t>> m;
+  std::lock_guard<std::mutex> g(mu);
+  auto it = m.find(dev);
+  if (it != m.end()) return it->second;
+  hipStream_t s = nullptr;
+  hipEvent_t e = nullptr;
+  TORCH_CHECK(hipStreamCreateWithPriority(&s, hipStreamNonBlocking, 0) == hipSuccess &&
+                  hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess,
+              "reducer: step stream creation failed");
+  m[dev] = {s, e};
+  return m[dev];
 }
+}  // namespace
 
 void Reducer::set_bucket_step(int64_t b, at::Tensor p, at::Tensor g, c10::optional<at::Tensor> buf,
                               c10::optional<at::Tensor> lr_t, double lr, double momentum, double dampening, double wd,
@@ -143,11 +158,7 @@ void Reducer::set_bucket_step(int64_t b, at::Tensor p, at::Tensor g, c10::option
 void Reducer::run_step(int b) {
   BucketStep& s = steps_[b];
   const int dev = s.p.get_device();
-  if (!step_stream_) {
-    TORCH_CHECK(hipStreamCreateWithPriority(&step_stream_, hipStreamNonBlocking, 0) == hipSuccess &&
-                    hipEventCreateWithFlags(&step_done_, hipEventDisableTiming) == hipSuccess,
-                "reducer: step stream creation failed");
-  }
+  if (!step_stream_) std::tie(step_stream_, step_done_) = device_step_stream(dev);
   TORCH_CHECK(hipStreamWaitEvent(step_stream_, works_[b]->event(), 0) == hipSuccess, "reducer: step stream wait");
   {
     c10::hip::HIPStreamGuard guard(c10::hip::getStreamFromExternal(step_stream_, (c10::DeviceIndex)dev));
