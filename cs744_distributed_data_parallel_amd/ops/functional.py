@@ -11,6 +11,8 @@ Reference anchors: the VGG block ``Conv2d -> BatchNorm2d -> ReLU [-> MaxPool2d]`
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.nn.functional as F
 
@@ -327,10 +329,17 @@ class _Linear(torch.autograd.Function):
         ctx.save_for_backward(x, w)
         ctx.has_bias = b is not None
         ctx.params = (w, b)
+        ctx.narrow = w.shape[0] <= 16
+        ctx.fused = None  # (dlogits, dx, dw, db) from a loss backward that did this backward too (_XEnt)
         return _native.lib().linear_fwd(x, w, b)
 
     @staticmethod
     def backward(ctx, gy):
+        f, ctx.fused = ctx.fused, None
+        if f is not None and gy.data_ptr() == f[0].data_ptr() and gy._version == f[0]._version:
+            # the incoming gradient IS the cross-entropy gradient the fused launch started from
+            # (with a second consumer of the logits autograd would have summed into a new tensor)
+            return f[1], f[2], f[3]
         x, w = ctx.saved_tensors
         wp, bp = ctx.params
         nig = ctx.needs_input_grad
@@ -350,12 +359,29 @@ class _XEnt(torch.autograd.Function):
     @staticmethod
     def forward(ctx, logits, target):
         ctx.save_for_backward(logits, target)
+        # logits straight from a narrow native Linear (VGG's fc1): its backward rides on ours
+        node = logits.grad_fn
+        ctx.lin = node if (getattr(node, "narrow", False) and hasattr(node, "fused")
+                           and logits.shape[0] * logits.shape[1] <= _XENT_LIN_MAX) else None
         return _native.lib().xent_fwd(logits, target)
 
     @staticmethod
     def backward(ctx, g):
         logits, target = ctx.saved_tensors
+        lin, ctx.lin = ctx.lin, None
+        if lin is not None and os.environ.get("CDP_FUSED_CLASSIFIER", "1") != "0":
+            x, w = lin.saved_tensors
+            wp, bp = lin.params
+            nig = lin.needs_input_grad
+            has_b = lin.has_bias
+            dl, dx, dw, db = _native.lib().xent_linear_bwd(g.reshape(1), logits, target, x, w, nig[0], has_b,
+                                                           _slot(wp, nig[1]), _slot(bp, nig[2] and has_b))
+            lin.fused = (dl, dx if nig[0] else None, dw, db if has_b else None)
+            return dl, None
         return _native.lib().xent_bwd(g.reshape(1), logits, target), None
+
+
+_XENT_LIN_MAX = 8192  # batch x classes held in each block's LDS (csrc kernels.h kXentLinMax)
 
 
 def cross_entropy(logits, target):

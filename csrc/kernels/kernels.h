@@ -285,6 +285,11 @@ void small_linear_fwd_launch(const float* x, const float* w, const float* b, int
                              hipStream_t st);
 void small_linear_bwd_launch(const float* dy, const float* x, const float* w, int B, int I, int O, float* dx, float* dw,
                              float* db, hipStream_t st);
+// CrossEntropy backward + narrow Linear backward in one launch (B * O <= kXentLinMax, O <= 16)
+constexpr int kXentLinMax = 8192;
+void xent_linear_bwd_launch(const float* logits, const long long* tgt, const float* gscale, const float* x,
+                            const float* w, int B, int I, int O, float* dlogits, float* dx, float* dw, float* db,
+                            hipStream_t st);
 void avgpool_fwd_launch(const float* x, int N, int HW, int C, float* y, hipStream_t st);
 void avgpool_bwd_launch(const float* gy, int N, int HW, int C, float* gx, hipStream_t st);
 // NHWC, C % 4 == 0; arg = window-local argmax tap (uint8, k*k <= 255)

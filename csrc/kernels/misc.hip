@@ -660,10 +660,11 @@ __global__ __launch_bounds__(256) void small_linear_fwd_kernel(const float* __re
 //   blocks [nbx, nbx + nbw)  dW[o][i] = sum_r dy[r][o] * x[r][i]       (16 columns x 16 row-lanes per
 //                            block; every thread accumulates all O outputs of its column)
 //   last block               db[o]    = sum_r dy[r][o]
-__global__ __launch_bounds__(256) void small_linear_bwd_kernel(const float* __restrict__ dy, const float* __restrict__ x,
-                                                               const float* __restrict__ w, int B, int I, int O,
-                                                               float* __restrict__ dx, float* __restrict__ dw,
-                                                               float* __restrict__ db, int nbx, int nbw) {
+// (dy: global memory, or the block's LDS copy in xent_linear_bwd_kernel)
+__device__ __forceinline__ void small_linear_bwd_body(const float* __restrict__ dy, const float* __restrict__ x,
+                                                      const float* __restrict__ w, int B, int I, int O,
+                                                      float* __restrict__ dx, float* __restrict__ dw,
+                                                      float* __restrict__ db, int nbx, int nbw) {
   __shared__ float red[16][SL_MAXO][17];
   const int bid = blockIdx.x;
   if (bid < nbx) {
@@ -708,6 +709,55 @@ __global__ __launch_bounds__(256) void small_linear_bwd_kernel(const float* __re
     __syncthreads();
     if (rl == 0 && o < O) db[o] = rdb[0][o] + rdb[1][o] + rdb[2][o] + rdb[3][o];
   }
+}
+
+__global__ __launch_bounds__(256) void small_linear_bwd_kernel(const float* __restrict__ dy, const float* __restrict__ x,
+                                                               const float* __restrict__ w, int B, int I, int O,
+                                                               float* __restrict__ dx, float* __restrict__ dw,
+                                                               float* __restrict__ db, int nbx, int nbw) {
+  small_linear_bwd_body(dy, x, w, B, I, O, dx, dw, db, nbx, nbw);
+}
+
+// The classifier's backward in one launch (CrossEntropyLoss -> Linear(512, 10), the reference's
+// fc1 + criterion, /root/reference/src/Part 1/model.py:40-45 with main.py:39-40,110): every block
+// first forms dlogits = (softmax(logits) - onehot(t)) * gscale / B for all B rows in its LDS (one
+// thread per row, O <= 16 classes), block 0 also stores it (the loss's gradient autograd passes on),
+// then the block does its part of the narrow Linear's three gradients (small_linear_bwd_body). Two
+// launches (xent_bwd, small_linear_bwd) and one kernel boundary less per step.
+__global__ __launch_bounds__(256) void xent_linear_bwd_kernel(const float* __restrict__ logits,
+                                                              const long long* __restrict__ tgt,
+                                                              const float* __restrict__ gscale,
+                                                              const float* __restrict__ x, const float* __restrict__ w,
+                                                              int B, int I, int O, float* __restrict__ dlogits,
+                                                              float* __restrict__ dx, float* __restrict__ dw,
+                                                              float* __restrict__ db, int nbx, int nbw) {
+  __shared__ float sdy[kXentLinMax];
+  const float k = gscale[0] / (float)B;
+  for (int r = threadIdx.x; r < B; r += 256) {
+    const float* row = logits + (long long)r * O;
+    float v[SL_MAXO];
+    float mx = -INFINITY;
+#pragma unroll
+    for (int o = 0; o < SL_MAXO; ++o) {
+      v[o] = o < O ? row[o] : -INFINITY;
+      mx = fmaxf(mx, v[o]);
+    }
+    float se = 0.f;
+#pragma unroll
+    for (int o = 0; o < SL_MAXO; ++o)
+      if (o < O) se += expf(v[o] - mx);
+    const float inv = 1.f / se;
+    const long long t = tgt[r];
+#pragma unroll
+    for (int o = 0; o < SL_MAXO; ++o) {
+      if (o >= O) break;
+      const float d = (expf(v[o] - mx) * inv - (o == t ? 1.f : 0.f)) * k;
+      sdy[r * O + o] = d;
+      if (blockIdx.x == 0) dlogits[(long long)r * O + o] = d;
+    }
+  }
+  __syncthreads();
+  small_linear_bwd_body(sdy, x, w, B, I, O, dx, dw, db, nbx, nbw);
 }
 
 // global average pool over HW of NHWC -> [N][C]; and its backward (32-bit index decode by
@@ -936,6 +986,15 @@ void small_linear_bwd_launch(const float* dy, const float* x, const float* w, in
   const int nbw = (I + 15) / 16;
   hipLaunchKernelGGL(small_linear_bwd_kernel, dim3(nbx + nbw + 1), dim3(256), 0, st, dy, x, w, B, I, O, dx, dw, db,
                      nbx, nbw);
+}
+void xent_linear_bwd_launch(const float* logits, const long long* tgt, const float* gscale, const float* x,
+                            const float* w, int B, int I, int O, float* dlogits, float* dx, float* dw, float* db,
+                            hipStream_t st) {
+  if (O > SL_MAXO || (long long)B * O > kXentLinMax) throw std::runtime_error("xent_linear_bwd: classifier too wide");
+  const int nbx = dx ? (int)(((long long)B * I + 255) / 256) : 0;
+  const int nbw = (I + 15) / 16;
+  hipLaunchKernelGGL(xent_linear_bwd_kernel, dim3(nbx + nbw + 1), dim3(256), 0, st, logits, tgt, gscale, x, w, B, I, O,
+                     dlogits, dx, dw, db, nbx, nbw);
 }
 void avgpool_fwd_launch(const float* x, int N, int HW, int C, float* y, hipStream_t st) {
   if ((long long)N * HW * C >= (1LL << 31)) throw std::runtime_error("avgpool: tensor too large");

@@ -1720,6 +1720,35 @@ at::Tensor xent_bwd(const at::Tensor& gloss, const at::Tensor& logits_, const at
   return d;
 }
 
+// {dlogits, dx, dw, db}: the softmax cross-entropy gradient and, in the same launch, the narrow
+// Linear's three gradients from it (ops/functional.py fuses them when the loss directly consumes
+// the classifier's logits)
+std::vector<at::Tensor> xent_linear_bwd(const at::Tensor& gloss, const at::Tensor& logits_, const at::Tensor& target,
+                                        const at::Tensor& x_, const at::Tensor& w_, bool need_dx, bool has_bias,
+                                        const c10::optional<at::Tensor>& dw_out,
+                                        const c10::optional<at::Tensor>& db_out) {
+  const at::Tensor logits = logits_.contiguous(), x = x_.contiguous(), w = w_.contiguous();
+  const at::Tensor g = gloss.to(at::kFloat).contiguous();
+  const at::Tensor tgt = target.contiguous();
+  check_f32_cuda(logits, "logits");
+  check_f32_cuda(x, "input");
+  const int B = x.size(0), I = x.size(1), O = w.size(0);
+  TORCH_CHECK(logits.size(0) == B && logits.size(1) == O && w.size(1) == I, "xent_linear_bwd: shape mismatch");
+  TORCH_CHECK(O <= 16 && (long long)B * O <= kXentLinMax, "xent_linear_bwd: classifier too wide");
+  TORCH_CHECK(tgt.scalar_type() == at::kLong && tgt.numel() == B, "xent_linear_bwd: int64 target per row");
+  at::Tensor dl = at::empty_like(logits);
+  at::Tensor dx = need_dx ? at::empty({B, I}, x.options()) : at::Tensor();
+  at::Tensor dw = (dw_out.has_value() && dw_out->defined()) ? *dw_out : at::empty({O, I}, x.options());
+  TORCH_CHECK(dw.is_contiguous() && dw.numel() == (int64_t)O * I, "linear dW slot must be contiguous [O, I]");
+  at::Tensor db;
+  if (has_bias) db = (db_out.has_value() && db_out->defined()) ? *db_out : at::empty({O}, x.options());
+  xent_linear_bwd_launch(logits.data_ptr<float>(), reinterpret_cast<const long long*>(tgt.data_ptr<int64_t>()),
+                         g.data_ptr<float>(), x.data_ptr<float>(), w.data_ptr<float>(), B, I, O, dl.data_ptr<float>(),
+                         need_dx ? dx.data_ptr<float>() : nullptr, dw.data_ptr<float>(),
+                         has_bias ? db.data_ptr<float>() : nullptr, cur_stream());
+  return {dl, dx, dw, db};
+}
+
 // ---------------------------------------------------------------- SGD over a flat arena
 long long* counter_ptr(const c10::optional<at::Tensor>& c) {
   if (!(c.has_value() && c->defined())) return nullptr;

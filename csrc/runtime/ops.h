@@ -71,6 +71,10 @@ std::vector<at::Tensor> linear_bwd(const at::Tensor& gy, const at::Tensor& x, co
                                    const c10::optional<at::Tensor>& db_out);
 at::Tensor xent_fwd(const at::Tensor& logits, const at::Tensor& target, const c10::optional<at::Tensor>& correct);
 at::Tensor xent_bwd(const at::Tensor& gloss, const at::Tensor& logits, const at::Tensor& target);
+std::vector<at::Tensor> xent_linear_bwd(const at::Tensor& gloss, const at::Tensor& logits, const at::Tensor& target,
+                                        const at::Tensor& x, const at::Tensor& w, bool need_dx, bool has_bias,
+                                        const c10::optional<at::Tensor>& dw_out,
+                                        const c10::optional<at::Tensor>& db_out);
 std::vector<at::Tensor> sgd_prep_plan(const at::Tensor& flat, int64_t s, int64_t e, const std::vector<at::Tensor>& ws,
                                       const std::vector<bool>& want_t,
                                       const c10::optional<at::Tensor>& amax_out = c10::nullopt,
