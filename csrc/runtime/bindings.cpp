@@ -2,6 +2,10 @@
 #include <torch/csrc/utils/pybind.h>
 #include <torch/extension.h>
 
+#include <execinfo.h>
+#include <signal.h>
+#include <unistd.h>
+
 #include "ops.h"
 #include "rccl_comm.h"
 #include "reducer.h"
@@ -9,7 +13,22 @@
 namespace py = pybind11;
 using namespace cdp;
 
+namespace {
+// Diagnostics (CDP_SEGV_BT=1 at import): print the native stack of a SIGSEGV to stderr, then die
+// with the default action. Host-side only; no debugger attaches to the GPU process.
+void segv_backtrace(int sig) {
+  void* frames[64];
+  const int n = backtrace(frames, 64);
+  const char msg[] = "[cdp] native backtrace:\n";
+  (void)!write(2, msg, sizeof(msg) - 1);
+  backtrace_symbols_fd(frames, n, 2);
+  signal(sig, SIG_DFL);
+  raise(sig);
+}
+}  // namespace
+
 PYBIND11_MODULE(_C, m) {
+  if (const char* bt = std::getenv("CDP_SEGV_BT"); bt && bt[0] == '1') signal(SIGSEGV, segv_backtrace);
   m.doc() = "cs744_distributed_data_parallel_amd native runtime (gfx950 kernels, RCCL comm, reducer)";
   m.attr("ARCH") = "gfx950";
 

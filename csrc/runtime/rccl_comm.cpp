@@ -13,6 +13,8 @@
 #include <torch/extension.h>
 
 #include <cstring>
+#include <map>
+#include <mutex>
 
 #include "../kernels/kernels.h"
 #include <sstream>
@@ -60,6 +62,23 @@ void check_tensor(const at::Tensor& t) {
   TORCH_CHECK(t.is_cuda(), "RCCL collectives need GPU tensors");
   TORCH_CHECK(t.is_contiguous() || t.is_contiguous(at::MemoryFormat::ChannelsLast),
               "RCCL collectives need dense tensors");
+}
+
+// The communicator's stream lives as long as the process (one per device and priority, reused by
+// later communicators): asynchronous collectives recordStream() their buffers on it, so the caching
+// allocator records an event on this stream whenever such a buffer is freed -- possibly after the
+// communicator is gone (e.g. a gradient arena collected at interpreter exit), which on a destroyed
+// stream crashes inside the HIP runtime. PyTorch's own pool streams are never destroyed either.
+hipStream_t process_stream(int device, int priority) {
+  static std::mutex mu;
+  static std::map<std::pair<int, int>, hipStream_t> streams;
+  std::lock_guard<std::mutex> g(mu);
+  auto it = streams.find({device, priority});
+  if (it != streams.end()) return it->second;
+  hipStream_t s = nullptr;
+  HIP_CHECK(hipStreamCreateWithPriority(&s, hipStreamNonBlocking, priority));
+  streams[{device, priority}] = s;
+  return s;
 }
 
 }  // namespace
@@ -116,8 +135,7 @@ RcclComm::RcclComm(const std::string& uid, int rank, int world, int device, doub
   if (stream_kind_ == "own" || stream_kind_ == "low") {
     int lo = 0, hi = 0;
     HIP_CHECK(hipDeviceGetStreamPriorityRange(&lo, &hi));
-    HIP_CHECK(hipStreamCreateWithPriority(&stream_, hipStreamNonBlocking, stream_kind_ == "low" ? lo : 0));
-    own_stream_ = true;
+    stream_ = process_stream(device, stream_kind_ == "low" ? lo : 0);
   } else {
     TORCH_CHECK(stream_kind_ == "pool", "CDP_COMM_STREAM must be own, pool or low");
     stream_ = c10::hip::getStreamFromPool(/*isHighPriority=*/false, (c10::DeviceIndex)device).stream();
@@ -154,7 +172,7 @@ RcclComm::~RcclComm() {
     free_events_.clear();
   }
   if (start_ev_) hipEventDestroy(start_ev_);
-  if (own_stream_ && stream_) hipStreamDestroy(stream_);  // (a pool stream belongs to PyTorch)
+  // (the stream is the process's, see process_stream; a pool stream belongs to PyTorch)
 }
 
 std::string RcclComm::error() const {

@@ -118,7 +118,6 @@ class RcclComm : public std::enable_shared_from_this<RcclComm> {
   int postop_w_ = 0;
   int rank_, world_, device_;
   hipStream_t stream_ = nullptr;
-  bool own_stream_ = false;  // created here (destroyed with the communicator), not PyTorch's pool
   std::string stream_kind_;
   hipEvent_t start_ev_ = nullptr;
   std::mutex mu_;

@@ -101,7 +101,8 @@ Reducer::~Reducer() { remove_hooks(); }
 namespace {
 // One step stream (and its join event) per device for the process, shared by every reducer: a
 // reducer is re-created when the caller switches streams (rebind_if_stream_changed, e.g. at the start
-// of a hipGraph capture), and destroying or synchronizing a stream there would invalidate the capture.
+// of a hipGraph capture), and destroying or synchronizing a stream there would invalidate the capture
+// (and, as for the communicator's stream, a stream must outlive every buffer used on it).
 std::pair<hipStream_t, hipEvent_t> device_step_stream(int dev) {
   static std::mutex mu;
   static std::unordered_map<int, std::pair<hipStream_t, hipEvent_t>> m;
