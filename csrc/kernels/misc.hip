@@ -968,6 +968,12 @@ void timestamp_launch(long long* ts, int idx, hipStream_t st) {
 void delay_scale_launch(float* x, long long n, float a, double delay_us, hipStream_t st) {
   // s_sleep 127 ~ 127*64 cycles ~ 3.4 us at 2.4 GHz
   const int sleeps = (int)(delay_us / 3.4) + 1;
+  if (a == 1.f) {
+    // a pure delay (the modelled all-reduce time): 16 sleeping workgroups, about the CUs an RCCL
+    // all-reduce's channels occupy, so the compute stream keeps the rest of the chip
+    hipLaunchKernelGGL(delay_scale_kernel, dim3(16), dim3(64), 0, st, x, 0LL, a, sleeps);
+    return;
+  }
   hipLaunchKernelGGL(delay_scale_kernel, dim3(grid_for(n)), dim3(256), 0, st, x, n, a, sleeps);
 }
 void scale_launch(float* x, long long n, float a, hipStream_t st) {
