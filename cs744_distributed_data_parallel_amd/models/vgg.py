@@ -83,13 +83,14 @@ class VGG(nn.Module):
             need = [k > 0 or x.requires_grad for k in range(len(self._plan))]
             weights = [layers[ci].weight for ci, _, _ in self._plan]
             wam, wts = CF.weight_prep(weights, need)
-            last = len(self._plan) - 1
             for k, (ci, bi, pool) in enumerate(self._plan):
-                # each block's output feeds only the next block: its BN statistics reduction rides
-                # on that block's backward (CF.conv_bn_act bn_link)
+                # each block's output feeds only the next block -- the last one's only fc1, through
+                # the flatten: its BN statistics reduction rides on that consumer's backward
+                # (CF.conv_bn_act bn_link; for the last block the fused classifier backward)
                 x = CF.conv_bn_act(x, layers[ci], layers[bi], relu=True, pool=pool,
-                                   w_amax=wam[k] if wam is not None else None, w_t=wts[k], bn_link=k < last)
+                                   w_amax=wam[k] if wam is not None else None, w_t=wts[k], bn_link=True)
             y = x.reshape(x.size(0), -1)
+            CF.pass_link(x, y)  # the flatten is a view: the hand-off follows it
             return CF.linear(y, self.fc1.weight, self.fc1.bias)
         y = self.layers(x)
         y = y.reshape(y.size(0), -1)

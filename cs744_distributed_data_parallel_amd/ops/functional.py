@@ -149,6 +149,14 @@ class _BNLink:
 LINK_HANDOFFS = [0]  # BN statistics reductions taken from the consumer block's backward (tests read it)
 
 
+def pass_link(src, view):
+    """Carry ``src``'s BN hand-off tag (:class:`_BNLink`) to ``view``, a view of it (same storage and
+    version counter), e.g. the flatten between a block and the classifier."""
+    tag = getattr(src, "_cdp_bnlink", None)
+    if tag is not None and view.data_ptr() == src.data_ptr():
+        view._cdp_bnlink = tag
+
+
 def _get_link(t):
     tag = getattr(t, "_cdp_bnlink", None)
     if tag is None or tag[1] != t._version:
@@ -331,11 +339,17 @@ class _Linear(torch.autograd.Function):
         ctx.params = (w, b)
         ctx.narrow = w.shape[0] <= 16
         ctx.fused = None  # (dlogits, dx, dw, db) from a loss backward that did this backward too (_XEnt)
+        # the producer of x (VGG's last block, through the flatten) handed over its BN statistics
+        # reduction (_BNLink): the fused classifier backward can make it from the dX it forms
+        ctx.link_in = _get_link(x) if ctx.narrow else None
+        if ctx.link_in is not None:
+            ctx.link_in.consumers += 1
         return _native.lib().linear_fwd(x, w, b)
 
     @staticmethod
     def backward(ctx, gy):
         f, ctx.fused = ctx.fused, None
+        ctx.link_in = None
         if f is not None and gy.data_ptr() == f[0].data_ptr() and gy._version == f[0]._version:
             # the incoming gradient IS the cross-entropy gradient the fused launch started from
             # (with a second consumer of the logits autograd would have summed into a new tensor)
@@ -374,8 +388,15 @@ class _XEnt(torch.autograd.Function):
             wp, bp = lin.params
             nig = lin.needs_input_grad
             has_b = lin.has_bias
-            dl, dx, dw, db = _native.lib().xent_linear_bwd(g.reshape(1), logits, target, x, w, nig[0], has_b,
-                                                           _slot(wp, nig[1]), _slot(bp, nig[2] and has_b))
+            li, lin.link_in = lin.link_in, None
+            link = li is not None and li.consumers == 1 and nig[0] and li.y.shape[2] == li.y.shape[3] == (
+                2 if li.pool else 1)
+            dl, dx, dw, db, part = _native.lib().xent_linear_bwd(
+                g.reshape(1), logits, target, x, w, nig[0], has_b, _slot(wp, nig[1]), _slot(bp, nig[2] and has_b),
+                li.y if link else None, li.stats if link else None, bool(li.pool) if link else False,
+                bool(li.relu) if link else False, li.ps if link else 2)
+            if link:  # the producer block's backward takes these partials if its gradient is this dX
+                li.part, li.gptr, li.gver = part, dx.data_ptr(), dx._version
             lin.fused = (dl, dx if nig[0] else None, dw, db if has_b else None)
             return dl, None
         return _native.lib().xent_bwd(g.reshape(1), logits, target), None

@@ -285,11 +285,20 @@ void small_linear_fwd_launch(const float* x, const float* w, const float* b, int
                              hipStream_t st);
 void small_linear_bwd_launch(const float* dy, const float* x, const float* w, int B, int I, int O, float* dx, float* dw,
                              float* db, hipStream_t st);
-// CrossEntropy backward + narrow Linear backward in one launch (B * O <= kXentLinMax, O <= 16)
+// CrossEntropy backward + narrow Linear backward in one launch (B * O <= kXentLinMax, O <= 16),
+// optionally with the BN backward partials of the block that produced the Linear's input
+// (y != nullptr: that block's pre-BN output [B][pool ? 2x2 : 1x1][C = I] NHWC, stats [4][C],
+// part [1][C][ps] out)
 constexpr int kXentLinMax = 8192;
+struct XentBnLink {
+  const float* y;
+  const float* stats;
+  float* part;
+  int pool, relu, ps;
+};
 void xent_linear_bwd_launch(const float* logits, const long long* tgt, const float* gscale, const float* x,
                             const float* w, int B, int I, int O, float* dlogits, float* dx, float* dw, float* db,
-                            hipStream_t st);
+                            const XentBnLink& lk, hipStream_t st);
 void avgpool_fwd_launch(const float* x, int N, int HW, int C, float* y, hipStream_t st);
 void avgpool_bwd_launch(const float* gy, int N, int HW, int C, float* gx, hipStream_t st);
 // NHWC, C % 4 == 0; arg = window-local argmax tap (uint8, k*k <= 255)

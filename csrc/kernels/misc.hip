@@ -664,9 +664,8 @@ __global__ __launch_bounds__(256) void small_linear_fwd_kernel(const float* __re
 __device__ __forceinline__ void small_linear_bwd_body(const float* __restrict__ dy, const float* __restrict__ x,
                                                       const float* __restrict__ w, int B, int I, int O,
                                                       float* __restrict__ dx, float* __restrict__ dw,
-                                                      float* __restrict__ db, int nbx, int nbw) {
+                                                      float* __restrict__ db, int nbx, int nbw, int bid) {
   __shared__ float red[16][SL_MAXO][17];
-  const int bid = blockIdx.x;
   if (bid < nbx) {
     const long long e = (long long)bid * 256 + threadIdx.x;
     if (e >= (long long)B * I) return;
@@ -715,22 +714,31 @@ __global__ __launch_bounds__(256) void small_linear_bwd_kernel(const float* __re
                                                                const float* __restrict__ w, int B, int I, int O,
                                                                float* __restrict__ dx, float* __restrict__ dw,
                                                                float* __restrict__ db, int nbx, int nbw) {
-  small_linear_bwd_body(dy, x, w, B, I, O, dx, dw, db, nbx, nbw);
+  small_linear_bwd_body(dy, x, w, B, I, O, dx, dw, db, nbx, nbw, blockIdx.x);
 }
 
 // The classifier's backward in one launch (CrossEntropyLoss -> Linear(512, 10), the reference's
 // fc1 + criterion, /root/reference/src/Part 1/model.py:40-45 with main.py:39-40,110): every block
 // first forms dlogits = (softmax(logits) - onehot(t)) * gscale / B for all B rows in its LDS (one
 // thread per row, O <= 16 classes), block 0 also stores it (the loss's gradient autograd passes on),
-// then the block does its part of the narrow Linear's three gradients (small_linear_bwd_body). Two
-// launches (xent_bwd, small_linear_bwd) and one kernel boundary less per step.
+// then the block does its part of the narrow Linear's gradients:
+//   blocks [0, nbx)          16 columns i of dX over all rows (16 row lanes x 16 columns), each
+//                            dX[r][i] = sum_o dy[r][o] W[o][i] in small_linear_bwd_body's order; with a
+//                            BatchNorm link (lk.y != null: the input is the last VGG block's pooled,
+//                            1x1 output, so column i is channel i) the block also reduces that block's
+//                            BN backward partials from the dX it just formed -- sum dz, sum dz * xhat,
+//                            sum xhat over each 2x2 window through max-pool + ReLU, as bn_bwd_reduce --
+//                            into part[0][i][0..ps), so the block's backward takes them instead of a
+//                            statistics launch of its own (ops/functional.py _BNLink)
+//   blocks [nbx, nbx + nbw)  dW, last block db (small_linear_bwd_body)
+// Three launches (xent_bwd, small_linear_bwd, bn_bwd_reduce) and two kernel boundaries less per step.
 __global__ __launch_bounds__(256) void xent_linear_bwd_kernel(const float* __restrict__ logits,
                                                               const long long* __restrict__ tgt,
                                                               const float* __restrict__ gscale,
                                                               const float* __restrict__ x, const float* __restrict__ w,
                                                               int B, int I, int O, float* __restrict__ dlogits,
                                                               float* __restrict__ dx, float* __restrict__ dw,
-                                                              float* __restrict__ db, int nbx, int nbw) {
+                                                              float* __restrict__ db, int nbx, int nbw, XentBnLink lk) {
   __shared__ float sdy[kXentLinMax];
   const float k = gscale[0] / (float)B;
   for (int r = threadIdx.x; r < B; r += 256) {
@@ -757,7 +765,68 @@ __global__ __launch_bounds__(256) void xent_linear_bwd_kernel(const float* __res
     }
   }
   __syncthreads();
-  small_linear_bwd_body(sdy, x, w, B, I, O, dx, dw, db, nbx, nbw);
+  if ((int)blockIdx.x >= nbx) {
+    small_linear_bwd_body(sdy, x, w, B, I, O, nullptr, dw, db, 0, nbw, blockIdx.x - nbx);
+    return;
+  }
+  __shared__ float red[3][16][17];
+  const int col = threadIdx.x & 15, rl = threadIdx.x >> 4;
+  const int i = blockIdx.x * 16 + col;
+  const bool ok = i < I;
+  float wc[SL_MAXO];
+#pragma unroll
+  for (int o = 0; o < SL_MAXO; ++o) wc[o] = ok ? w[(long long)min(o, O - 1) * I + i] : 0.f;
+  float a1 = 0.f, a2 = 0.f, a3 = 0.f;
+  float sc = 0.f, sh = 0.f, mu = 0.f, is = 0.f;
+  const bool link = lk.y != nullptr && ok;
+  if (link) {
+    mu = lk.stats[i];
+    is = lk.stats[I + i];
+    sc = lk.stats[2 * I + i];
+    sh = lk.stats[3 * I + i];
+  }
+  for (int r = rl; r < B && ok; r += 16) {
+    float s = 0.f;
+    for (int o = 0; o < O; ++o) s = fmaf(sdy[r * O + o], wc[o], s);
+    dx[(long long)r * I + i] = s;
+    if (link) {
+      // the block's 2x2 pre-BN window of channel i (lk.H = lk.W = 2) or its single pixel
+      const int np = lk.pool ? 4 : 1;
+      float yv[4], z[4], d[4];
+      for (int p = 0; p < np; ++p) {
+        yv[p] = lk.y[((long long)r * np + p) * I + i];  // NHWC, pixels (0,0),(0,1),(1,0),(1,1)
+        z[p] = fmaf(yv[p], sc, sh);
+        if (lk.relu) z[p] = fmaxf(z[p], 0.f);
+      }
+      if (lk.pool) {
+        int arg = 0;
+        float m = z[0];
+        if (z[1] > m) { m = z[1]; arg = 1; }
+        if (z[2] > m) { m = z[2]; arg = 2; }
+        if (z[3] > m) { m = z[3]; arg = 3; }
+        const float gg = (!lk.relu || m > 0.f) ? s : 0.f;
+        for (int p = 0; p < 4; ++p) d[p] = arg == p ? gg : 0.f;
+      } else {
+        d[0] = (!lk.relu || z[0] > 0.f) ? s : 0.f;
+      }
+      for (int p = 0; p < np; ++p) {
+        const float xh = (yv[p] - mu) * is;
+        a1 += d[p];
+        a2 += d[p] * xh;
+        a3 += xh;
+      }
+    }
+  }
+  if (lk.y == nullptr) return;  // (uniform over the block)
+  red[0][rl][col] = a1;
+  red[1][rl][col] = a2;
+  red[2][rl][col] = a3;
+  __syncthreads();
+  if (rl < lk.ps && ok) {
+    float t = 0.f;
+    for (int q = 0; q < 16; ++q) t += red[rl][q][col];
+    lk.part[(long long)i * lk.ps + rl] = t;
+  }
 }
 
 // global average pool over HW of NHWC -> [N][C]; and its backward (32-bit index decode by
@@ -995,12 +1064,13 @@ void small_linear_bwd_launch(const float* dy, const float* x, const float* w, in
 }
 void xent_linear_bwd_launch(const float* logits, const long long* tgt, const float* gscale, const float* x,
                             const float* w, int B, int I, int O, float* dlogits, float* dx, float* dw, float* db,
-                            hipStream_t st) {
+                            const XentBnLink& lk, hipStream_t st) {
   if (O > SL_MAXO || (long long)B * O > kXentLinMax) throw std::runtime_error("xent_linear_bwd: classifier too wide");
-  const int nbx = dx ? (int)(((long long)B * I + 255) / 256) : 0;
+  if (lk.y && (!dx || lk.ps < 2 || lk.ps > 3)) throw std::runtime_error("xent_linear_bwd: BN link needs dX");
+  const int nbx = dx ? (I + 15) / 16 : 0;
   const int nbw = (I + 15) / 16;
   hipLaunchKernelGGL(xent_linear_bwd_kernel, dim3(nbx + nbw + 1), dim3(256), 0, st, logits, tgt, gscale, x, w, B, I, O,
-                     dlogits, dx, dw, db, nbx, nbw);
+                     dlogits, dx, dw, db, nbx, nbw, lk);
 }
 void avgpool_fwd_launch(const float* x, int N, int HW, int C, float* y, hipStream_t st) {
   if ((long long)N * HW * C >= (1LL << 31)) throw std::runtime_error("avgpool: tensor too large");

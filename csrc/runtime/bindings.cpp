@@ -87,7 +87,10 @@ PYBIND11_MODULE(_C, m) {
   m.def("xent_bwd", &xent_bwd);
   m.def("xent_linear_bwd", &xent_linear_bwd, py::arg("gloss"), py::arg("logits"), py::arg("target"), py::arg("x"),
         py::arg("w"), py::arg("need_dx"), py::arg("has_bias"), py::arg("dw_out") = py::none(),
-        py::arg("db_out") = py::none(), "CrossEntropy backward + narrow Linear backward in one launch");
+        py::arg("db_out") = py::none(), py::arg("link_y") = py::none(), py::arg("link_stats") = py::none(),
+        py::arg("link_pool") = false, py::arg("link_relu") = false, py::arg("link_ps") = 2,
+        "CrossEntropy backward + narrow Linear backward in one launch (+ the BN backward partials of the block "
+        "that produced the Linear's input, link_*): {dlogits, dx, dw, db, part}");
   m.def("sgd_step", &sgd_step, py::arg("p"), py::arg("g"), py::arg("buf"), py::arg("lr_t"), py::arg("lr"),
         py::arg("momentum"), py::arg("dampening"), py::arg("wd"), py::arg("grad_scale"), py::arg("nesterov"),
         py::arg("first"), py::arg("maximize"), py::arg("counter") = py::none());

@@ -1725,8 +1725,10 @@ at::Tensor xent_bwd(const at::Tensor& gloss, const at::Tensor& logits_, const at
 // the classifier's logits)
 std::vector<at::Tensor> xent_linear_bwd(const at::Tensor& gloss, const at::Tensor& logits_, const at::Tensor& target,
                                         const at::Tensor& x_, const at::Tensor& w_, bool need_dx, bool has_bias,
-                                        const c10::optional<at::Tensor>& dw_out,
-                                        const c10::optional<at::Tensor>& db_out) {
+                                        const c10::optional<at::Tensor>& dw_out, const c10::optional<at::Tensor>& db_out,
+                                        const c10::optional<at::Tensor>& link_y,
+                                        const c10::optional<at::Tensor>& link_stats, bool link_pool, bool link_relu,
+                                        int64_t link_ps) {
   const at::Tensor logits = logits_.contiguous(), x = x_.contiguous(), w = w_.contiguous();
   const at::Tensor g = gloss.to(at::kFloat).contiguous();
   const at::Tensor tgt = target.contiguous();
@@ -1742,11 +1744,28 @@ std::vector<at::Tensor> xent_linear_bwd(const at::Tensor& gloss, const at::Tenso
   TORCH_CHECK(dw.is_contiguous() && dw.numel() == (int64_t)O * I, "linear dW slot must be contiguous [O, I]");
   at::Tensor db;
   if (has_bias) db = (db_out.has_value() && db_out->defined()) ? *db_out : at::empty({O}, x.options());
+  XentBnLink lk{nullptr, nullptr, nullptr, 0, 0, 2};
+  at::Tensor part;
+  if (link_y.has_value() && link_y->defined()) {
+    // the block that produced x: pre-BN output y [B, C = I, 2, 2] (pooled to 1x1) or [B, I, 1, 1]
+    const at::Tensor& yb = *link_y;
+    check_f32_cuda(yb, "link y");
+    const int hw = link_pool ? 2 : 1;
+    TORCH_CHECK(need_dx && yb.dim() == 4 && yb.size(0) == B && yb.size(1) == I && yb.size(2) == hw &&
+                    yb.size(3) == hw && yb.is_contiguous(at::MemoryFormat::ChannelsLast),
+                "xent_linear_bwd: BN link needs the block's channels_last [B, I, ", hw, ", ", hw, "] output");
+    TORCH_CHECK(link_stats.has_value() && link_stats->is_cuda() && link_stats->numel() == 4LL * I &&
+                    link_stats->is_contiguous() && (link_ps == 2 || link_ps == 3),
+                "xent_linear_bwd: BN link stats [4, C] and ps in {2, 3}");
+    part = at::empty({1, I, link_ps}, x.options());
+    lk = XentBnLink{yb.data_ptr<float>(), link_stats->data_ptr<float>(), part.data_ptr<float>(), link_pool ? 1 : 0,
+                    link_relu ? 1 : 0, (int)link_ps};
+  }
   xent_linear_bwd_launch(logits.data_ptr<float>(), reinterpret_cast<const long long*>(tgt.data_ptr<int64_t>()),
                          g.data_ptr<float>(), x.data_ptr<float>(), w.data_ptr<float>(), B, I, O, dl.data_ptr<float>(),
                          need_dx ? dx.data_ptr<float>() : nullptr, dw.data_ptr<float>(),
-                         has_bias ? db.data_ptr<float>() : nullptr, cur_stream());
-  return {dl, dx, dw, db};
+                         has_bias ? db.data_ptr<float>() : nullptr, lk, cur_stream());
+  return {dl, dx, dw, db, part};
 }
 
 // ---------------------------------------------------------------- SGD over a flat arena

@@ -73,8 +73,10 @@ at::Tensor xent_fwd(const at::Tensor& logits, const at::Tensor& target, const c1
 at::Tensor xent_bwd(const at::Tensor& gloss, const at::Tensor& logits, const at::Tensor& target);
 std::vector<at::Tensor> xent_linear_bwd(const at::Tensor& gloss, const at::Tensor& logits, const at::Tensor& target,
                                         const at::Tensor& x, const at::Tensor& w, bool need_dx, bool has_bias,
-                                        const c10::optional<at::Tensor>& dw_out,
-                                        const c10::optional<at::Tensor>& db_out);
+                                        const c10::optional<at::Tensor>& dw_out, const c10::optional<at::Tensor>& db_out,
+                                        const c10::optional<at::Tensor>& link_y = c10::nullopt,
+                                        const c10::optional<at::Tensor>& link_stats = c10::nullopt,
+                                        bool link_pool = false, bool link_relu = false, int64_t link_ps = 2);
 std::vector<at::Tensor> sgd_prep_plan(const at::Tensor& flat, int64_t s, int64_t e, const std::vector<at::Tensor>& ws,
                                       const std::vector<bool>& want_t,
                                       const c10::optional<at::Tensor>& amax_out = c10::nullopt,

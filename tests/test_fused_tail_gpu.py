@@ -66,3 +66,38 @@ def test_fused_classifier_falls_back_when_logits_have_a_second_consumer(monkeypa
     (F.cross_entropy(ld, t) + ld.square().mean()).backward()
     torch.testing.assert_close(x.grad.double(), xd.grad, rtol=1e-5, atol=1e-7)
     torch.testing.assert_close(w.grad.double(), wd.grad, rtol=1e-5, atol=1e-7)
+
+
+@pytest.mark.parametrize("B", [32, 256])
+def test_vgg11_fused_classifier_takes_the_last_blocks_bn_reduction(B, monkeypatch):
+    """In a VGG-11 step the fused classifier backward also reduces the last block's BN backward
+    statistics from the dX it forms (one hand-off more than with the unfused classifier), and every
+    gradient matches the unfused path's."""
+    import cs744_distributed_data_parallel_amd as cdp
+    from cs744_distributed_data_parallel_amd.ops import functional as CF
+
+    torch.manual_seed(0)
+    model = cdp.VGG11().cuda()
+    g = torch.Generator(device="cuda").manual_seed(B)
+    x = torch.randn(B, 3, 32, 32, device="cuda", generator=g).contiguous(memory_format=torch.channels_last)
+    t = torch.randint(0, 10, (B,), device="cuda", generator=g)
+    crit = cdp.CrossEntropyLoss()
+
+    def grads(fused):
+        monkeypatch.setenv("CDP_FUSED_CLASSIFIER", "1" if fused else "0")
+        model.zero_grad(set_to_none=True)
+        n0 = CF.LINK_HANDOFFS[0]
+        crit(model(x), t).backward()
+        torch.cuda.synchronize()
+        return [p.grad.detach().clone() for p in model.parameters()], CF.LINK_HANDOFFS[0] - n0
+
+    g_f, h_f = grads(True)
+    g_u, h_u = grads(False)
+    assert h_f == h_u + 1, (h_f, h_u)
+    names = [n for n, _ in model.named_parameters()]
+    for name, a, b in zip(names, g_f, g_u):
+        if name.startswith("layers.") and name.endswith(".bias") and isinstance(
+                model.layers[int(name.split(".")[1])], torch.nn.Conv2d):
+            continue  # conv bias before training-mode BN: analytically zero, rounding noise
+        err = ((a - b).norm() / b.norm().clamp_min(1e-30)).item()
+        assert err < 1e-5, (name, err)
