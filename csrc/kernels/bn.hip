@@ -15,7 +15,6 @@
 // All element kernels move float4 along C (C % 4 == 0).
 #include <algorithm>
 #include <cstdlib>
-#include <stdexcept>
 
 #include "act_max.h"
 #include "common.h"
@@ -320,154 +319,6 @@ __global__ __launch_bounds__(256) void bn_fin_act_kernel(const float* __restrict
     sam.add_ch4(4 * cq, cm);
     __syncthreads();
     sam.publish(am, img0, N, cg * CG, CG, C, blockIdx.x % kActCopies, tid, 256);
-  }
-}
-
-// Split-K reduction + BatchNorm finalize + apply in ONE launch, for the layers whose GEMM splits K
-// and whose output is small (the deep VGG layers at small batches: 2x2 .. 8x8 maps): a block owns
-// CG = 4 CQ channels over ALL output rows, so it holds its channels' statistics outright -- no
-// partials, no merge, no separate reduction launch (one launch instead of splitk_reduce4 +
-// bn_fin_act per layer, and one kernel boundary less). Thread rl takes a contiguous run of (pooled)
-// rows, so every pixel it reads back is one it wrote itself:
-//   pass 1  y = sum_s slab[s] + bias, splitk_reduce4's summation order (bitwise its y), stored for
-//           the backward; fp64 sum per channel -> mean
-//   pass 2  M2 = sum (y - mean)^2 over the thread's own y (re-read, L2-resident) -> biased variance
-//   the block publishes stats and the running statistics (bn_finalize_kernel's formulas), then
-//   pass 3  out = [pool2](relu(y * scale + shift)) with the per-image / per-channel |max| (act_max.h).
-template <int CQ, bool POOL>
-__global__ __launch_bounds__(256) void splitk_fin_act_kernel(const float* __restrict__ slab, int S,
-                                                             const float* __restrict__ bias,
-                                                             const float* __restrict__ gamma,
-                                                             const float* __restrict__ beta, float* running_mean,
-                                                             float* running_var, long long* nbt, float momentum,
-                                                             float eps, float* __restrict__ stats, float* y,
-                                                             float* __restrict__ out, int N, int H, int W, int C,
-                                                             int relu, FastDiv fd_HWo, ActMaxOut am, PoolDiv pd) {
-  constexpr int pool = POOL ? 1 : 0;
-  constexpr int CG = 4 * CQ, RL = 256 / CQ;
-  constexpr int NP = POOL ? 4 : 1;  // pixels per (pooled) row
-  __shared__ double red[RL][CG];
-  __shared__ double s_mean[CG];
-  __shared__ float s_sc[CG], s_sh[CG];
-  __shared__ ActMaxBlock<CG> sam;
-  const int tid = threadIdx.x;
-  const int cq = tid % CQ, rl = tid / CQ;
-  const int c0 = blockIdx.x * CG, n0 = c0 + 4 * cq;
-  const int Ho = pool ? H / 2 : H, Wo = pool ? W / 2 : W;
-  const int M = N * H * W;
-  const int rows = N * Ho * Wo;
-  const int per = (rows + RL - 1) / RL;
-  const int r0 = rl * per, r1 = min(rows, r0 + per);
-  const long long plane = (long long)M * C;
-  const bool want = am.img != nullptr;
-  if (want) sam.init(tid, 256);
-  const float4 bv = bias ? ld4(bias + n0) : f4zero();
-  auto pix_off = [&](int r, int p) -> long long {  // element offset of pixel p of (pooled) row r, channel n0
-    if (!pool) return (long long)r * C + n0;
-    int n, ho, wo;
-    pool_decode(r, Wo, Ho, pd, n, ho, wo);
-    return (((long long)n * H + 2 * ho + (p >> 1)) * W + 2 * wo + (p & 1)) * C + n0;
-  };
-  // pass 1
-  double s1[4] = {0.0, 0.0, 0.0, 0.0};
-  for (int r = r0; r < r1; ++r) {
-#pragma unroll
-    for (int p = 0; p < NP; ++p) {
-      const long long o = pix_off(r, p);
-      float4 a = f4zero();
-      for (int z0 = 0; z0 < S; z0 += 8) {
-        float4 t[8];
-#pragma unroll
-        for (int k = 0; k < 8; ++k) t[k] = z0 + k < S ? ld4(slab + (long long)(z0 + k) * plane + o) : f4zero();
-        a.x += ((t[0].x + t[1].x) + (t[2].x + t[3].x)) + ((t[4].x + t[5].x) + (t[6].x + t[7].x));
-        a.y += ((t[0].y + t[1].y) + (t[2].y + t[3].y)) + ((t[4].y + t[5].y) + (t[6].y + t[7].y));
-        a.z += ((t[0].z + t[1].z) + (t[2].z + t[3].z)) + ((t[4].z + t[5].z) + (t[6].z + t[7].z));
-        a.w += ((t[0].w + t[1].w) + (t[2].w + t[3].w)) + ((t[4].w + t[5].w) + (t[6].w + t[7].w));
-      }
-      a.x += bv.x; a.y += bv.y; a.z += bv.z; a.w += bv.w;
-      st4(y + o, a);
-      s1[0] += a.x; s1[1] += a.y; s1[2] += a.z; s1[3] += a.w;
-    }
-  }
-#pragma unroll
-  for (int e = 0; e < 4; ++e) red[rl][4 * cq + e] = s1[e];
-  __syncthreads();
-  if (tid < CG) {
-    double t = 0.0;
-    for (int k = 0; k < RL; ++k) t += red[k][tid];
-    s_mean[tid] = t / (double)M;
-  }
-  __syncthreads();
-  // pass 2
-  double mu[4], s2[4] = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-  for (int e = 0; e < 4; ++e) mu[e] = s_mean[4 * cq + e];
-  for (int r = r0; r < r1; ++r) {
-#pragma unroll
-    for (int p = 0; p < NP; ++p) {
-      const float4 v = ld4(y + pix_off(r, p));
-      const double d0 = v.x - mu[0], d1 = v.y - mu[1], d2 = v.z - mu[2], d3 = v.w - mu[3];
-      s2[0] += d0 * d0; s2[1] += d1 * d1; s2[2] += d2 * d2; s2[3] += d3 * d3;
-    }
-  }
-#pragma unroll
-  for (int e = 0; e < 4; ++e) red[rl][4 * cq + e] = s2[e];
-  __syncthreads();
-  if (tid < CG) {
-    const int c = c0 + tid;
-    double m2 = 0.0;
-    for (int k = 0; k < RL; ++k) m2 += red[k][tid];
-    const double mean = s_mean[tid];
-    const double var = m2 / (double)M;
-    const float invstd = (float)(1.0 / sqrt(var + (double)eps));
-    const float g = gamma ? gamma[c] : 1.f;
-    const float bb = beta ? beta[c] : 0.f;
-    const float scale = g * invstd;
-    const float shift = bb - (float)mean * scale;
-    s_sc[tid] = scale;
-    s_sh[tid] = shift;
-    stats[c] = (float)mean;
-    stats[C + c] = invstd;
-    stats[2 * C + c] = scale;
-    stats[3 * C + c] = shift;
-    if (running_mean) {
-      float f = momentum;
-      if (f < 0.f) f = 1.f / (float)(nbt[0] + 1);  // momentum=None: cumulative average
-      const double unb = M > 1 ? m2 / (double)(M - 1) : var;
-      running_mean[c] = (1.f - f) * running_mean[c] + f * (float)mean;
-      running_var[c] = (1.f - f) * running_var[c] + f * (float)unb;
-    }
-    if (c == 0 && nbt) nbt[0] += 1;
-  }
-  __syncthreads();
-  // pass 3
-  const float4 sc = make_float4(s_sc[4 * cq], s_sc[4 * cq + 1], s_sc[4 * cq + 2], s_sc[4 * cq + 3]);
-  const float4 sh = make_float4(s_sh[4 * cq], s_sh[4 * cq + 1], s_sh[4 * cq + 2], s_sh[4 * cq + 3]);
-  ImgRun run;
-  float4 cm = f4zero();
-  const int img0 = 0;
-  for (int r = r0; r < r1; ++r) {
-    float4 z = affine_act(ld4(y + pix_off(r, 0)), sc, sh, relu);
-    if (pool) {
-      const float4 z1 = affine_act(ld4(y + pix_off(r, 1)), sc, sh, relu);
-      const float4 z2 = affine_act(ld4(y + pix_off(r, 2)), sc, sh, relu);
-      const float4 z3 = affine_act(ld4(y + pix_off(r, 3)), sc, sh, relu);
-      z.x = fmaxf(fmaxf(z.x, z1.x), fmaxf(z2.x, z3.x));
-      z.y = fmaxf(fmaxf(z.y, z1.y), fmaxf(z2.y, z3.y));
-      z.z = fmaxf(fmaxf(z.z, z1.z), fmaxf(z2.z, z3.z));
-      z.w = fmaxf(fmaxf(z.w, z1.w), fmaxf(z2.w, z3.w));
-    }
-    st4(out + (long long)r * C + n0, z);
-    if (want) {
-      run.add(fdiv(r, fd_HWo), absmax4(z), sam, img0, am);
-      cm = absmax4(cm, z);
-    }
-  }
-  if (want) {
-    run.flush(sam, img0, am);
-    sam.add_ch4(4 * cq, cm);
-    __syncthreads();
-    sam.publish(am, img0, N, c0, CG, C, blockIdx.x % kActCopies, tid, 256);
   }
 }
 
@@ -1229,22 +1080,6 @@ void bn_fin_act_launch(const float* part, int nparts, int rpp, int C, const floa
                      exp_merge_parts(nparts), rpp, M, C, gamma, beta, running_mean, running_var, nbt, momentum, eps, stats, y, out, N,
                      H, W, relu ? 1 : 0, grid / (C / cg),
                      make_fastdiv(out_pixels_per_image(H, W, pool)), am, make_pooldiv(W / 2, H / 2));
-}
-
-bool splitk_fin_act_ok(int N, int H, int W, int C, bool pool) {
-  return (C % 4) == 0 && (long long)N * H * W <= kSplitkFinMaxRows && !(pool && ((H & 1) || (W & 1)));
-}
-
-void splitk_fin_act_launch(const float* slab, int S, const float* bias, const float* gamma, const float* beta,
-                           float* running_mean, float* running_var, long long* nbt, float momentum, float eps,
-                           float* stats, float* y, float* out, int N, int H, int W, int C, bool pool, bool relu,
-                           ActMaxOut am, hipStream_t st) {
-  if (!splitk_fin_act_ok(N, H, W, C, pool)) throw std::runtime_error("splitk_fin_act: shape not supported");
-  constexpr int CQ = 1;
-  auto k = pool ? splitk_fin_act_kernel<CQ, true> : splitk_fin_act_kernel<CQ, false>;
-  hipLaunchKernelGGL(k, dim3(C / (4 * CQ)), dim3(256), 0, st, slab, S, bias, gamma, beta, running_mean, running_var, nbt, momentum, eps,
-                     stats, y, out, N, H, W, C, relu ? 1 : 0, make_fastdiv(out_pixels_per_image(H, W, pool)), am,
-                     make_pooldiv(W / 2, H / 2));
 }
 
 bool bn_bwd_fin_apply_ok(int nparts, int C, int H, int W, bool pool) {

@@ -219,14 +219,6 @@ void bn_eval_stats_launch(int C, const float* gamma, const float* beta, const fl
 // operand scales.
 // finalize + apply in one launch (training, no residual, nparts <= 128, C % 64 == 0)
 bool bn_fin_act_ok(int nparts, int C, bool residual);
-// split-K GEMM slabs -> y, BatchNorm statistics and [pool2](relu(BN(y))) in one launch (bn.hip
-// splitk_fin_act_kernel): training mode, no residual, at most kSplitkFinMaxRows output pixels
-constexpr long long kSplitkFinMaxRows = 16384;
-bool splitk_fin_act_ok(int N, int H, int W, int C, bool pool);
-void splitk_fin_act_launch(const float* slab, int S, const float* bias, const float* gamma, const float* beta,
-                           float* running_mean, float* running_var, long long* nbt, float momentum, float eps,
-                           float* stats, float* y, float* out, int N, int H, int W, int C, bool pool, bool relu,
-                           ActMaxOut am, hipStream_t st);
 int bn_fin_act_grid(int N, int H, int W, int C, bool pool, int nparts = 0);  // nparts 0: 64-channel blocks
 void bn_fin_act_launch(const float* part, int nparts, int rpp, int C, const float* gamma, const float* beta,
                        float* running_mean, float* running_var, long long* nbt, float momentum, float eps,

@@ -952,24 +952,9 @@ std::string get_conv_gemm() {
 // ---------------------------------------------------------------- conv forward
 // Returns y (channels_last [N, Cout, P, Q]). When `part` is requested the per-tile BatchNorm
 // partials are returned in a second tensor [nparts, Cout, 2] together with rows-per-part.
-// With `slab_out` (internal, conv_bn_act_fwd): a split-K plan leaves its partial products in
-// *slab_out ([splits, M, Cout], no bias) and launches no reduction -- y is allocated, not written --
-// for a consumer that reduces them itself (splitk_fin_act); *slab_out stays undefined without split-K.
-static std::vector<at::Tensor> conv2d_fwd_core(const at::Tensor& x_, const at::Tensor& w_,
-                                               const c10::optional<at::Tensor>& bias, int64_t stride, int64_t pad,
-                                               bool want_stats, const c10::optional<at::Tensor>& x_amax,
-                                               const c10::optional<at::Tensor>& w_amax, at::Tensor* slab_out);
-
 std::vector<at::Tensor> conv2d_fwd(const at::Tensor& x_, const at::Tensor& w_, const c10::optional<at::Tensor>& bias,
                                    int64_t stride, int64_t pad, bool want_stats, const c10::optional<at::Tensor>& x_amax,
                                    const c10::optional<at::Tensor>& w_amax) {
-  return conv2d_fwd_core(x_, w_, bias, stride, pad, want_stats, x_amax, w_amax, nullptr);
-}
-
-static std::vector<at::Tensor> conv2d_fwd_core(const at::Tensor& x_, const at::Tensor& w_,
-                                               const c10::optional<at::Tensor>& bias, int64_t stride, int64_t pad,
-                                               bool want_stats, const c10::optional<at::Tensor>& x_amax,
-                                               const c10::optional<at::Tensor>& w_amax, at::Tensor* slab_out) {
   check_f32_cuda(x_, "x");
   check_f32_cuda(w_, "weight");
   TORCH_CHECK(x_.dim() == 4 && w_.dim() == 4, "conv2d_fwd expects 4-D input and weight");
@@ -1000,15 +985,6 @@ static std::vector<at::Tensor> conv2d_fwd_core(const at::Tensor& x_, const at::T
   set_scales(p, xa, wa, false, Co, C);
   p.y = y.data_ptr<float>();
   p.bias = fptr(bias);
-  if (slab_out && g.splits > 1) {
-    at::Tensor slab = at::empty({g.splits, M, Co}, opts);
-    p.y = slab.data_ptr<float>();
-    p.bias = nullptr;
-    p.splits = g.splits;
-    conv_launch(p, g.bm, g.bn, false, st);
-    *slab_out = slab;
-    return {y};
-  }
   // BN partials: one per BM-row tile (splits == 1) or per reduction row block (split-K)
   std::function<float*(int)> alloc_part;
   if (want_stats)
@@ -1301,12 +1277,6 @@ static bool exp_skip_bn_apply() {
   const char* e = std::getenv("CDP_EXP_SKIP_BN_APPLY");
   return e && e[0] == '1';
 }
-// CDP_SPLITK_FIN=0: split-K reduction and BN finalize + apply as two launches (A/B)
-static bool splitk_fin_enabled() {
-  const char* e = std::getenv("CDP_SPLITK_FIN");
-  return !(e && e[0] == '0');
-}
-
 static bool bn_fin_enabled(bool bwd = false) {
   const char* e = std::getenv(bwd ? "CDP_BN_BWD_FIN" : "CDP_BN_FIN_ACT");
   return !(e && e[0] == '0');
@@ -1349,40 +1319,14 @@ std::vector<at::Tensor> conv_bn_act_fwd(const at::Tensor& x, const at::Tensor& w
                                      : padc ? c10::optional<at::Tensor>() : x_amax,
                                 cur_stream());
   const at::Tensor wa = weight_max(win, padc ? c10::optional<at::Tensor>() : w_amax);
-  const bool has_res = (residual.has_value() && residual->defined()) || lazy_res;
-  // the split-K reduction, the BatchNorm statistics and the apply in one launch (splitk_fin_act)
-  // when the GEMM splits K and the output is small: the deep layers at small batches
-  const int Ho_ = (int)((x.size(2) + 2 * pad - w.size(2)) / stride + 1), Wo_ = (int)((x.size(3) + 2 * pad - w.size(3)) / stride + 1);
-  const bool try_sfa = training && !has_res && !defer_apply && splitk_fin_enabled() &&
-                       splitk_fin_act_ok((int)x.size(0), Ho_, Wo_, (int)w.size(0), pool) && !exp_skip_bn_apply();
-  at::Tensor slab;
-  std::vector<at::Tensor> r = conv2d_fwd_core(xin, win, b, stride, pad, training, xa, wa, try_sfa ? &slab : nullptr);
+  std::vector<at::Tensor> r = conv2d_fwd(xin, win, b, stride, pad, training, xa, wa);
   at::Tensor y = r[0];
   const int N = y.size(0), C = y.size(1), H = y.size(2), W = y.size(3);
   TORCH_CHECK(C % 4 == 0, "BatchNorm channel count must be a multiple of 4");
   auto opts = y.options();
   at::Tensor stats = at::empty({4, C}, opts);
   hipStream_t st = cur_stream();
-  if (slab.defined()) {
-    long long* nbt_ = nullptr;
-    if (num_batches_tracked.has_value() && num_batches_tracked->defined()) {
-      TORCH_CHECK(num_batches_tracked->scalar_type() == at::kLong, "num_batches_tracked must be int64");
-      nbt_ = reinterpret_cast<long long*>(num_batches_tracked->data_ptr<int64_t>());
-    }
-    at::Tensor out = at::empty({N, C, pool ? H / 2 : H, pool ? W / 2 : W},
-                               opts.memory_format(at::MemoryFormat::ChannelsLast));
-    at::Tensor out_amax;
-    ActMaxOut am{nullptr, nullptr};
-    if (f16x2_mode()) {
-      out_amax = new_act_max(N, C, out, st);
-      am = act_out(out_amax, N);
-    }
-    splitk_fin_act_launch(slab.data_ptr<float>(), (int)slab.size(0), fptr(b), fptr(gamma), fptr(beta),
-                          fptr_mut(running_mean), fptr_mut(running_var), nbt_, (float)momentum, (float)eps,
-                          stats.data_ptr<float>(), y.data_ptr<float>(), out.data_ptr<float>(), N, H, W, C, pool, relu,
-                          am, st);
-    return {out, y, stats, xin, out_amax, xa, wa, at::Tensor()};
-  }
+  const bool has_res = (residual.has_value() && residual->defined()) || lazy_res;
   TORCH_CHECK(!(lazy_res && residual.has_value() && residual->defined()), "conv_bn_act_fwd: residual or res_y, not both");
   // few statistics partials (the deep layers): finalize and apply in one launch (bn_fin_act_kernel)
   bool fused_fin = false;
