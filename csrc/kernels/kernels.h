@@ -290,6 +290,8 @@ void small_linear_bwd_launch(const float* dy, const float* x, const float* w, in
 // (y != nullptr: that block's pre-BN output [B][pool ? 2x2 : 1x1][C = I] NHWC, stats [4][C],
 // part [1][C][ps] out)
 constexpr int kXentLinMax = 8192;
+constexpr int kXentLinRows = 32;  // dX rows per block (and per BN partial)
+inline int xent_lin_chunks(int B) { return (B + kXentLinRows - 1) / kXentLinRows; }
 struct XentBnLink {
   const float* y;
   const float* stats;

@@ -722,13 +722,13 @@ __global__ __launch_bounds__(256) void small_linear_bwd_kernel(const float* __re
 // first forms dlogits = (softmax(logits) - onehot(t)) * gscale / B for all B rows in its LDS (one
 // thread per row, O <= 16 classes), block 0 also stores it (the loss's gradient autograd passes on),
 // then the block does its part of the narrow Linear's gradients:
-//   blocks [0, nbx)          16 columns i of dX over all rows (16 row lanes x 16 columns), each
+//   blocks [0, nbx)          16 columns i of dX x 32 rows (16 row lanes x 16 columns), each
 //                            dX[r][i] = sum_o dy[r][o] W[o][i] in small_linear_bwd_body's order; with a
 //                            BatchNorm link (lk.y != null: the input is the last VGG block's pooled,
 //                            1x1 output, so column i is channel i) the block also reduces that block's
 //                            BN backward partials from the dX it just formed -- sum dz, sum dz * xhat,
 //                            sum xhat over each 2x2 window through max-pool + ReLU, as bn_bwd_reduce --
-//                            into part[0][i][0..ps), so the block's backward takes them instead of a
+//                            into part[row chunk][i][0..ps), so the block's backward takes them instead of a
 //                            statistics launch of its own (ops/functional.py _BNLink)
 //   blocks [nbx, nbx + nbw)  dW, last block db (small_linear_bwd_body)
 // Three launches (xent_bwd, small_linear_bwd, bn_bwd_reduce) and two kernel boundaries less per step.
@@ -771,8 +771,11 @@ __global__ __launch_bounds__(256) void xent_linear_bwd_kernel(const float* __res
   }
   __shared__ float red[3][16][17];
   const int col = threadIdx.x & 15, rl = threadIdx.x >> 4;
-  const int i = blockIdx.x * 16 + col;
+  const int ncol = (I + 15) / 16;
+  const int chunk = blockIdx.x / ncol;  // rows [32 chunk, 32 chunk + 32): the BN partial index
+  const int i = (blockIdx.x - chunk * ncol) * 16 + col;
   const bool ok = i < I;
+  const int rend = min(B, kXentLinRows * (chunk + 1));
   float wc[SL_MAXO];
 #pragma unroll
   for (int o = 0; o < SL_MAXO; ++o) wc[o] = ok ? w[(long long)min(o, O - 1) * I + i] : 0.f;
@@ -785,7 +788,7 @@ __global__ __launch_bounds__(256) void xent_linear_bwd_kernel(const float* __res
     sc = lk.stats[2 * I + i];
     sh = lk.stats[3 * I + i];
   }
-  for (int r = rl; r < B && ok; r += 16) {
+  for (int r = kXentLinRows * chunk + rl; r < rend && ok; r += 16) {
     float s = 0.f;
     for (int o = 0; o < O; ++o) s = fmaf(sdy[r * O + o], wc[o], s);
     dx[(long long)r * I + i] = s;
@@ -825,7 +828,7 @@ __global__ __launch_bounds__(256) void xent_linear_bwd_kernel(const float* __res
   if (rl < lk.ps && ok) {
     float t = 0.f;
     for (int q = 0; q < 16; ++q) t += red[rl][q][col];
-    lk.part[(long long)i * lk.ps + rl] = t;
+    lk.part[((long long)chunk * I + i) * lk.ps + rl] = t;
   }
 }
 
@@ -1067,7 +1070,7 @@ void xent_linear_bwd_launch(const float* logits, const long long* tgt, const flo
                             const XentBnLink& lk, hipStream_t st) {
   if (O > SL_MAXO || (long long)B * O > kXentLinMax) throw std::runtime_error("xent_linear_bwd: classifier too wide");
   if (lk.y && (!dx || lk.ps < 2 || lk.ps > 3)) throw std::runtime_error("xent_linear_bwd: BN link needs dX");
-  const int nbx = dx ? (I + 15) / 16 : 0;
+  const int nbx = dx ? ((I + 15) / 16) * xent_lin_chunks(B) : 0;
   const int nbw = (I + 15) / 16;
   hipLaunchKernelGGL(xent_linear_bwd_kernel, dim3(nbx + nbw + 1), dim3(256), 0, st, logits, tgt, gscale, x, w, B, I, O,
                      dlogits, dx, dw, db, nbx, nbw, lk);

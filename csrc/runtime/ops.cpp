@@ -1757,7 +1757,7 @@ std::vector<at::Tensor> xent_linear_bwd(const at::Tensor& gloss, const at::Tenso
     TORCH_CHECK(link_stats.has_value() && link_stats->is_cuda() && link_stats->numel() == 4LL * I &&
                     link_stats->is_contiguous() && (link_ps == 2 || link_ps == 3),
                 "xent_linear_bwd: BN link stats [4, C] and ps in {2, 3}");
-    part = at::empty({1, I, link_ps}, x.options());
+    part = at::empty({xent_lin_chunks(B), I, link_ps}, x.options());
     lk = XentBnLink{yb.data_ptr<float>(), link_stats->data_ptr<float>(), part.data_ptr<float>(), link_pool ? 1 : 0,
                     link_relu ? 1 : 0, (int)link_ps};
   }
