@@ -41,6 +41,17 @@ METRIC = "images/sec (whole node) VGG-11 CIFAR-shaped at 1/2/4/8 MI355X; scaling
 REF_GLOBAL_BATCH = 256
 _GRAPH_FALLBACKS = []  # measurements that timed eager steps because a capture failed (see _Run._note_fallback)
 _LAST_GRAPH_COLLECTIVES = [None]  # native collectives recorded in the last measured captured step
+# profiling aid (CDP_GEMM_LOG=1 CDP_GEMM_LOG_OUT=path, eager runs): the last step's GEMM launches as
+# JSON (kind, M, N, K, tile, splits), to label a rocprofv3 trace's dispatches (scripts/pmc_resnet_layers.py)
+_GEMM_LOG_OUT = os.environ.get("CDP_GEMM_LOG_OUT")
+
+
+def _dump_gemm_log(cdp):
+    if not _GEMM_LOG_OUT:
+        return
+    rows = [dict(zip(("kind", "M", "N", "K", "bm", "bn", "splits"), r)) for r in cdp._native.lib().gemm_log(False)]
+    with open(_GEMM_LOG_OUT, "w") as f:
+        json.dump(rows, f)
 
 
 def parse(argv=None):
@@ -203,6 +214,8 @@ class _Run:
         import contextlib
 
         cdp, strategy = self.cdp, self.strategy
+        if _GEMM_LOG_OUT and self.args.backend == "native" and not self.torch.cuda.is_current_stream_capturing():
+            cdp._native.lib().gemm_log(True)  # keep only the latest step's GEMM launches (_dump_gemm_log)
         x, y = self.loader.batch(self.order, 0, self.local_batch, nbatches=self.nb)
         self.opt.zero_grad()
         nosync = (not self.sync_grads and self.world > 1 and hasattr(self.model, "no_sync"))
@@ -933,6 +946,8 @@ def single_main(args) -> int:
     main_lb = args.local_batch if args.scaling == "weak" else max(1, args.global_batch)
     os.environ["CDP_BENCH_PHASE"] = "headline"
     head = ctx.point({"lb": main_lb, "sync": True, "full": True, "strategy": args.strategy})
+    if args.backend == "native" and not ctx.cpu:
+        _dump_gemm_log(cdp)
     head.update(ranks_seen=1, comm="none", engine="reference" if ctx.cpu else _conv_gemm_engine(args.backend),
                 graph_collectives=_LAST_GRAPH_COLLECTIVES[0])
     ms = head["ms"]

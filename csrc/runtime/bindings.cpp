@@ -85,6 +85,8 @@ PYBIND11_MODULE(_C, m) {
         py::arg("has_bias"), py::arg("dw_out") = py::none(), py::arg("db_out") = py::none());
   m.def("xent_fwd", &xent_fwd, py::arg("logits"), py::arg("target"), py::arg("correct") = py::none());
   m.def("xent_bwd", &xent_bwd);
+  m.def("gemm_log", &gemm_log, py::arg("clear") = false,
+        "CDP_GEMM_LOG=1: (kind, M, N, K, bm, bn, splits) of every conv / weight-gradient GEMM launch so far");
   m.def("xent_linear_bwd", &xent_linear_bwd, py::arg("gloss"), py::arg("logits"), py::arg("target"), py::arg("x"),
         py::arg("w"), py::arg("need_dx"), py::arg("has_bias"), py::arg("dw_out") = py::none(),
         py::arg("db_out") = py::none(), py::arg("link_y") = py::none(), py::arg("link_stats") = py::none(),

@@ -22,6 +22,7 @@
 #include <cstring>
 #include <functional>
 #include <mutex>
+#include <tuple>
 #include <string>
 #include <unordered_map>
 
@@ -396,7 +397,49 @@ bool x3_ok(const WgradParams& p) {
          (long long)p.P * p.Q < kIdx;
 }
 
+// ---------------------------------------------------------------- GEMM launch log
+// CDP_GEMM_LOG=1: every conv / weight-gradient GEMM launch appends (kind, M, N, K, bm, bn, splits)
+// in enqueue order, so a profile's GEMM dispatches can be labelled with their shapes
+// (scripts/pmc_resnet_layers.py joins it with rocprofv3's kernel trace and counters).
+struct GemmLogRec {
+  std::string kind;
+  long long M, N, K;
+  int bm, bn, splits;
+};
+static std::mutex& gemm_log_mu() {
+  static std::mutex m;
+  return m;
+}
+static std::vector<GemmLogRec>& gemm_log_vec() {
+  static std::vector<GemmLogRec> v;
+  return v;
+}
+static bool gemm_log_on() {
+  static const bool on = [] {
+    const char* e = std::getenv("CDP_GEMM_LOG");
+    return e && e[0] == '1';
+  }();
+  return on;
+}
+static void gemm_log_add(const char* kind, long long M, long long N, long long K, int bm, int bn, int splits) {
+  if (!gemm_log_on()) return;
+  std::lock_guard<std::mutex> g(gemm_log_mu());
+  gemm_log_vec().push_back({kind, M, N, K, bm, bn, splits});
+}
+std::vector<std::tuple<std::string, int64_t, int64_t, int64_t, int64_t, int64_t, int64_t>> gemm_log(bool clear) {
+  std::lock_guard<std::mutex> g(gemm_log_mu());
+  std::vector<std::tuple<std::string, int64_t, int64_t, int64_t, int64_t, int64_t, int64_t>> out;
+  for (const auto& r : gemm_log_vec()) out.emplace_back(r.kind, r.M, r.N, r.K, r.bm, r.bn, r.splits);
+  if (clear) gemm_log_vec().clear();
+  return out;
+}
+static void wgrad_launch_logged(const WgradParams& p, int bm, int bn, bool x3, hipStream_t st, int np) {
+  gemm_log_add("wgrad", p.Cout, p.Kdim, (long long)p.M, bm, bn, p.splits);
+  wgrad_launch(p, bm, bn, x3, st, np);
+}
+
 void conv_launch(const ConvGemmParams& p, int bm, int bn, bool dgrad, hipStream_t st) {
+  gemm_log_add(dgrad ? "dgrad" : "fwd", p.M, p.Nout, p.Kdim, bm, bn, p.splits);
   if (x3_family() && x3_ok(p, dgrad)) {
     TORCH_CHECK(!f16x2_mode() || (p.a_img && p.b_row), "f16x2 conv GEMM launched without operand maxima");
     conv_x3_launch(p, bm, bn, dgrad, st, split_planes());
@@ -448,7 +491,7 @@ struct PendingWgrad {
   // launch it alone (no data-gradient GEMM took it)
   void flush(hipStream_t st) {
     if (!set) return;
-    wgrad_launch(p, bm, bn, true, st, 2);
+    wgrad_launch_logged(p, bm, bn, true, st, 2);
     run_after();
   }
 };
@@ -481,6 +524,9 @@ void conv_launch_or_pair(const ConvGemmParams& p, const GemmPlan& g, bool dgrad,
                          PendingWgrad* pending) {
   if (pending && pending->set && dgrad && f16x2_mode() && x3_ok(p, true) && p.a_img && p.b_row &&
       bwd_pair_ok(p, g.bm, g.bn, pending->p, pending->bm, pending->bn, split_planes())) {
+    gemm_log_add("pair_dgrad", p.M, p.Nout, p.Kdim, g.bm, g.bn, p.splits);
+    gemm_log_add("pair_wgrad", pending->p.Cout, pending->p.Kdim, (long long)pending->p.M, pending->bm, pending->bn,
+                 pending->p.splits);
     bwd_pair_launch(p, g.bm, g.bn, pending->p, pending->bm, pending->bn, st);
     pair_counter().fetch_add(1, std::memory_order_relaxed);
     pending->run_after();
@@ -1172,7 +1218,7 @@ at::Tensor wgrad_impl(const at::Tensor& dy_, const at::Tensor& x_, std::vector<i
       pending->keep = {dy, x, dya, xa};
       return;
     }
-    wgrad_launch(p, wp.bm, wp.bn, x3_family() && x3_ok(p), st, split_planes());
+    wgrad_launch_logged(p, wp.bm, wp.bn, x3_family() && x3_ok(p), st, split_planes());
     if (after) after();
   };
   if (p.splits == 1 && !accumulate && Ckeep == C) {
@@ -1229,6 +1275,7 @@ std::vector<at::Tensor> stem_bn_act_fwd(const at::Tensor& x_, const at::Tensor& 
   const long long M = (long long)N * H * W;
   const int nparts = (int)((M + 255) / 256);
   at::Tensor part = at::empty({nparts, Co, 2}, opts);
+  gemm_log_add("stem_fwd", (long long)N * H * W, Co, 9LL * Cin, 256, 64, 1);
   stem_fwd_launch(x.data_ptr<float>(), w.data_ptr<float>(), fptr(b), y.data_ptr<float>(),
                   part.data_ptr<float>(), N, H, W, Cin, Co, st);
   at::Tensor stats = at::empty({4, Co}, opts);
@@ -1496,6 +1543,7 @@ std::vector<at::Tensor> conv_bn_act_bwd(const at::Tensor& gout_, const at::Tenso
     const at::Tensor xin = nhwc(x);
     const int nb = stem_wgrad_blocks(N, H, W);
     at::Tensor slab = at::empty({nb, C, 36}, opts);
+    gemm_log_add("stem_wgrad", C, 9LL * cin, (long long)N * H * W, 64, 36, nb);
     stem_wgrad_launch(y.data_ptr<float>(), gout.data_ptr<float>(), stats.data_ptr<float>(), sums.data_ptr<float>(),
                       xin.data_ptr<float>(), slab.data_ptr<float>(), nb, N, H, W, cin, st);
     at::Tensor dw = dw_out.has_value() && dw_out->defined()
@@ -1679,11 +1727,11 @@ std::vector<at::Tensor> linear_bwd(const at::Tensor& gy_, const at::Tensor& x_, 
   set_scales(p, act_max(gy, c10::nullopt, st), act_max(x, c10::nullopt, st));
   if (p.splits == 1) {
     p.out = dw.data_ptr<float>();
-    wgrad_launch(p, wp.bm, wp.bn, x3_family() && x3_ok(p), st, split_planes());
+    wgrad_launch_logged(p, wp.bm, wp.bn, x3_family() && x3_ok(p), st, split_planes());
   } else {
     at::Tensor slab = at::empty({p.splits, O, I}, x.options());
     p.out = slab.data_ptr<float>();
-    wgrad_launch(p, wp.bm, wp.bn, x3_family() && x3_ok(p), st, split_planes());
+    wgrad_launch_logged(p, wp.bm, wp.bn, x3_family() && x3_ok(p), st, split_planes());
     slab_sum_launch(slab.data_ptr<float>(), p.splits, (long long)O * I, dw.data_ptr<float>(), false, st);
   }
   at::Tensor db;

@@ -2,6 +2,8 @@
 #include <ATen/ATen.h>
 #include <c10/util/Optional.h>
 
+#include <string>
+#include <tuple>
 #include <vector>
 
 namespace cdp {
@@ -104,5 +106,8 @@ at::Tensor maxpool2d_bwd(const at::Tensor& gy, const at::Tensor& arg, std::vecto
                          int64_t s, int64_t p);
 at::Tensor avgpool_fwd(const at::Tensor& x);
 at::Tensor avgpool_bwd(const at::Tensor& gy, std::vector<int64_t> in_shape);
+
+// CDP_GEMM_LOG=1: the GEMM launches so far as (kind, M, N, K, bm, bn, splits), in enqueue order
+std::vector<std::tuple<std::string, int64_t, int64_t, int64_t, int64_t, int64_t, int64_t>> gemm_log(bool clear);
 
 }  // namespace cdp
