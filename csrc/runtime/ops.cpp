@@ -426,7 +426,7 @@ static void gemm_log_add(const char* kind, long long M, long long N, long long K
   std::lock_guard<std::mutex> g(gemm_log_mu());
   gemm_log_vec().push_back({kind, M, N, K, bm, bn, splits});
 }
-std::vector<std::tuple<std::string, int64_t, int64_t, int64_t, int64_t, int64_t, int64_t>> gemm_log(bool clear) {
+std::vector<std::tuple<std::string, int64_t, int64_t, int64_t, int64_t, int64_t, int64_t>> gemm_log_snapshot(bool clear) {
   std::lock_guard<std::mutex> g(gemm_log_mu());
   std::vector<std::tuple<std::string, int64_t, int64_t, int64_t, int64_t, int64_t, int64_t>> out;
   for (const auto& r : gemm_log_vec()) out.emplace_back(r.kind, r.M, r.N, r.K, r.bm, r.bn, r.splits);
@@ -2073,5 +2073,9 @@ at::Tensor avgpool_bwd(const at::Tensor& gy_, std::vector<int64_t> in_shape) {
   return gx;
 }
 
+
+std::vector<std::tuple<std::string, int64_t, int64_t, int64_t, int64_t, int64_t, int64_t>> gemm_log(bool clear) {
+  return gemm_log_snapshot(clear);
+}
 
 }  // namespace cdp
