@@ -264,6 +264,8 @@ void augment_launch(const unsigned char* imgs, const long long* idx, long long i
                     const float* mean, const float* inv_std, int pad, bool flip, const long long* counter,
                     unsigned long long seed, float* out, hipStream_t st, long long nbatches = 0,
                     const long long* labels = nullptr, long long* labels_out = nullptr);
+// zeros into the NHWC dX pixels of the sub-pixel parity classes set in mask (bit 2 ph + pw)
+void subpixel_zero_launch(float* dx, int N, int H, int W, int C, int mask, hipStream_t st);
 void counter_inc_launch(long long* c, hipStream_t st);
 void wtrans_launch(const float* w, float* wt, int Co, int T, int Ci, hipStream_t st);
 // sub-filter transpose: wt[ci][a][b][co] = w[co][kh0 + 2a][kw0 + 2b][ci] (a < nkh, b < nkw)

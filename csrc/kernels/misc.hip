@@ -463,6 +463,20 @@ __global__ __launch_bounds__(256) void augment_kernel(const unsigned char* __res
 
 __global__ void counter_inc_kernel(long long* c) { c[0] += 1; }
 
+// dX of a stride-2 conv's sub-pixel parity classes with no filter taps (bit 2 ph + pw of mask):
+// zeros, float4 along C (NHWC), one thread per float4 of the classes' pixels
+__global__ __launch_bounds__(256) void subpixel_zero_kernel(float* __restrict__ dx, int N, int H, int W, int C4,
+                                                            int mask, FastDiv fd_C4, FastDiv fd_W) {
+  const long long total = (long long)N * H * W * C4;
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
+    const int pix = (int)(i / C4);  // < 2^31 pixels (launcher)
+    const int t = fdiv(pix, fd_W);
+    const int w = pix - t * W;
+    const int h = t % H;
+    if ((mask >> (2 * (h & 1) + (w & 1))) & 1) st4(dx + 4 * i, f4zero());
+  }
+}
+
 // ------------------------------------------------------------------ weight transpose
 // W[co][tap][ci] -> Wt[ci][tap][co]   (tap = kh*KW+kw; conv data-gradient uses Wt as its B^T)
 __global__ __launch_bounds__(256) void wtrans_kernel(const float* __restrict__ w, float* __restrict__ wt, int Co,
@@ -999,6 +1013,12 @@ void augment_launch(const unsigned char* imgs, const long long* idx, long long i
   hipLaunchKernelGGL(augment_kernel, grid, dim3(256), 0, st, imgs, idx, idx_off, B, H, W, C, mean[0], mean[1],
                      mean[2], inv_std[0], inv_std[1], inv_std[2], pad, flip ? 1 : 0, counter, seed, out, nbatches,
                      labels, labels_out);
+}
+void subpixel_zero_launch(float* dx, int N, int H, int W, int C, int mask, hipStream_t st) {
+  if ((long long)N * H * W >= (1LL << 31) || (C & 3)) throw std::runtime_error("subpixel_zero: bad shape");
+  const long long n4 = (long long)N * H * W * (C / 4);
+  hipLaunchKernelGGL(subpixel_zero_kernel, dim3(grid_for(n4)), dim3(256), 0, st, dx, N, H, W, C / 4, mask,
+                     make_fastdiv(C / 4), make_fastdiv(W));
 }
 void counter_inc_launch(long long* c, hipStream_t st) {
   hipLaunchKernelGGL(counter_inc_kernel, dim3(1), dim3(1), 0, st, c);

@@ -1045,14 +1045,23 @@ std::vector<at::Tensor> conv2d_fwd(const at::Tensor& x_, const at::Tensor& w_, c
   return {y};
 }
 
+// CDP_SUBPIXEL_ZERO=0: the tap-less sub-pixel classes as K-less GEMM launches (A/B)
+static bool subpixel_zero_enabled() {
+  const char* e = std::getenv("CDP_SUBPIXEL_ZERO");
+  return !(e && e[0] == '0');
+}
+
 // ---------------------------------------------------------------- conv data gradient
 // Stride-2 data gradient by sub-pixel decomposition: the input pixels of parity class (ph, pw)
 // receive gradient only from the filter taps kh = kh0 + 2a, kw = kw0 + 2b, kh0 = (ph + pad) % 2,
 // through dY[(ih + pad - kh) / 2]. Each class is therefore a dense stride-1 correlation of dY with
 // a quarter-size sub-filter over a quarter of the rows: 4 GEMMs doing 1/4 of the work of the
 // masked full-resolution gather (which spends 3/4 of its MACs on taps that cannot contribute).
-// Classes without taps (e.g. the odd pixels of a 1x1 stride-2 conv) get zeros from a K-less
-// launch. Returns false when a shape is outside the x3 kernels' addressing limits.
+// Classes without taps (e.g. the odd pixels of a 1x1 stride-2 conv: three of the four) receive no
+// gradient: with an addend, dX is the addend itself (accumulated in place) and those pixels are
+// already final; without one, a single fill pass writes their zeros (subpixel_zero_launch: one
+// bandwidth-bound launch instead of three K-less GEMM launches, whose epilogues wrote at ~2 TB/s).
+// Returns false when a shape is outside the x3 kernels' addressing limits.
 bool conv2d_dgrad_subpixel(const at::Tensor& dy, const at::Tensor& w, at::Tensor& dx, int pad, hipStream_t st,
                            const float* addend, const at::Tensor& dya, const at::Tensor& wa) {
   const int N = dx.size(0), C = dx.size(1), H = dx.size(2), W = dx.size(3);
@@ -1060,6 +1069,22 @@ bool conv2d_dgrad_subpixel(const at::Tensor& dy, const at::Tensor& w, at::Tensor
   const int P = dy.size(2), Q = dy.size(3);
   if (Co % 32 != 0) return false;
   std::vector<at::Tensor> keep;  // sub-filters / slabs stay alive until the launches are enqueued
+  // pass 1: every class within the kernels' addressing limits (decided before any launch)
+  int empty_mask = 0;
+  for (int ph = 0; ph < 2; ++ph)
+    for (int pw = 0; pw < 2; ++pw) {
+      const int Hc = (H - ph + 1) / 2, Wc = (W - pw + 1) / 2;
+      if (Hc <= 0 || Wc <= 0) continue;
+      const int kh0 = (ph + pad) % 2, kw0 = (pw + pad) % 2;
+      const int nkh = kh0 < KH ? (KH - kh0 + 1) / 2 : 0, nkw = kw0 < KW ? (KW - kw0 + 1) / 2 : 0;
+      if (nkh * nkw == 0) empty_mask |= 1 << (2 * ph + pw);
+    }
+  if (empty_mask && !addend && (C % 4) == 0 && !subpixel_zero_enabled()) empty_mask = 0;
+  if (empty_mask && (addend || (C % 4) == 0)) {
+    if (!addend) subpixel_zero_launch(dx.data_ptr<float>(), N, H, W, C, empty_mask, st);
+  } else {
+    empty_mask = 0;  // (C % 4 != 0 without an addend: the K-less GEMM launches write the zeros)
+  }
   for (int ph = 0; ph < 2; ++ph)
     for (int pw = 0; pw < 2; ++pw) {
       const int Hc = (H - ph + 1) / 2, Wc = (W - pw + 1) / 2;
@@ -1068,6 +1093,7 @@ bool conv2d_dgrad_subpixel(const at::Tensor& dy, const at::Tensor& w, at::Tensor
       const int nkh = kh0 < KH ? (KH - kh0 + 1) / 2 : 0, nkw = kw0 < KW ? (KW - kw0 + 1) / 2 : 0;
       const long long Mc = (long long)N * Hc * Wc;
       const int Kc = nkh * nkw * Co;
+      if (Kc == 0 && (empty_mask >> (2 * ph + pw) & 1)) continue;  // written above / already the addend
       ConvGemmParams p{};
       p.N = N; p.H = P; p.W = Q; p.C = Co; p.P = Hc; p.Q = Wc;
       p.KH = std::max(nkh, 1); p.KW = std::max(nkw, 1); p.stride = 1;
