@@ -9,6 +9,7 @@
 // (mean_b, M2_b per column, two exact passes over the registers) so the following
 // BatchNorm never re-reads the conv output for its statistics.
 #pragma once
+#include <cstdint>
 #include <type_traits>
 
 #include "common.h"
@@ -19,6 +20,54 @@ namespace cdp {
 // Wave grid: WM x 2 waves (WM = 4 for BM = 256, else 2), each owning (BM/WM) x (BN/2).
 template <int BM>
 constexpr int waves_m() { return BM >= 256 ? 4 : 2; }
+
+// Wide stores: the accumulator layout gives a lane one column, so a plain epilogue writes a 32 x 32
+// sub-tile with 16 four-byte store instructions per lane. For the small-K GEMMs (ResNet's 1x1
+// convolutions, K = 64..256) that store stream, not HBM, bounds the kernel (200704 x 256 x 64: 2.2
+// TB/s written, a fill of the same bytes 6.8). A full tile instead goes through LDS one 32 x 32
+// sub-tile per wave and leaves as 16-B row segments: 4 store instructions. Staging area per wave
+// (row stride kStageLd floats: the two half-waves' rows of one ds_write land 32 banks apart), past
+// the statistics scratch (WM x BN floats) and the f16x2 row-scale arrays (BM + BN floats).
+constexpr int kStageLd = 40;
+template <int BM, int BN>
+constexpr int epi_stage_base() { return (waves_m<BM>() * BN + BM + BN + 3) & ~3; }
+template <int BM, int BN>
+constexpr int epi_lds_floats() { return epi_stage_base<BM, BN>() + waves_m<BM>() * 2 * 32 * kStageLd; }
+
+// Store the wave's accumulators (full tile) to dst[rowmap(m) * ld + n] with 16-B stores.
+template <int BM, int BN, class RowMap>
+__device__ __forceinline__ void wide_store(const f32x16 (&acc)[BM / waves_m<BM>() / 32][BN / 64], float* red,
+                                           float* __restrict__ dst, long long ld, int m0, int n0, RowMap rowmap) {
+  constexpr int WM = waves_m<BM>();
+  constexpr int TM = BM / WM / 32, TN = BN / 64;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wid = tid >> 6;
+  const int wm = wid >> 1, wn = wid & 1;
+  const int l32 = lane & 31;
+  const int hh = lane >> 5;
+  float* st = red + epi_stage_base<BM, BN>() + wid * 32 * kStageLd;
+  const int rq = lane >> 3, cq = (lane & 7) * 4;
+#pragma unroll
+  for (int a = 0; a < TM; ++a)
+#pragma unroll
+    for (int b = 0; b < TN; ++b) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) st[((r & 3) + 8 * (r >> 2) + 4 * hh) * kStageLd + l32] = acc[a][b][r];
+      // one wave's private area: LDS runs a wave's operations in order, the wait keeps the
+      // compiler from moving the reads above the writes
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      const int mb = m0 + wm * (BM / WM) + a * 32;
+      const int n = n0 + wn * (BN / 2) + b * 32 + cq;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int row = rq + 8 * i;
+        const float4 v = *reinterpret_cast<const float4*>(st + row * kStageLd + cq);
+        *reinterpret_cast<float4*>(dst + rowmap(mb + row) * ld + n) = v;
+      }
+      asm volatile("" ::: "memory");  // the next sub-tile's writes stay behind these reads
+    }
+}
 
 template <int BM, int BN>
 __device__ __forceinline__ void conv_tile_stats(const ConvGemmParams& p,
@@ -39,6 +88,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvGemmParams& p,
   const int hh = lane >> 5;
   // whole tile in bounds (the common case): unpredicated stores, no per-element exec branches
   const bool full = m0 + BM <= p.M && n0 + BN <= p.Nout;
+  const bool wide = !p.narrow && (p.Nout & 3) == 0 && ((reinterpret_cast<uintptr_t>(p.y) & 15) == 0);
   if (p.splits > 1) {
     float* out = p.y + (long long)split * p.M * p.Nout;
     auto slab_store = [&](auto pred) {
@@ -54,8 +104,14 @@ __device__ __forceinline__ void conv_epilogue(const ConvGemmParams& p,
           }
         }
     };
-    if (full) slab_store(std::false_type{});
-    else slab_store(std::true_type{});
+    if (full && wide) {
+      __syncthreads();  // the staging area aliases the operand LDS the last K-tile may still read
+      wide_store<BM, BN>(acc, red, out, p.Nout, m0, n0, [](int m) { return (long long)m; });
+    } else if (full) {
+      slab_store(std::false_type{});
+    } else {
+      slab_store(std::true_type{});
+    }
     return;
   }
 
@@ -102,8 +158,10 @@ __device__ __forceinline__ void conv_epilogue(const ConvGemmParams& p,
         }
       }
   };
-  if (p.part) conv_tile_stats<BM, BN>(p, acc, red, m0, n0, tm_idx);
-  if (full) out_store(std::false_type{});
+  if (p.part) conv_tile_stats<BM, BN>(p, acc, red, m0, n0, tm_idx);  // ends past a barrier
+  else if (full && wide) __syncthreads();  // the staging area aliases the operand LDS
+  if (full && wide) wide_store<BM, BN>(acc, red, p.y, p.Nout, m0, n0, [&](int m) { return remap_row(p.rr, m); });
+  else if (full) out_store(std::false_type{});
   else out_store(std::true_type{});
 }
 

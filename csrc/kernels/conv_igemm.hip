@@ -39,6 +39,7 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvGemmParams p) {
   constexpr int TN = BN / 64;  // 32-col MFMA tiles per wave
   constexpr int STAGE = (BM + BN) * LDK;
   __shared__ __attribute__((aligned(16))) float smem[2 * STAGE];
+  static_assert(2 * STAGE >= epi_lds_floats<BM, BN>(), "epilogue scratch");
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;

@@ -56,9 +56,13 @@ __device__ __forceinline__ u32x4 pack8(const float (&v)[8]) {
   return r;
 }
 
-// LDS of one workgroup (bf16 elements): two stages of NP planes of A and B
+// LDS of one workgroup (bf16 elements): two stages of NP planes of A and B, at least the epilogue's
+// scratch (conv_epilogue.h; only the one-plane 64 x 64 tile needs more than its stages)
 template <int BM, int BN, int NP>
-constexpr int conv_x3_smem_elems() { return 2 * NP * (BM + BN) * LDH; }
+constexpr int conv_x3_smem_elems() {
+  return 2 * NP * (BM + BN) * LDH > 2 * epi_lds_floats<BM, BN>() ? 2 * NP * (BM + BN) * LDH
+                                                                  : 2 * epi_lds_floats<BM, BN>();
+}
 
 // The kernel body as a device function: `smem` holds conv_x3_smem_elems() bf16 (the caller's one
 // LDS array), `vbid` / `nvb` are this workgroup's id and the count of workgroups running this
@@ -77,7 +81,6 @@ __device__ __forceinline__ void conv_x3_body(const ConvGemmParams& p, __bf16* __
   static_assert(A_LD >= 1 && B_LD >= 1, "tile too narrow for the loader");
   constexpr int PA = BM * LDH, PB = BN * LDH;
   constexpr int STAGE = NP * (PA + PB);  // bf16 per stage: A planes [NP][BM][LDH], B planes [NP][BN][LDH]
-  static_assert(2 * STAGE * 2 >= 2 * BN * 4, "epilogue scratch");
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;

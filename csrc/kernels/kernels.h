@@ -72,6 +72,7 @@ struct ConvGemmParams {
   const unsigned* a_img;
   const float* b_row;
   int b_np, b_stride;
+  int narrow;  // 1: four-byte epilogue stores (the A/B of conv_epilogue.h's wide stores, CDP_WIDE_STORES=0)
 };
 
 struct WgradParams {

@@ -438,8 +438,19 @@ static void wgrad_launch_logged(const WgradParams& p, int bm, int bn, bool x3, h
   wgrad_launch(p, bm, bn, x3, st, np);
 }
 
-void conv_launch(const ConvGemmParams& p, int bm, int bn, bool dgrad, hipStream_t st) {
-  gemm_log_add(dgrad ? "dgrad" : "fwd", p.M, p.Nout, p.Kdim, bm, bn, p.splits);
+// CDP_WIDE_STORES=0: the conv GEMM epilogues store four bytes per lane (conv_epilogue.h)
+static bool narrow_stores() {
+  static const bool on = [] {
+    const char* e = std::getenv("CDP_WIDE_STORES");
+    return e && e[0] == '0';
+  }();
+  return on;
+}
+
+void conv_launch(const ConvGemmParams& p0, int bm, int bn, bool dgrad, hipStream_t st) {
+  gemm_log_add(dgrad ? "dgrad" : "fwd", p0.M, p0.Nout, p0.Kdim, bm, bn, p0.splits);
+  ConvGemmParams p = p0;
+  p.narrow = narrow_stores();
   if (x3_family() && x3_ok(p, dgrad)) {
     TORCH_CHECK(!f16x2_mode() || (p.a_img && p.b_row), "f16x2 conv GEMM launched without operand maxima");
     conv_x3_launch(p, bm, bn, dgrad, st, split_planes());
@@ -527,7 +538,9 @@ void conv_launch_or_pair(const ConvGemmParams& p, const GemmPlan& g, bool dgrad,
     gemm_log_add("pair_dgrad", p.M, p.Nout, p.Kdim, g.bm, g.bn, p.splits);
     gemm_log_add("pair_wgrad", pending->p.Cout, pending->p.Kdim, (long long)pending->p.M, pending->bm, pending->bn,
                  pending->p.splits);
-    bwd_pair_launch(p, g.bm, g.bn, pending->p, pending->bm, pending->bn, st);
+    ConvGemmParams q = p;
+    q.narrow = narrow_stores();
+    bwd_pair_launch(q, g.bm, g.bn, pending->p, pending->bm, pending->bn, st);
     pair_counter().fetch_add(1, std::memory_order_relaxed);
     pending->run_after();
     return;
