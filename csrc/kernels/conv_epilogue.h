@@ -115,6 +115,8 @@ __device__ __forceinline__ void conv_epilogue(const ConvGemmParams& p,
     return;
   }
 
+  // (measured and rejected: the addend loaded as 16-B rows through LDS, like the stores -- ResNet-50
+  // 14.87 -> 15.35 ms, the extra barrier and 64 more VGPRs in the data-gradient kernels)
   if (p.addend) {  // y += addend (may alias y): every load is issued before any store
 #pragma unroll
     for (int a = 0; a < TM; ++a)

@@ -827,6 +827,11 @@ const std::vector<TunedPlan>& tuned_plans() {
       {0, 3, 50176, 512, 128, 64, 128, 1},
       {0, 3, 12544, 256, 1024, 64, 128, 1},
       {0, 3, 200704, 64, 64, 64, 64, 1},
+      // round 6, after the LDS-staged 16-B epilogue stores: forward 64->256 1x1 @56 83.1 -> 73.5,
+      // data gradients 64->64 1x1 @56 22.6 -> 21.4 and 64->256 1x1 @56 45.6 -> 44.5
+      {0, 3, 200704, 256, 64, 128, 128, 1},
+      {1, 3, 200704, 64, 64, 64, 64, 1},
+      {1, 3, 200704, 64, 256, 64, 64, 1},
       // data gradients of 256->64 @56 70.4 -> 65.9, 256->128 @56 111.7 -> 105.4, 512->128 @28
       // 54.8 -> 48.9, 512->256 @28 77.5 -> 69.5, 256->1024 @14 36.7 -> 34.2 (all 1x1)
       {1, 3, 200704, 256, 64, 128, 128, 1},

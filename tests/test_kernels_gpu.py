@@ -61,6 +61,31 @@ def test_conv_fwd_dgrad_wgrad(N, Ci, H, W, Co, k, s, p):
     assert rel_err(dw, wr.grad) < 2e-5
 
 
+@pytest.mark.parametrize("N,Ci,H,W,Co,k,s,p", [
+    (4, 64, 28, 28, 256, 1, 1, 0),   # full tiles and an M tail through the wide epilogue loads
+    (2, 64, 56, 56, 64, 3, 1, 1),
+    (2, 128, 14, 14, 256, 1, 2, 0),  # stride 2: sub-pixel classes, tap-less ones skipped
+    (3, 64, 14, 14, 64, 1, 1, 0),
+])
+def test_conv_dgrad_accumulates_into_addend(N, Ci, H, W, Co, k, s, p):
+    """dX += dgrad in place (the parked residual gradient of a ResNet block): the epilogue's addend
+    loads (16-B rows through LDS on full tiles, per element on edge tiles) before any store."""
+    torch.manual_seed(3)
+    dev = "cuda"
+    x = torch.randn(N, Ci, H, W, device=dev)
+    w = torch.randn(Co, Ci, k, k, device=dev) * (1.0 / (Ci * k * k) ** 0.5)
+    xr = x.double().cpu().requires_grad_()
+    y = F.conv2d(xr, w.double().cpu(), None, s, p)
+    gy = torch.randn(y.shape, dtype=torch.float64)
+    y.backward(gy)
+    base = cl(torch.randn(N, Ci, H, W, device=dev))
+    ref = xr.grad + base.double().cpu()
+    acc = base.clone()
+    dx = C().conv2d_dgrad(cl(gy.float().to(dev)), cl(w), list(x.shape), s, p, acc)
+    assert dx.data_ptr() == acc.data_ptr()
+    assert rel_err(dx, ref) < 2e-5
+
+
 def test_conv_bn_stats_match_batchnorm():
     torch.manual_seed(1)
     x = torch.randn(16, 64, 16, 16, device="cuda")
