@@ -84,6 +84,10 @@ def parse(argv=None):
     p.add_argument("--overlap-step", action="store_true",
                    help="DDP: run the SGD step bucket by bucket right after each bucket's all-reduce "
                         "(DistributedDataParallel.overlap_optimizer); recorded as config.optimizer_overlap")
+    p.add_argument("--early-bcast", action="store_true",
+                   help="DDP: broadcast the BN buffers at the end of backward behind the last bucket, joined "
+                        "after the SGD (DistributedDataParallel.early_buffer_broadcast); recorded as "
+                        "config.early_buffer_broadcast")
     p.add_argument("--dataset-size", type=int, default=50000)
     p.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
                    help="cpu = gloo smoke mode of the multi-process path (reference ops, tiny sizes)")
@@ -184,6 +188,8 @@ class _Run:
             self.opt = cdp.SGD(model.parameters(), lr=0.1, momentum=0.9, weight_decay=1e-4)
             if args.overlap_step and isinstance(model, cdp.DistributedDataParallel):
                 model.overlap_optimizer(self.opt)
+            if args.early_bcast and isinstance(model, cdp.DistributedDataParallel) and self.dev.type == "cuda":
+                model.early_buffer_broadcast(self.opt)
             # A/B hook: the optimizer step without the next forward's weight preparation (a separate
             # weight_prep launch per forward, as before round 4)
             self.opt.fused_prep = os.environ.get("CDP_BENCH_NO_FUSED_PREP") != "1"
@@ -920,6 +926,7 @@ def _record(args, world, main_lb, ms, head, fallbacks, extra):
             "optimizer": "SGD(lr=0.1, momentum=0.9, wd=1e-4)",
             # the step split per gradient bucket and run behind each bucket's all-reduce (--overlap-step)
             "optimizer_overlap": bool(args.overlap_step) and args.strategy == "ddp" and (world > 1 or os.environ.get("CDP_BENCH_DDP_W1") == "1"),
+            "early_buffer_broadcast": bool(args.early_bcast) and args.strategy == "ddp" and not cpu and (world > 1 or os.environ.get("CDP_BENCH_DDP_W1") == "1"),
             # conv GEMM numerics, all with fp32 operands and fp32 accumulation: "f16x2" =
             # power-of-two-scaled operands split into two fp16 terms, three products on the
             # fp16 MFMA; "x3" = 3-term bf16 split, six products on the bf16 MFMA; "f32" =

@@ -48,6 +48,9 @@ class SGD(Optimizer):
             maximize=maximize, foreach=None, differentiable=False, fused=None,
         )
         super().__init__(params, defaults)
+        # callables run at the end of every step (DistributedDataParallel.early_buffer_broadcast
+        # joins its end-of-backward buffer broadcast here, after the SGD it overlaps)
+        self._post_step_joins = []
         self._flat = flat
         self._arena = None
         self._lr_tensor = None
@@ -132,6 +135,7 @@ class SGD(Optimizer):
             done = ov["reducer"].stepped_buckets()
             if done == ov["n"]:
                 self._finish_overlapped(ov)
+                self._run_post_step_joins()
                 return loss
             if done:
                 raise RuntimeError(f"overlapped optimizer step: only {done} of {ov['n']} buckets were stepped")
@@ -154,7 +158,18 @@ class SGD(Optimizer):
                 c += 1
             self._counter_pending = None
         self._steps += 1
+        self._run_post_step_joins()
         return loss
+
+    def add_post_step_join(self, fn):
+        """Run ``fn()`` at the end of every ``step()`` (e.g. to order the current stream after
+        communication issued during backward; see ``DistributedDataParallel.early_buffer_broadcast``)."""
+        if fn not in self._post_step_joins:
+            self._post_step_joins.append(fn)
+
+    def _run_post_step_joins(self):
+        for fn in getattr(self, "_post_step_joins", ()):
+            fn()
 
     # ------------------------------------------------------------------ overlapped step (DDP)
     def bucket_steps(self, ranges, reducer):

@@ -124,9 +124,13 @@ class RcclCommunicator(Communicator):
         self._c = C.RcclComm(bytes(uid), rank, size, device, float(timeout_s))
 
         spec = os.environ.get("CDP_REDUCER_TEST_POSTOP")
+        # modelled-xGMI mode: one rank stands in for W (collectives cost alpha + bytes / B on the
+        # comm stream), so DDP's one-rank shortcuts (no buffer broadcast) are off
+        self.models_world = 0
         if spec and spec.startswith("xgmi:"):  # "xgmi:alpha_us:GBps:W" -- RcclComm::set_test_postop_model
             _, a, bw, w = spec.split(":")
             self._c.set_test_postop_model(float(a), float(bw), int(w))
+            self.models_world = int(w)
         elif spec:  # "delay_us:scale" -- test hook, see RcclComm::set_test_postop
             d, sc = spec.split(":")
             self._c.set_test_postop(float(d), float(sc))

@@ -97,6 +97,7 @@ class DistributedDataParallel(nn.Module):
         self._rebuild = rebuild_buckets
         self._rebuilt = False
         self._step_opt = None
+        self._early_bcast = False
 
     def overlap_optimizer(self, optimizer):
         """Opt-in: run ``optimizer``'s step bucket by bucket inside backward, each bucket's SGD on the
@@ -110,6 +111,34 @@ class DistributedDataParallel(nn.Module):
             raise TypeError("overlap_optimizer needs cs744_distributed_data_parallel_amd.SGD")
         self._step_opt = optimizer
         return self
+
+    def early_buffer_broadcast(self, optimizer):
+        """Opt-in (RCCL communicator, native reducer): broadcast rank 0's buffers (BatchNorm running
+        statistics) at the end of every synced backward -- on the comm stream right behind the last
+        gradient bucket -- instead of at the start of the next forward, where the compute stream
+        waits for it. ``optimizer.step()`` (this package's ``SGD``) joins it afterwards, so the
+        broadcast runs under the SGD; the next forward then skips its own broadcast.
+
+        The buffers only change in forward, so forward k+1 sees the values torch DDP would
+        broadcast to it -- unless rank 0's buffers are modified between backward k and forward k+1
+        (e.g. a ``load_state_dict`` there), which then reaches the other ranks one step later.
+        Returns self; a no-op without buffers to broadcast."""
+        if not hasattr(optimizer, "add_post_step_join"):
+            raise TypeError("early_buffer_broadcast needs cs744_distributed_data_parallel_amd.SGD")
+        if self._buffers_arena is None or not self._bcast_needed():
+            return self
+        self.reducer.set_post_broadcast(list(self._buffers_arena.flats()))
+        optimizer.add_post_step_join(self._join_early_broadcast)
+        self._early_bcast = True
+        return self
+
+    def _join_early_broadcast(self):
+        self.reducer.join_post_broadcast()
+
+    def _bcast_needed(self):
+        # one rank has nothing to broadcast -- except under the modelled-xGMI test mode, where the
+        # one rank stands in for W and its collectives carry the modelled cost
+        return self.world_size > 1 or getattr(self.comm, "models_world", 0) > 1
 
     def _register_bucket_steps(self):
         opt, red = self._step_opt, self.reducer
@@ -150,7 +179,7 @@ class DistributedDataParallel(nn.Module):
 
     @torch.no_grad()
     def _sync_buffers(self):
-        if self._buffers_arena is None or self.world_size == 1:
+        if self._buffers_arena is None or not self._bcast_needed():
             return
         for f in self._buffers_arena.flats():
             self.comm.broadcast(f, 0)
@@ -166,7 +195,10 @@ class DistributedDataParallel(nn.Module):
         # like torch DDP: the buffer broadcast of forward k is decided by forward k-1 (so the first
         # no-grad eval forward after training still syncs once)
         if self.broadcast_buffers and self.require_forward_param_sync:
-            self._sync_buffers()
+            if self._early_bcast and self.reducer.take_post_issued() > 0:
+                self._join_early_broadcast()  # the last backward broadcast them (usually joined already)
+            else:
+                self._sync_buffers()
         out = self.module(*inputs, **kwargs)
         if grad_sync:
             self.require_forward_param_sync = True
@@ -194,6 +226,7 @@ class DistributedDataParallel(nn.Module):
     def _get_ddp_logging_data(self):
         return {
             "overlapped_step_buckets": self.reducer.stepped_buckets() if self._step_opt is not None else 0,
+            "early_buffer_broadcast": self._early_bcast,
             "bucket_sizes": self.reducer.bucket_sizes_bytes(),
             "num_buckets": self.reducer.num_buckets,
             "native_reducer": self.reducer.native,

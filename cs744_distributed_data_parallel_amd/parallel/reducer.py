@@ -244,6 +244,11 @@ class GradReducer:
         if self._impl is not None and getattr(self, "_trace", False):
             self._old_log = self._old_log + [tuple(e) for e in self._impl.trace_log()]  # keep across rebuilds
         if self._impl is not None:
+            if hasattr(self._impl, "join_post_broadcast"):
+                # an early buffer broadcast still pending on the old reducer: ordered before anything
+                # that follows, and still counted for the next forward
+                self._impl.join_post_broadcast()
+                self._carry_issued = getattr(self, "_carry_issued", 0) + int(self._impl.take_post_issued())
             # drop every reference to the old AccumulateGrad nodes first so that fresh ones are
             # created on the current stream (see rebind_if_stream_changed)
             self._impl.remove_hooks()
@@ -266,6 +271,29 @@ class GradReducer:
             self._impl.set_trace(True)
         if getattr(self, "_timing", None) is not None:
             self._impl.set_defer(True)
+        if getattr(self, "_post_bcast", None) and hasattr(self._impl, "set_post_broadcast"):
+            self._impl.set_post_broadcast(self._post_bcast)
+
+    # early buffer broadcast (DistributedDataParallel.early_buffer_broadcast): kept across rebuilds
+    def set_post_broadcast(self, tensors):
+        """Broadcast ``tensors`` from rank 0 behind the last bucket at the end of every synced backward
+        (native reducer on the RCCL communicator only)."""
+        if not self.native or not isinstance(self.comm, RcclCommunicator):
+            raise RuntimeError("the end-of-backward buffer broadcast needs the native reducer on the RCCL communicator")
+        self._post_bcast = list(tensors)
+        self._impl.set_post_broadcast(self._post_bcast)
+
+    def join_post_broadcast(self) -> int:
+        """The current stream waits for the pending end-of-backward broadcasts; returns their count."""
+        return int(self._impl.join_post_broadcast()) if hasattr(self._impl, "join_post_broadcast") else 0
+
+    def take_post_issued(self) -> int:
+        """End-of-backward broadcasts issued since the last call."""
+        n = getattr(self, "_carry_issued", 0)
+        self._carry_issued = 0
+        if hasattr(self._impl, "take_post_issued"):
+            n += int(self._impl.take_post_issued())
+        return n
 
     @property
     def native(self) -> bool:

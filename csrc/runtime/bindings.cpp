@@ -219,5 +219,8 @@ PYBIND11_MODULE(_C, m) {
            "SGD over bucket b's arena range, run on the reducer's step stream as soon as b's all-reduce completes "
            "(held for the next backward only)")
       .def("clear_bucket_steps", &Reducer::clear_bucket_steps)
+      .def("set_post_broadcast", &Reducer::set_post_broadcast, py::arg("tensors"))
+      .def("join_post_broadcast", &Reducer::join_post_broadcast)
+      .def("take_post_issued", &Reducer::take_post_issued)
       .def_property_readonly("stepped_buckets", &Reducer::stepped_buckets);
 }

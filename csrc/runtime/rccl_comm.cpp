@@ -324,6 +324,10 @@ std::shared_ptr<RcclWork> RcclComm::broadcast(at::Tensor t, int root, bool async
   hipStream_t cur = begin();
   if (world_ > 1)
     RCCL_CHECK(ncclBroadcast(t.data_ptr(), t.data_ptr(), t.numel(), to_nccl(t.scalar_type()), root, comm_, stream_));
+  // modelled-xGMI test mode (set_test_postop_model): a pipelined broadcast costs about
+  // alpha + bytes / B; the pure delay kernel touches no data (any dtype)
+  if (postop_w_ > 1 && postop_gbps_ > 0.0)
+    delay_scale_launch(nullptr, 0, 1.f, postop_alpha_us_ + (double)t.nbytes() / (postop_gbps_ * 1e3), stream_);
   return end(cur, async, {t}, "broadcast");
 }
 

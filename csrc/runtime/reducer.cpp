@@ -292,6 +292,14 @@ void Reducer::launch(int b) {
   ++launched_total_;
 }
 
+int64_t Reducer::join_post_broadcast() {
+  std::lock_guard<std::mutex> g(mu_);
+  const int64_t n = (int64_t)post_works_.size();
+  for (auto& w : post_works_) w->wait();  // orders the current stream after the broadcast
+  post_works_.clear();
+  return n;
+}
+
 void Reducer::finalize() {
   std::lock_guard<std::mutex> g(mu_);
   if (!armed_) return;
@@ -328,6 +336,12 @@ void Reducer::finalize() {
   if (rccl_) {
     // all buckets run in order on the communicator stream: waiting on the last one covers them all
     if (!works_.empty() && works_.back()) works_.back()->wait();
+    // the buffer broadcast behind the last bucket: nothing on the compute stream waits for it here
+    // (a previous backward's broadcasts nobody joined: the compute stream waits for them first)
+    for (auto& w : post_works_) w->wait();
+    post_works_.clear();
+    for (auto& t : post_bcast_) post_works_.push_back(rccl_->broadcast(t, 0, /*async=*/true));
+    post_issued_ += (int64_t)post_bcast_.size();
     if (stepped_now_ > 0) {
       // ... and the bucket steps in order on the step stream: the compute stream (the next forward
       // reads the stepped weights) waits for the last one

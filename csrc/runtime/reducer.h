@@ -54,6 +54,8 @@ class Reducer {
     std::lock_guard<std::mutex> g(mu_);
     armed_ = false;
     steps_.clear();
+    post_works_.clear();  // a failed capture's broadcasts never ran
+    post_issued_ = 0;
   }
   // Overlapped optimizer step (opt-in, RCCL path): the SGD of bucket b's arena range is enqueued on
   // the reducer's own step stream right behind b's all-reduce, so it runs while later buckets are
@@ -70,6 +72,23 @@ class Reducer {
   }
   // buckets whose step ran in the last completed backward
   int64_t stepped_buckets() const { return stepped_last_; }
+  // Early buffer broadcast (opt-in, RCCL path): rank 0's module buffers are broadcast on the comm
+  // stream right behind the last bucket at the end of every synced backward, instead of at the start
+  // of the next forward; the compute stream does not wait for them there. join_post_broadcast()
+  // makes the current stream wait for the pending broadcasts (the optimizer step's end or the next
+  // forward calls it) and returns how many it joined. An empty list turns it off.
+  void set_post_broadcast(std::vector<at::Tensor> ts) {
+    std::lock_guard<std::mutex> g(mu_);
+    post_bcast_ = std::move(ts);
+  }
+  int64_t join_post_broadcast();
+  // broadcasts issued by the backwards since the last call (the next forward skips its own then)
+  int64_t take_post_issued() {
+    std::lock_guard<std::mutex> g(mu_);
+    const int64_t n = post_issued_;
+    post_issued_ = 0;
+    return n;
+  }
 
  private:
   void reset_state();
@@ -85,6 +104,9 @@ class Reducer {
     bool nesterov = false, first = false, maximize = false;
   };
   std::vector<BucketStep> steps_;
+  std::vector<at::Tensor> post_bcast_;
+  std::vector<std::shared_ptr<RcclWork>> post_works_;
+  int64_t post_issued_ = 0;
   hipStream_t step_stream_ = nullptr;
   hipEvent_t step_done_ = nullptr;
   int64_t stepped_now_ = 0, stepped_last_ = 0;

@@ -32,14 +32,18 @@ SCRIPT = textwrap.dedent(
           for _ in range(5)]
     ys = [torch.randint(0, 10, (32,), device="cuda", generator=g) for _ in range(5)]
 
-    def make(overlap):
+    MODE = os.environ["CDP_TEST_MODE"]  # the variant run: "overlap", "early" or "both"
+
+    def make(variant):
         torch.manual_seed(0)
         model = cdp.DistributedDataParallel(cdp.VGG11().cuda())
         opt = cdp.SGD(model.parameters(), lr=0.05, momentum=0.9, weight_decay=1e-4)
         ctr = torch.zeros(1, dtype=torch.int64, device="cuda")
         opt.advance_each_step(ctr)
-        if overlap:
+        if variant and MODE in ("overlap", "both"):
             model.overlap_optimizer(opt)
+        if variant and MODE in ("early", "both"):
+            model.early_buffer_broadcast(opt)
         return model, opt, ctr
 
     runs = {k: make(k) for k in (False, True)}
@@ -53,7 +57,7 @@ SCRIPT = textwrap.dedent(
         return loss
 
     def state(model, opt):
-        ps = [p.detach().clone() for p in model.parameters()]
+        ps = [p.detach().clone() for p in model.parameters()] + [b.detach().clone() for b in model.buffers()]
         ms = [opt.state[p]["momentum_buffer"].detach().clone() for p in model.parameters()]
         return ps, ms
 
@@ -71,7 +75,12 @@ SCRIPT = textwrap.dedent(
         same(state(*runs[False][:2]), state(*runs[True][:2]), f"eager step {step}")
     m1 = runs[True][0]
     nb = m1.reducer.num_buckets
-    assert m1._get_ddp_logging_data()["overlapped_step_buckets"] == nb >= 2, (nb, m1._get_ddp_logging_data())
+    if MODE in ("overlap", "both"):
+        assert m1._get_ddp_logging_data()["overlapped_step_buckets"] == nb >= 2, (nb, m1._get_ddp_logging_data())
+    if MODE in ("early", "both"):
+        # every synced backward issued the broadcast (the next forward took it instead of its own)
+        assert m1._get_ddp_logging_data()["early_buffer_broadcast"]
+        assert m1.reducer.take_post_issued() == len(list(m1._buffers_arena.flats())) > 0
     assert runs[True][0]._get_ddp_logging_data()["rebuilt_buckets"]
     assert int(runs[False][2]) == 20 and int(runs[True][2]) == 20
 
@@ -110,9 +119,13 @@ def _free_port():
     return p
 
 
-def test_overlapped_step_is_bitwise_the_end_of_step_sgd():
+@pytest.mark.parametrize("mode", ["overlap", "early", "both"])
+def test_overlapped_step_is_bitwise_the_end_of_step_sgd(mode):
+    """mode: the variant run overlaps the SGD with the buckets (overlap), broadcasts the BN buffers
+    behind the last bucket joined after the SGD (early: DistributedDataParallel.early_buffer_broadcast;
+    in the modelled mode the one rank's broadcasts are timed delays on the comm stream), or both."""
     env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()), RANK="0", WORLD_SIZE="1",
-               LOCAL_RANK="0")
+               LOCAL_RANK="0", CDP_TEST_MODE=mode)
     repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     env["PYTHONPATH"] = repo + os.pathsep + env.get("PYTHONPATH", "")
     r = subprocess.run([sys.executable, "-c", SCRIPT], env=env, capture_output=True, text=True, timeout=300)
