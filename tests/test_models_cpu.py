@@ -117,3 +117,19 @@ def test_resnet18_forward_backward():
     out = m(torch.randn(2, 3, 32, 32))
     out.sum().backward()
     assert m.conv1.weight.grad is not None
+
+
+def test_sgd_post_step_joins_run_once_per_step():
+    """SGD.add_post_step_join: the hook DistributedDataParallel.early_buffer_broadcast joins its
+    end-of-backward broadcast through runs after every step, once, and registers only once."""
+    lin = nn.Linear(4, 3)
+    opt = cdp.SGD(lin.parameters(), lr=0.1, momentum=0.9)
+    calls = []
+    fn = lambda: calls.append(len(calls))  # noqa: E731
+    opt.add_post_step_join(fn)
+    opt.add_post_step_join(fn)
+    for _ in range(3):
+        opt.zero_grad()
+        lin(torch.randn(2, 4)).sum().backward()
+        opt.step()
+    assert calls == [0, 1, 2]
