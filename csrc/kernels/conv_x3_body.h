@@ -57,11 +57,16 @@ __device__ __forceinline__ u32x4 pack8(const float (&v)[8]) {
 }
 
 // LDS of one workgroup (bf16 elements): two stages of NP planes of A and B, at least the epilogue's
-// scratch (conv_epilogue.h; only the one-plane 64 x 64 tile needs more than its stages)
+// scratch (conv_epilogue.h; only the one-plane 64 x 64 tile needs more than its stages), then
+// (f16x2) the reciprocal row scales of both operands, BM + BN floats that alias nothing
 template <int BM, int BN, int NP>
-constexpr int conv_x3_smem_elems() {
+constexpr int conv_x3_scales_at() {
   return 2 * NP * (BM + BN) * LDH > 2 * epi_lds_floats<BM, BN>() ? 2 * NP * (BM + BN) * LDH
                                                                   : 2 * epi_lds_floats<BM, BN>();
+}
+template <int BM, int BN, int NP>
+constexpr int conv_x3_smem_elems() {
+  return conv_x3_scales_at<BM, BN, NP>() + (NP == 2 ? 2 * (BM + BN) : 0);
 }
 
 // The kernel body as a device function: `smem` holds conv_x3_smem_elems() bf16 (the caller's one
@@ -407,10 +412,26 @@ __device__ __forceinline__ void conv_x3_body(const ConvGemmParams& p, __bf16* __
   // Software pipeline, one barrier per K-tile: while the MFMAs consume stage t&1, tile t+1
   // (loaded into registers one iteration earlier) is split into stage (t+1)&1 and tile t+2 is
   // being fetched into the other register set.
+  // f16x2: each row's reciprocal scale goes to its own LDS slot now, so the epilogue reads them
+  // without a barrier of its own (the main loop's first barrier publishes them; a tile-less
+  // split slice has one below). The threads with kq == 0 hold the scales of their loader rows.
+  float* s_ia = reinterpret_cast<float*>(smem + conv_x3_scales_at<BM, BN, NP>());
+  float* s_ib = s_ia + BM;
+  auto publish_scales = [&]() {
+    if constexpr (NP == 2) {
+      if ((tid & 3) == 0) {
+#pragma unroll
+        for (int i = 0; i < A_LD; ++i) s_ia[rrow + RS * i] = 1.f / sa_r[i];
+#pragma unroll
+        for (int i = 0; i < B_LD; ++i) s_ib[rrow + RS * i] = 1.f / sb_r[i];
+      }
+    }
+  };
   if (kt_begin < kt_end) {
     load_tile(kt_begin, va0, vb0, true);
     load_tile(kt_begin + 1, va1, vb1, kt_begin + 1 < kt_end);
     finish_scales();
+    publish_scales();
     store_tile(va0, vb0, smem);
     __syncthreads();
     int kt = kt_begin;
@@ -429,22 +450,13 @@ __device__ __forceinline__ void conv_x3_body(const ConvGemmParams& p, __bf16* __
     if (kt < kt_end) compute(smem);  // odd tile count: the last tile sits in stage 0
   } else {  // no K-tiles: the (zero) accumulators still get unscaled
     finish_scales();
+    publish_scales();
+    __syncthreads();
   }
 
   if constexpr (NP == 2) {
-    // undo the row scales (exact: powers of two). Each row's reciprocal goes through LDS (the
-    // stages are free now; past conv_tile_stats' WM x BN floats): the threads with kq == 0 hold the
-    // scales of their loader rows, a lane's accumulators span 16 x TM rows and TN columns.
-    float* s_ia = reinterpret_cast<float*>(smem) + WM * BN;
-    float* s_ib = s_ia + BM;
-    __syncthreads();
-    if ((tid & 3) == 0) {
-#pragma unroll
-      for (int i = 0; i < A_LD; ++i) s_ia[rrow + RS * i] = 1.f / sa_r[i];
-#pragma unroll
-      for (int i = 0; i < B_LD; ++i) s_ib[rrow + RS * i] = 1.f / sb_r[i];
-    }
-    __syncthreads();
+    // undo the row scales (exact: powers of two); a lane's accumulators span 16 x TM rows and TN
+    // columns, their reciprocals published before the main loop's first barrier
 #pragma unroll
     for (int b = 0; b < TN; ++b) {
       const float ib = s_ib[wn * (BN / 2) + b * 32 + l32];
