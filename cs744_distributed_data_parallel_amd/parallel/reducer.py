@@ -381,6 +381,10 @@ class GradReducer:
 
     def set_bucket_steps(self, steps):
         """Register this backward's per-bucket SGD launches (``SGD.bucket_steps``); None clears."""
+        if not self.native:  # the Python twin runs no bucket steps (can_step_buckets is False)
+            if steps:
+                raise RuntimeError("per-bucket optimizer steps need the native reducer")
+            return
         self._impl.clear_bucket_steps()
         for b, kw in enumerate(steps or []):
             self._impl.set_bucket_step(b, **kw)
