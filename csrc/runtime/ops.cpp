@@ -129,6 +129,10 @@ std::atomic<long long>& slot_memsets() {
   return n;
 }
 
+template <class Fresh>
+at::Tensor alloc_slots_impl(SlotPool& P, long long n, const at::TensorOptions& opts, hipStream_t st,
+                            hipStreamCaptureStatus cs, unsigned long long id, Fresh& fresh);
+
 at::Tensor alloc_slots(long long n, const at::Tensor& like, hipStream_t st) {
   static std::mutex mu;
   static std::unordered_map<int, SlotPool> pools;
@@ -145,6 +149,21 @@ at::Tensor alloc_slots(long long n, const at::Tensor& like, hipStream_t st) {
   hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
   unsigned long long id = 0;
   TORCH_CHECK(hipStreamGetCaptureInfo(st, &cs, &id) == hipSuccess, "act max slots: capture query failed");
+  static const bool trace = [] {
+    const char* e = std::getenv("CDP_SLOT_TRACE");
+    return e && e[0] == '1';
+  }();
+  if (trace) {
+    at::Tensor v = alloc_slots_impl(P, n, opts, st, cs, id, fresh);
+    std::fprintf(stderr, "[slots] cap=%d id=%llu st=%p ptr=%p n=%lld\n", (int)cs, id, (void*)st, v.data_ptr(), n);
+    return v;
+  }
+  return alloc_slots_impl(P, n, opts, st, cs, id, fresh);
+}
+
+template <class Fresh>
+at::Tensor alloc_slots_impl(SlotPool& P, long long n, const at::TensorOptions& opts, hipStream_t st,
+                            hipStreamCaptureStatus cs, unsigned long long id, Fresh& fresh) {
   if (cs == hipStreamCaptureStatusActive && id != P.cap_id && !P.cap_keep.empty()) {
     P.cap_keep.clear();  // a new capture: the earlier ones have ended (their pools keep the blocks)
     P.cap_cur = at::Tensor();

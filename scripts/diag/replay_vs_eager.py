@@ -108,7 +108,9 @@ for _ in range(4):
 cmp("eager")
 xb.copy_(xs[k % 3]); yb.copy_(ys[k % 3]); k += 1
 body(*E)
+print("=== capture G", flush=True)
 gr, lo = capture(*G)  # its side-stream warmup ran the same step
+print("=== captured", flush=True)
 cmp("after capture")
 held = []
 if grab:
@@ -130,6 +132,7 @@ if second:
     print("captured a second model", flush=True)
 for i in range(12):
     xb.copy_(xs[k % 3]); yb.copy_(ys[k % 3]); k += 1
+    print(f"=== step {i}: E", flush=True)
     if ework == "step":
         le = body(*E).item()
     elif ework == "fwd":
