@@ -266,6 +266,8 @@ void augment_launch(const unsigned char* imgs, const long long* idx, long long i
                     unsigned long long seed, float* out, hipStream_t st, long long nbatches = 0,
                     const long long* labels = nullptr, long long* labels_out = nullptr);
 // zeros into the NHWC dX pixels of the sub-pixel parity classes set in mask (bit 2 ph + pw)
+// p[0 .. n) = v as a kernel
+void fill_u32_launch(unsigned* p, long long n, unsigned v, hipStream_t st);
 void subpixel_zero_launch(float* dx, int N, int H, int W, int C, int mask, hipStream_t st);
 void counter_inc_launch(long long* c, hipStream_t st);
 void wtrans_launch(const float* w, float* wt, int Co, int T, int Ci, hipStream_t st);

@@ -1020,6 +1020,17 @@ void subpixel_zero_launch(float* dx, int N, int H, int W, int C, int mask, hipSt
   hipLaunchKernelGGL(subpixel_zero_kernel, dim3(grid_for(n4)), dim3(256), 0, st, dx, N, H, W, C / 4, mask,
                      make_fastdiv(C / 4), make_fastdiv(W));
 }
+// Zero-fill as a kernel (act-max slot chunks, ops.cpp alloc_slots): a kernel node of a captured
+// graph is ordered like every other kernel of the step
+__global__ __launch_bounds__(256) void fill_u32_kernel(unsigned* __restrict__ p, long long n, unsigned v) {
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x)
+    p[i] = v;
+}
+void fill_u32_launch(unsigned* p, long long n, unsigned v, hipStream_t st) {
+  if (n <= 0) return;
+  const long long blocks = std::min<long long>(1024, (n + 255) / 256);
+  hipLaunchKernelGGL(fill_u32_kernel, dim3((unsigned)blocks), dim3(256), 0, st, p, n, v);
+}
 void counter_inc_launch(long long* c, hipStream_t st) {
   hipLaunchKernelGGL(counter_inc_kernel, dim3(1), dim3(1), 0, st, c);
 }

@@ -92,11 +92,11 @@ int split_planes() { return conv_gemm_mode() == 2 ? 1 : conv_gemm_mode() == 3 ? 
 // ---------------------------------------------------------------- act max slots
 // An activation's per-image / per-channel |max| slots (ActMaxOut, kernels.h) must start at zero:
 // its producer atomically maxes into them. They are views into chunks of device memory zeroed by
-// ONE memset per chunk, not per producer:
+// ONE fill kernel per chunk, not per producer:
 //  * eager: a ring of chunks; the current chunk is bumped through, and a chunk is re-zeroed and
 //    reused only once no slot view of it is alive (its storage is then held by the ring alone);
 //  * inside a hipGraph capture: every capture takes fresh chunks (from the graph's memory pool,
-//    kept alive with it) whose memset is captured, so each replay re-zeroes them before its
+//    kept alive with it) whose zero-fill kernel is captured, so each replay re-zeroes them before its
 //    producers run.
 // Everything is ordered on the current stream, like the caching allocator's reuse; a chunk taken up
 // on another stream than its last allocating stream (its memset and producers) first makes the new
@@ -104,7 +104,7 @@ int split_planes() { return conv_gemm_mode() == 2 ? 1 : conv_gemm_mode() == 3 ? 
 // before its next work (the consumer GEMMs of this runtime run on the producer's stream); a caller
 // reading slots on another stream must keep the slot tensor alive until that read has completed.
 constexpr long long kSlotChunk = 1LL << 16;     // int32 slots per eager chunk (256 KB)
-constexpr long long kCapSlotChunk = 1LL << 18;  // ... per captured chunk (1 MB: one memset node for a VGG-11 step)
+constexpr long long kCapSlotChunk = 1LL << 18;  // ... per captured chunk (1 MB: one fill node for a VGG-11 step)
 struct SlotPool {
   std::vector<at::Tensor> ring;
   std::vector<long long> used;
@@ -140,9 +140,12 @@ at::Tensor alloc_slots(long long n, const at::Tensor& like, hipStream_t st) {
   n = (n + 63) / 64 * 64;  // 256-B aligned views
   SlotPool& P = pools[like.get_device()];
   const at::TensorOptions opts = like.options().dtype(at::kInt);
+  // Chunks are zeroed by a KERNEL, not hipMemsetAsync: a captured memset node was measured to race
+  // with the step's first producers when other work ran between replays (the replayed step drifted
+  // from its eager twin; with the fill kernel it is bitwise equal, scripts/diag/replay_vs_eager.py)
   auto fresh = [&](long long size) {
     at::Tensor b = at::empty({size}, opts);
-    TORCH_CHECK(hipMemsetAsync(b.data_ptr(), 0, (size_t)size * 4, st) == hipSuccess, "act max slots: memset failed");
+    fill_u32_launch(reinterpret_cast<unsigned*>(b.data_ptr<int>()), size, 0u, st);
     slot_memsets().fetch_add(1, std::memory_order_relaxed);
     return b;
   };
@@ -211,8 +214,7 @@ at::Tensor alloc_slots_impl(SlotPool& P, long long n, const at::TensorOptions& o
       pick = (int)P.ring.size() - 1;
     } else {
       order_after(pick);  // the chunk's last readers finish before the re-zeroing
-      TORCH_CHECK(hipMemsetAsync(P.ring[pick].data_ptr(), 0, (size_t)P.ring[pick].numel() * 4, st) == hipSuccess,
-                  "act max slots: memset failed");
+      fill_u32_launch(reinterpret_cast<unsigned*>(P.ring[pick].data_ptr<int>()), P.ring[pick].numel(), 0u, st);
       slot_memsets().fetch_add(1, std::memory_order_relaxed);
       P.used[pick] = 0;
     }

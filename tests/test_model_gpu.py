@@ -327,3 +327,55 @@ def test_vgg11_every_gradient_lands_in_its_arena_slot(batch):
         bad = [n for n, p in model.named_parameters() if p.grad.data_ptr() != views[p._cdp_index].data_ptr()]
         assert not bad, bad
         opt.step()
+
+
+def test_replayed_step_matches_eager_with_other_work_between():
+    """A captured VGG-11 step replays bitwise like the same step run eagerly, also when another model
+    trains eagerly between the replays. (With the act-max slot chunks zeroed by a captured
+    hipMemsetAsync node, the replays drifted from their eager twin here -- loss 0.881 vs 1.388 by the
+    second step; the chunks are zeroed by a fill kernel now. scripts/diag/replay_vs_eager.py)"""
+    import cs744_distributed_data_parallel_amd as cdp
+
+    crit = cdp.CrossEntropyLoss()
+    g = torch.Generator(device="cuda").manual_seed(1)
+    xs = [torch.randn(32, 3, 32, 32, device="cuda", generator=g).contiguous(memory_format=torch.channels_last)
+          for _ in range(3)]
+    ys = [torch.randint(0, 10, (32,), device="cuda", generator=g) for _ in range(3)]
+    xb, yb = torch.empty_like(xs[0]), torch.empty_like(ys[0])
+
+    def make():
+        torch.manual_seed(0)
+        m = cdp.VGG11().cuda()
+        return m, cdp.SGD(m.parameters(), lr=0.01, momentum=0.9, weight_decay=1e-4)
+
+    def body(m, o):
+        o.zero_grad()
+        loss = crit(m(xb), yb)
+        loss.backward()
+        o.step()
+        return loss
+
+    E, G = make(), make()
+    k = 0
+    for _ in range(4):
+        xb.copy_(xs[k % 3]); yb.copy_(ys[k % 3]); k += 1
+        body(*E); body(*G)
+    xb.copy_(xs[k % 3]); yb.copy_(ys[k % 3]); k += 1
+    body(*E)
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        body(*G)
+    torch.cuda.current_stream().wait_stream(s)
+    gr = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(gr):
+        lo = body(*G)
+    torch.cuda.synchronize()
+    for i in range(6):
+        xb.copy_(xs[k % 3]); yb.copy_(ys[k % 3]); k += 1
+        le = body(*E).item()
+        gr.replay()
+        torch.cuda.synchronize()
+        assert lo.item() == le, (i, lo.item(), le)
+        for (n, a), b in zip(E[0].named_parameters(), G[0].parameters()):
+            assert torch.equal(a, b), (i, n)
