@@ -266,6 +266,8 @@ void augment_launch(const unsigned char* imgs, const long long* idx, long long i
                     unsigned long long seed, float* out, hipStream_t st, long long nbatches = 0,
                     const long long* labels = nullptr, long long* labels_out = nullptr);
 // zeros into the NHWC dX pixels of the sub-pixel parity classes set in mask (bit 2 ph + pw)
+// dst[0 .. bytes) = src[0 .. bytes) as a kernel (16-B accesses when both pointers and bytes allow)
+void copy_bytes_launch(void* dst, const void* src, long long bytes, hipStream_t st);
 // p[0 .. n) = v as a kernel
 void fill_u32_launch(unsigned* p, long long n, unsigned v, hipStream_t st);
 void subpixel_zero_launch(float* dx, int N, int H, int W, int C, int mask, hipStream_t st);

@@ -1031,6 +1031,30 @@ void fill_u32_launch(unsigned* p, long long n, unsigned v, hipStream_t st) {
   const long long blocks = std::min<long long>(1024, (n + 255) / 256);
   hipLaunchKernelGGL(fill_u32_kernel, dim3((unsigned)blocks), dim3(256), 0, st, p, n, v);
 }
+// Device-to-device copy as a kernel (the root's own block of the grouped gather / scatter): inside a
+// captured step a kernel node is ordered like the collectives around it (a captured memset node was
+// measured to race, see fill_u32_kernel)
+__global__ __launch_bounds__(256) void copy16_kernel(uint4* __restrict__ d, const uint4* __restrict__ s, long long n16) {
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += (long long)gridDim.x * blockDim.x)
+    d[i] = s[i];
+}
+__global__ __launch_bounds__(256) void copy1_kernel(unsigned char* __restrict__ d, const unsigned char* __restrict__ s,
+                                                    long long n) {
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x)
+    d[i] = s[i];
+}
+void copy_bytes_launch(void* dst, const void* src, long long bytes, hipStream_t st) {
+  if (bytes <= 0) return;
+  const bool wide = ((reinterpret_cast<uintptr_t>(dst) | reinterpret_cast<uintptr_t>(src) | (uintptr_t)bytes) & 15) == 0;
+  const long long n = wide ? bytes / 16 : bytes;
+  const long long blocks = std::max<long long>(1, std::min<long long>(2048, (n + 255) / 256));
+  if (wide)
+    hipLaunchKernelGGL(copy16_kernel, dim3((unsigned)blocks), dim3(256), 0, st, static_cast<uint4*>(dst),
+                       static_cast<const uint4*>(src), n);
+  else
+    hipLaunchKernelGGL(copy1_kernel, dim3((unsigned)blocks), dim3(256), 0, st, static_cast<unsigned char*>(dst),
+                       static_cast<const unsigned char*>(src), n);
+}
 void counter_inc_launch(long long* c, hipStream_t st) {
   hipLaunchKernelGGL(counter_inc_kernel, dim3(1), dim3(1), 0, st, c);
 }

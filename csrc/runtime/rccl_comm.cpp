@@ -376,7 +376,7 @@ std::shared_ptr<RcclWork> RcclComm::gather(at::Tensor t, std::vector<at::Tensor>
       check_tensor(outs[r]);
       TORCH_CHECK(outs[r].numel() == t.numel(), "gather: output size mismatch");
       keep.push_back(outs[r]);
-      if (r == root) HIP_CHECK(hipMemcpyAsync(outs[r].data_ptr(), t.data_ptr(), bytes, hipMemcpyDeviceToDevice, stream_));
+      if (r == root) copy_bytes_launch(outs[r].data_ptr(), t.data_ptr(), (long long)bytes, stream_);
       else RCCL_CHECK(ncclRecv(outs[r].data_ptr(), t.numel(), to_nccl(t.scalar_type()), r, comm_, stream_));
     }
   } else {
@@ -399,7 +399,7 @@ std::shared_ptr<RcclWork> RcclComm::scatter(at::Tensor t, std::vector<at::Tensor
       check_tensor(ins[r]);
       TORCH_CHECK(ins[r].numel() == t.numel(), "scatter: input size mismatch");
       keep.push_back(ins[r]);
-      if (r == root) HIP_CHECK(hipMemcpyAsync(t.data_ptr(), ins[r].data_ptr(), bytes, hipMemcpyDeviceToDevice, stream_));
+      if (r == root) copy_bytes_launch(t.data_ptr(), ins[r].data_ptr(), (long long)bytes, stream_);
       else RCCL_CHECK(ncclSend(ins[r].data_ptr(), t.numel(), to_nccl(t.scalar_type()), r, comm_, stream_));
     }
   } else {
