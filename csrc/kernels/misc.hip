@@ -1026,8 +1026,18 @@ __global__ __launch_bounds__(256) void fill_u32_kernel(unsigned* __restrict__ p,
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x)
     p[i] = v;
 }
+__global__ __launch_bounds__(256) void fill_u32x4_kernel(uint4* __restrict__ p, long long n4, unsigned v) {
+  const uint4 q = make_uint4(v, v, v, v);
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (long long)gridDim.x * blockDim.x)
+    p[i] = q;
+}
 void fill_u32_launch(unsigned* p, long long n, unsigned v, hipStream_t st) {
   if (n <= 0) return;
+  if ((reinterpret_cast<uintptr_t>(p) & 15) == 0 && (n & 3) == 0) {  // 16-B stores (slot chunks: 256-B multiples)
+    const long long n4 = n / 4, blocks = std::min<long long>(512, (n4 + 255) / 256);
+    hipLaunchKernelGGL(fill_u32x4_kernel, dim3((unsigned)blocks), dim3(256), 0, st, reinterpret_cast<uint4*>(p), n4, v);
+    return;
+  }
   const long long blocks = std::min<long long>(1024, (n + 255) / 256);
   hipLaunchKernelGGL(fill_u32_kernel, dim3((unsigned)blocks), dim3(256), 0, st, p, n, v);
 }

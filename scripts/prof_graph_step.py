@@ -14,7 +14,8 @@ busy = 0
 print("| # | kernel | us | gap us |\n|---|---|---|---|")
 for i, r in enumerate(step):
     s, e = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
-    nm = r["Kernel_Name"].replace("void ", "").replace("cdp::", "").split("(")[0][:60]
+    nm = r["Kernel_Name"].replace("(anonymous namespace)::", "").replace("void ", "").replace("cdp::", "")
+    nm = nm.split("(")[0][:60]
     print(f"| {i} | `{nm}` | {(e - s) / 1e3:.1f} | {(s - prev_end) / 1e3:.1f} |")
     busy += e - s
     prev_end = max(prev_end, e)
