@@ -168,10 +168,8 @@ void slab_sum_strided_launch(const float* slab, int S, long long n_src, int src_
 
 // stem.hip: 3x3 / stride 1 / pad 1 convs with Cin <= 4 and 64 outputs (exact fp32 MFMA)
 bool stem_ok(int Cin, int KH, int KW, int stride, int pad, int Co);
-// zero / zero_n (optional, zero_n a multiple of 4, zero 16-B aligned): a slot chunk the kernel also
-// zeroes (alloc_slots' deferred zeroing, ops.cpp)
 void stem_fwd_launch(const float* x, const float* w, const float* bias, float* y, float* part, int N, int H, int W,
-                     int Cin, int Co, hipStream_t st, unsigned* zero = nullptr, long long zero_n = 0);
+                     int Cin, int Co, hipStream_t st);
 int stem_wgrad_blocks(int N, int H, int W);
 // dW partials [nblk][64][36] with the pool(2x2)/ReLU/BatchNorm(training) backward applied on the fly;
 // Co = 64, even H and W

@@ -20,7 +20,6 @@
 #include "x3_common.h"
 
 #include <algorithm>
-#include <stdexcept>
 
 namespace cdp {
 
@@ -108,12 +107,7 @@ __device__ __forceinline__ void stem_y_mfma(const float (&lo)[9][2], const float
 // y = conv(x) + b (when y != nullptr) and the per-256-row BatchNorm partials (mean, M2).
 __global__ __launch_bounds__(256, 2) void stem_fwd_kernel(const float* __restrict__ x, const float* __restrict__ w,
                                                        const float* __restrict__ bias, float* __restrict__ y,
-                                                       float* __restrict__ part, int N, int H, int W, int Cin,
-                                                       uint4* __restrict__ zero, long long zero_n4) {
-  // a fresh act-max slot chunk of the step, zeroed here instead of by a launch of its own (its
-  // producers run after this kernel)
-  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < zero_n4; i += (long long)gridDim.x * 256)
-    zero[i] = make_uint4(0u, 0u, 0u, 0u);
+                                                       float* __restrict__ part, int N, int H, int W, int Cin) {
   constexpr int Co = 64;  // one block column: row stride and output offsets are compile-time
   __shared__ float red[4][64];
   __shared__ float wl[64][37];
@@ -342,13 +336,11 @@ bool stem_ok(int Cin, int KH, int KW, int stride, int pad, int Co) {
 }
 
 void stem_fwd_launch(const float* x, const float* w, const float* bias, float* y, float* part, int N, int H, int W,
-                     int Cin, int Co, hipStream_t st, unsigned* zero, long long zero_n) {
+                     int Cin, int Co, hipStream_t st) {
   const long long M = (long long)N * H * W;
   (void)Co;  // == 64 (stem_ok)
-  if (zero && ((zero_n & 3) || (reinterpret_cast<uintptr_t>(zero) & 15)))
-    throw std::runtime_error("stem_fwd: the chunk to zero must be 16-B aligned, a multiple of 4 slots");
   hipLaunchKernelGGL(stem_fwd_kernel, dim3((unsigned)((M + 255) / 256)), dim3(256), 0, st, x, w, bias, y, part, N, H,
-                     W, Cin, reinterpret_cast<uint4*>(zero), zero ? zero_n / 4 : 0LL);
+                     W, Cin);
 }
 
 int stem_wgrad_blocks(int N, int H, int W) {

@@ -129,19 +129,11 @@ std::atomic<long long>& slot_memsets() {
   return n;
 }
 
-// A chunk zeroing handed to the caller (alloc_slots' `defer`): the caller's next kernel on the same
-// stream zeroes [ptr, ptr + n) before any producer of the returned slots runs (the RGB stem does it
-// inside its own launch: one dispatch fewer at the head of every step)
-struct SlotZero {
-  unsigned* ptr = nullptr;
-  long long n = 0;
-};
-
-template <class Fresh, class Zero>
+template <class Fresh>
 at::Tensor alloc_slots_impl(SlotPool& P, long long n, const at::TensorOptions& opts, hipStream_t st,
-                            hipStreamCaptureStatus cs, unsigned long long id, Fresh& fresh, Zero& zero);
+                            hipStreamCaptureStatus cs, unsigned long long id, Fresh& fresh);
 
-at::Tensor alloc_slots(long long n, const at::Tensor& like, hipStream_t st, SlotZero* defer = nullptr) {
+at::Tensor alloc_slots(long long n, const at::Tensor& like, hipStream_t st) {
   static std::mutex mu;
   static std::unordered_map<int, SlotPool> pools;
   std::lock_guard<std::mutex> lk(mu);
@@ -151,19 +143,10 @@ at::Tensor alloc_slots(long long n, const at::Tensor& like, hipStream_t st, Slot
   // Chunks are zeroed by a KERNEL, not hipMemsetAsync: a captured memset node was measured to race
   // with the step's first producers when other work ran between replays (the replayed step drifted
   // from its eager twin; with the fill kernel it is bitwise equal, scripts/diag/replay_vs_eager.py)
-  auto zero = [&](const at::Tensor& b) {
-    unsigned* ptr = reinterpret_cast<unsigned*>(b.data_ptr<int>());
-    if (defer) {
-      TORCH_CHECK(defer->ptr == nullptr, "act max slots: one deferred zeroing per call");
-      *defer = SlotZero{ptr, b.numel()};
-    } else {
-      fill_u32_launch(ptr, b.numel(), 0u, st);
-    }
-    slot_memsets().fetch_add(1, std::memory_order_relaxed);
-  };
   auto fresh = [&](long long size) {
     at::Tensor b = at::empty({size}, opts);
-    zero(b);
+    fill_u32_launch(reinterpret_cast<unsigned*>(b.data_ptr<int>()), size, 0u, st);
+    slot_memsets().fetch_add(1, std::memory_order_relaxed);
     return b;
   };
   hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
@@ -174,16 +157,16 @@ at::Tensor alloc_slots(long long n, const at::Tensor& like, hipStream_t st, Slot
     return e && e[0] == '1';
   }();
   if (trace) {
-    at::Tensor v = alloc_slots_impl(P, n, opts, st, cs, id, fresh, zero);
+    at::Tensor v = alloc_slots_impl(P, n, opts, st, cs, id, fresh);
     std::fprintf(stderr, "[slots] cap=%d id=%llu st=%p ptr=%p n=%lld\n", (int)cs, id, (void*)st, v.data_ptr(), n);
     return v;
   }
-  return alloc_slots_impl(P, n, opts, st, cs, id, fresh, zero);
+  return alloc_slots_impl(P, n, opts, st, cs, id, fresh);
 }
 
-template <class Fresh, class Zero>
+template <class Fresh>
 at::Tensor alloc_slots_impl(SlotPool& P, long long n, const at::TensorOptions& opts, hipStream_t st,
-                            hipStreamCaptureStatus cs, unsigned long long id, Fresh& fresh, Zero& zero) {
+                            hipStreamCaptureStatus cs, unsigned long long id, Fresh& fresh) {
   if (cs == hipStreamCaptureStatusActive && id != P.cap_id && !P.cap_keep.empty()) {
     P.cap_keep.clear();  // a new capture: the earlier ones have ended (their pools keep the blocks)
     P.cap_cur = at::Tensor();
@@ -231,7 +214,8 @@ at::Tensor alloc_slots_impl(SlotPool& P, long long n, const at::TensorOptions& o
       pick = (int)P.ring.size() - 1;
     } else {
       order_after(pick);  // the chunk's last readers finish before the re-zeroing
-      zero(P.ring[pick]);
+      fill_u32_launch(reinterpret_cast<unsigned*>(P.ring[pick].data_ptr<int>()), P.ring[pick].numel(), 0u, st);
+      slot_memsets().fetch_add(1, std::memory_order_relaxed);
       P.used[pick] = 0;
     }
     P.cur = pick;
@@ -257,8 +241,8 @@ ActMaxOut act_out(const at::Tensor& s, long long N) {
   return ActMaxOut{b, b + N};
 }
 // Fresh zeroed act max slots for an activation of `like`'s images / channels (f16x2 engine only).
-at::Tensor new_act_max(long long N, long long C, const at::Tensor& like, hipStream_t st, SlotZero* defer = nullptr) {
-  return alloc_slots(act_max_elems(N, C), like, st, defer);
+at::Tensor new_act_max(long long N, long long C, const at::Tensor& like, hipStream_t st) {
+  return alloc_slots(act_max_elems(N, C), like, st);
 }
 
 // The act max of an f16x2 GEMM activation operand t (NHWC channels_last 4-D or contiguous 2-D):
@@ -1357,20 +1341,9 @@ std::vector<at::Tensor> stem_bn_act_fwd(const at::Tensor& x_, const at::Tensor& 
   const long long M = (long long)N * H * W;
   const int nparts = (int)((M + 255) / 256);
   at::Tensor part = at::empty({nparts, Co, 2}, opts);
-  at::Tensor out = at::empty({N, Co, pool ? H / 2 : H, pool ? W / 2 : W},
-                             opts.memory_format(at::MemoryFormat::ChannelsLast));
-  // the output's act max (the next conv's operand scales, f16x2), taken before the stem launch: a
-  // chunk that needs zeroing (usually the step's first) is zeroed by the stem kernel itself
-  at::Tensor out_amax;
-  ActMaxOut am{nullptr, nullptr};
-  SlotZero z;
-  if (f16x2_mode()) {
-    out_amax = new_act_max(N, Co, out, st, &z);
-    am = act_out(out_amax, N);
-  }
   gemm_log_add("stem_fwd", (long long)N * H * W, Co, 9LL * Cin, 256, 64, 1);
   stem_fwd_launch(x.data_ptr<float>(), w.data_ptr<float>(), fptr(b), y.data_ptr<float>(),
-                  part.data_ptr<float>(), N, H, W, Cin, Co, st, z.ptr, z.n);
+                  part.data_ptr<float>(), N, H, W, Cin, Co, st);
   at::Tensor stats = at::empty({4, Co}, opts);
   long long* nbt = nullptr;
   if (num_batches_tracked.has_value() && num_batches_tracked->defined())
@@ -1382,6 +1355,14 @@ std::vector<at::Tensor> stem_bn_act_fwd(const at::Tensor& x_, const at::Tensor& 
     bn_finalize_launch(part.data_ptr<float>(), nparts, 256, (int)M, Co, fptr(gamma), fptr(beta),
                        fptr_mut(running_mean), fptr_mut(running_var), nbt, (float)momentum, (float)eps,
                        stats.data_ptr<float>(), st);
+  at::Tensor out = at::empty({N, Co, pool ? H / 2 : H, pool ? W / 2 : W},
+                             opts.memory_format(at::MemoryFormat::ChannelsLast));
+  at::Tensor out_amax;  // the output's act max: the next conv's operand scales (f16x2)
+  ActMaxOut am{nullptr, nullptr};
+  if (f16x2_mode()) {
+    out_amax = new_act_max(N, Co, out, st);
+    am = act_out(out_amax, N);
+  }
   if (fused)
     bn_fin_act_launch(part.data_ptr<float>(), nparts, 256, Co, fptr(gamma), fptr(beta), fptr_mut(running_mean),
                       fptr_mut(running_var), nbt, (float)momentum, (float)eps, stats.data_ptr<float>(),
